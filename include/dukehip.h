@@ -1,0 +1,158 @@
+/*
+ * dukehip.h — C-ABI of libdukehip.so, the MI355X-native candidate-pair scoring engine
+ * that replaces Duke 1.2's matching loop behind the sesam-duke-microservice.
+ *
+ * The microservice drives Duke through four contracts; each entry point below replaces
+ * one reference interface (file:line under /root/reference/src/main/java/io/sesam/
+ * dukemicroservice/ unless stated):
+ *
+ *   dk_create        <- `new Processor(config, false)` + `config.setDatabase(db)` +
+ *                       `Processor.setThreads` (App.java:342-344, 463-465); the schema is
+ *                       what ConfigLoader.load builds from the <duke> block (App.java:613-647)
+ *                       with the synthetic ID / ignored properties removed (App.java:309-323).
+ *   dk_upsert        <- `Database.index(Record)` per record + `Database.commit()`
+ *                       (IncrementalLuceneDatabase.java:498-575, 146-165): delete-by-ID then
+ *                       add (:516-517, 578-590), dukeDeleted kept as a flag (:478).
+ *   dk_match         <- `Processor.deduplicate(Collection<Record>)`'s match loop
+ *                       (App.java:1005, 1159): findCandidateMatches
+ *                       (IncrementalDeduplicationLuceneDatabase.java:8-10,
+ *                       IncrementalRecordLinkageLuceneDatabase.java:12-14) with the
+ *                       key-function blocking contract of SURVEY §8a-5, then
+ *                       Processor.compareCandidatesSimple -> compare -> threshold.
+ *   dk_result        <- the MatchListener callbacks (BaseLinkDatabaseMatchListener.java:53-109):
+ *                       entries grouped per query in batch order, candidate order inside.
+ *   dk_compare_rows  <- `Processor.compare(Record, Record)` for one pair.
+ *   dk_set_profiling <- `Processor.setPerformanceProfiling` (App.java:345, 466).
+ *   dk_last_error    <- DukeException / RuntimeException text (App.java:1007-1009).
+ *
+ * Strings cross the boundary as Java chars (UTF-16 code units) or, when every unit of
+ * a column is <= 0xFF, as one byte per unit (width 1).  Plain pointers and sizes only;
+ * the caller owns its buffers and may free them as soon as a call returns.
+ * Every function returns DK_OK (0) or a negative DK_E* code; dk_last_error() then holds
+ * a thread-local message.  Calls on one dk_ctx must be serialised by the caller (the
+ * microservice's per-pipeline ReentrantLock, App.java:96,145,947,1096); distinct ctxs are
+ * independent (one HIP stream each).
+ */
+#ifndef DUKEHIP_H
+#define DUKEHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DK_ABI_VERSION 1
+
+/* status codes */
+#define DK_OK 0
+#define DK_E_INVALID (-1)     /* bad argument / schema */
+#define DK_E_UNSUPPORTED (-2) /* comparator or parameter the GPU path does not implement */
+#define DK_E_NOMEM (-3)
+#define DK_E_DEVICE (-4)      /* HIP runtime error, or no GPU */
+#define DK_E_STATE (-5)       /* call not valid in the ctx's current state */
+
+/* comparators: Duke 1.2 no.priv.garshol.duke.comparators.* class -> opcode */
+#define DK_CMP_NONE 0                 /* property without comparator: PropertyImpl -> 0.5 */
+#define DK_CMP_LEVENSHTEIN 1          /* comparators.Levenshtein */
+#define DK_CMP_JAROWINKLER 2          /* comparators.JaroWinkler */
+#define DK_CMP_QGRAM 3                /* comparators.QGramComparator */
+#define DK_CMP_EXACT 4                /* comparators.ExactComparator */
+#define DK_CMP_NUMERIC 5              /* comparators.NumericComparator */
+#define DK_CMP_WEIGHTED_LEVENSHTEIN 6 /* comparators.WeightedLevenshtein (reserved) */
+
+#define DK_QGRAM_OVERLAP 0 /* QGramComparator.Formula */
+#define DK_QGRAM_JACCARD 1
+#define DK_QGRAM_DICE 2
+#define DK_QGRAM_BASIC 0 /* QGramComparator.Tokenizer */
+#define DK_QGRAM_POSITIONAL 1
+
+#define DK_MODE_DEDUP 0    /* <Deduplication>: every other record is a candidate */
+#define DK_MODE_LINKAGE 1  /* <RecordLinkage>: candidates only from the other group */
+#define DK_MODE_ALLPAIRS 2 /* Duke InMemoryDatabase: no blocking, all records */
+
+#define DK_KIND_MATCH 1 /* MatchListener.matches */
+#define DK_KIND_MAYBE 2 /* MatchListener.matchesPerhaps */
+
+typedef struct dk_property {
+  int32_t comparator;      /* DK_CMP_* */
+  int32_t qgram_q;         /* QGramComparator.setQ (default 2; 1..4) */
+  int32_t qgram_formula;   /* DK_QGRAM_OVERLAP/JACCARD/DICE */
+  int32_t qgram_tokenizer; /* DK_QGRAM_BASIC/POSITIONAL (POSITIONAL: q <= 3) */
+  double low;              /* <low> */
+  double high;             /* <high> */
+  double min_ratio;        /* NumericComparator.setMinRatio (default 0.0) */
+} dk_property;
+
+typedef struct dk_schema {
+  int32_t nprops;           /* scored properties, in Processor.compare iteration order */
+  const dk_property* props;
+  double threshold;         /* <threshold> */
+  double maybe_threshold;   /* <maybe-threshold>; 0.0 = none (Duke's default) */
+  int32_t mode;             /* DK_MODE_* */
+  int32_t nkeys;            /* key functions (blocking); ignored in ALLPAIRS mode; <= 8 */
+} dk_schema;
+
+/* One property's values for the n records of a batch. */
+typedef struct dk_column {
+  const uint32_t* offsets; /* n+1 offsets, in code units, into units */
+  const void* units;       /* width 1: uint8_t units (<= 0xFF); width 2: uint16_t */
+  int32_t width;           /* 1 or 2 */
+  const uint8_t* present;  /* n flags: 0 = record has no value; NULL = all present */
+} dk_column;
+
+typedef struct dk_batch {
+  uint64_t n;
+  const uint64_t* ident;    /* n: equal <=> same ID property value (Processor.isSameAs) */
+  const uint8_t* group;     /* n: dukeGroupNo (1 or 2); NULL unless LINKAGE */
+  const uint8_t* deleted;   /* n: dukeDeleted == "true"; NULL = none */
+  const dk_column* columns; /* nprops */
+  /* key functions: either keys (nkeys*n, key-function major, equal <=> same key
+   * string) or key_columns (nkeys strings per record, interned exactly by the library) */
+  const uint64_t* keys;
+  const dk_column* key_columns;
+} dk_batch;
+
+typedef struct dk_result {
+  uint64_t nqueries;       /* queries passed to dk_match */
+  const uint64_t* first;   /* nqueries+1: entries of query i are [first[i], first[i+1]) */
+  uint64_t n;              /* match + maybe entries */
+  const uint32_t* query;   /* row of r1 (the query record) */
+  const uint32_t* candidate; /* row of r2 */
+  const double* prob;      /* Processor.compare(r1, r2) */
+  const uint8_t* kind;     /* DK_KIND_MATCH / DK_KIND_MAYBE */
+  uint64_t pairs_scored;   /* Processor.compare calls made (candidates after filters) */
+  uint64_t pairs_generated; /* candidate slots produced by blocking, before filters */
+} dk_result;
+
+typedef struct dk_profile {
+  double ms_index;        /* blocking-table build (sort, segments) */
+  double ms_generate;     /* candidate counting + pair emission */
+  double ms_score;        /* fused scoring kernels (the dominant kernel) */
+  double ms_gather;       /* match compaction sort + device->host copy */
+  double ms_total;        /* wall time of dk_match */
+  uint64_t score_launches;
+  uint64_t pairs_scored;
+  uint64_t pairs_generated;
+  uint64_t score_bytes;   /* algorithmic operand bytes of the scored pairs */
+} dk_profile;
+
+typedef struct dk_ctx dk_ctx;
+
+int dk_create(const dk_schema* schema, int device, dk_ctx** out);
+void dk_destroy(dk_ctx* ctx);
+int dk_upsert(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
+int dk_match(dk_ctx* ctx, const uint32_t* query_rows, uint64_t nq, dk_result** out);
+void dk_free_result(dk_result* result);
+int dk_compare_rows(dk_ctx* ctx, uint32_t r1, uint32_t r2, double* prob);
+uint64_t dk_num_rows(const dk_ctx* ctx);
+int dk_set_profiling(dk_ctx* ctx, int on);
+int dk_get_profile(const dk_ctx* ctx, dk_profile* out);
+int dk_reset_profile(dk_ctx* ctx);
+const char* dk_last_error(void);
+int dk_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

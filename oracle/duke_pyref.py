@@ -1,0 +1,260 @@
+"""Pure-Python restatement of Duke 1.2's scoring path — TEST INFRASTRUCTURE ONLY.
+
+Used only to generate the golden fixtures under tests/golden/ (tests/gen_golden.py) and
+inside tests as a second, independent restatement next to the C oracle
+(oracle/duke_oracle.c).  Nothing in the product imports it.
+
+PARITY UNPINNED against Duke itself: the algorithms live in the third-party jar
+no.priv.garshol.duke:duke:1.2 (/root/reference/pom.xml:32-36), which is absent; the
+reference ships no known-answer tests for this path (src/test/.../AppTest.java:34-37).
+Functions follow the Duke 1.2 sources as recalled.
+
+Strings are sequences of UTF-16 code units (Java ``char``); use :func:`units`.
+"""
+from __future__ import annotations
+
+import math
+import re
+
+LEVENSHTEIN, JAROWINKLER, QGRAM, EXACT, NUMERIC, WEIGHTED_LEVENSHTEIN = 1, 2, 3, 4, 5, 6
+OVERLAP, JACCARD, DICE = 0, 1, 2
+BASIC, POSITIONAL = 0, 1
+
+
+def units(s: str) -> tuple:
+    """Java String -> tuple of UTF-16 code units (surrogate pairs count as two)."""
+    b = s.encode("utf-16-le", "surrogatepass")
+    return tuple(int.from_bytes(b[i:i + 2], "little") for i in range(0, len(b), 2))
+
+
+def compact_distance(s1, s2) -> int:
+    """[Duke 1.2] Levenshtein.compactDistance (cost added to all three neighbours)."""
+    if len(s1) == 0:
+        return len(s2)
+    if len(s2) == 0:
+        return len(s1)
+    maxdist = min(len(s1), len(s2)) // 2
+    m = len(s1)
+    col = [0] * (m + 1)
+    col[0] = 1
+    for i in range(1, m + 1):
+        col[i] = min(col[i - 1], i - 1) + (0 if s1[i - 1] == s2[0] else 1)
+    above = 0
+    for j in range(1, len(s2)):
+        above = j + 1
+        smallest = 2 * m
+        for i in range(1, m + 1):
+            v = min(above, col[i - 1], col[i]) + (0 if s1[i - 1] == s2[j] else 1)
+            col[i - 1] = above
+            above = v
+            smallest = min(smallest, v)
+        col[m] = above
+        if smallest > maxdist:
+            return smallest
+    return above
+
+
+def levenshtein(s1, s2) -> float:
+    """[Duke 1.2] Levenshtein.compare — divides by the SHORTER length."""
+    n, mx = min(len(s1), len(s2)), max(len(s1), len(s2))
+    ratio = n / mx if mx else float("nan")
+    if ratio <= 0.5:
+        return 0.0
+    if n == mx and tuple(s1) == tuple(s2):
+        return 1.0
+    d = min(compact_distance(s1, s2), n)
+    return 1.0 - (d / n)
+
+
+def jarowinkler(s1, s2) -> float:
+    """[Duke 1.2] JaroWinkler.similarity (first match in window, t not halved)."""
+    if tuple(s1) == tuple(s2):
+        return 1.0
+    if len(s1) > len(s2):
+        s1, s2 = s2, s1
+    maxdist = len(s2) // 2
+    c = t = 0
+    prev = -1
+    for i, ch in enumerate(s1):
+        for j in range(max(0, i - maxdist), min(len(s2), i + maxdist)):
+            if s2[j] == ch:
+                c += 1
+                if prev != -1 and j < prev:
+                    t += 1
+                prev = j
+                break
+    if c == 0:
+        return 0.0
+    score = ((c / len(s1)) + (c / len(s2)) + ((c - t) / c)) / 3.0
+    p = 0
+    last = min(4, len(s1))
+    while p < last and s1[p] == s2[p]:
+        p += 1
+    score += (p * (1 - score)) / 10
+    return score
+
+
+def qgrams(s, q, tokenizer=BASIC) -> set:
+    out = set()
+    for ix in range(0, len(s) - q + 1):
+        g = tuple(s[ix:ix + q])
+        out.add((g, ix) if tokenizer == POSITIONAL else g)
+    return out
+
+
+def qgram(s1, s2, q=2, formula=OVERLAP, tokenizer=BASIC) -> float:
+    """[Duke 1.2] QGramComparator.compare + Formula.compute."""
+    if tuple(s1) == tuple(s2):
+        return 1.0
+    g1, g2 = qgrams(s1, q, tokenizer), qgrams(s2, q, tokenizer)
+    if not g1 or not g2:
+        return 0.0
+    common = len(g1 & g2)
+    if formula == JACCARD:
+        return common / (len(g1) + len(g2) - common)
+    if formula == DICE:
+        return (2.0 * common) / (len(g1) + len(g2))
+    return common / min(float(len(g1)), float(len(g2)))
+
+
+def exact(s1, s2) -> float:
+    return 1.0 if tuple(s1) == tuple(s2) else 0.0
+
+
+_DEC = re.compile(r"^[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?[fFdD]?$")
+_HEX = re.compile(r"^([+-]?)0[xX]([0-9a-fA-F]*)(?:\.([0-9a-fA-F]*))?[pP]([+-]?\d+)[fFdD]?$")
+
+
+def parse_java_double(s):
+    """java.lang.Double.parseDouble on code units; None for NumberFormatException."""
+    a, b = 0, len(s)
+    while a < b and s[a] <= 0x20:
+        a += 1
+    while b > a and s[b - 1] <= 0x20:
+        b -= 1
+    if a == b or any(u >= 0x80 for u in s[a:b]):
+        return None
+    t = "".join(chr(u) for u in s[a:b])
+    body = t[1:] if t[:1] in "+-" else t
+    neg = t.startswith("-")
+    if body == "NaN":
+        return float("nan")
+    if body == "Infinity":
+        return -math.inf if neg else math.inf
+    m = _HEX.match(t)
+    if m:
+        ip, fp, ex = m.group(2), m.group(3) or "", m.group(4)
+        if not ip and not fp:
+            return None
+        v = float.fromhex(f"{m.group(1)}0x{ip or '0'}.{fp or '0'}p{ex}")
+        return v
+    if _DEC.match(t):
+        t2 = t[:-1] if t[-1] in "fFdD" else t
+        return float(t2)
+    return None
+
+
+def numeric(s1, s2, min_ratio=0.0) -> float:
+    """[Duke 1.2] NumericComparator.compare."""
+    d1 = parse_java_double(s1)
+    d2 = parse_java_double(s2)
+    if d1 is None or d2 is None:
+        return 0.5
+    if d1 == 0.0 and d2 == 0.0:
+        return 1.0
+    if d2 < d1:
+        d1, d2 = d2, d1
+    try:
+        ratio = d1 / d2
+    except ZeroDivisionError:  # IEEE: x/0 -> +-inf, 0/0 -> nan
+        ratio = math.nan if d1 == 0.0 or d1 != d1 else math.copysign(math.inf, d1) * math.copysign(1.0, d2)
+    if ratio < min_ratio:
+        return 0.0
+    return ratio
+
+
+def java_max(a, b):
+    if a != a:
+        return a
+    if b != b:
+        return b
+    if a == 0.0 and b == 0.0:
+        return b if math.copysign(1.0, a) < 0 else a
+    return a if a >= b else b
+
+
+def compute_bayes(p1, p2):
+    """[Duke 1.2] Utils.computeBayes."""
+    num = p1 * p2
+    den = num + ((1.0 - p1) * (1.0 - p2))
+    if den == 0.0:
+        return math.nan if num == 0.0 else math.copysign(math.inf, num)
+    return num / den
+
+
+def property_compare(prop, v1, v2):
+    """[Duke 1.2] PropertyImpl.compare.  prop: dict(comparator, low, high, ...)."""
+    c = prop["comparator"]
+    if c == LEVENSHTEIN:
+        sim = levenshtein(v1, v2)
+    elif c == JAROWINKLER:
+        sim = jarowinkler(v1, v2)
+    elif c == QGRAM:
+        sim = qgram(v1, v2, prop.get("q", 2), prop.get("formula", OVERLAP), prop.get("tokenizer", BASIC))
+    elif c == EXACT:
+        sim = exact(v1, v2)
+    elif c == NUMERIC:
+        sim = numeric(v1, v2, prop.get("min_ratio", 0.0))
+    else:
+        return 0.5
+    if sim < 0.5:
+        return prop["low"]
+    return ((prop["high"] - 0.5) * (sim * sim)) + 0.5
+
+
+def compare_records(props, r1, r2):
+    """[Duke 1.2] Processor.compare.  r1/r2: list (per property, schema order) of a
+    code-unit tuple or None (no value)."""
+    prob = 0.5
+    for i, prop in enumerate(props):
+        v1, v2 = r1[i], r2[i]
+        if v1 is None or v2 is None:
+            continue
+        high = 0.0
+        if len(v1) and len(v2):
+            high = java_max(high, property_compare(prop, v1, v2))
+        prob = compute_bayes(prob, high)
+    return prob
+
+
+def match(props, records, keys, queries, threshold, maybe=0.0, mode="dedup",
+          idents=None, groups=None, deleted=None):
+    """Processor.deduplicate's match loop with exact-key blocking (SURVEY §8a-5 build
+    contract).  records: list of per-property values; keys: per record list of key
+    strings (tuples).  Returns (list of (q, c, prob, kind), pairs_scored)."""
+    n = len(records)
+    idents = idents if idents is not None else list(range(n))
+    out, scored = [], 0
+    for q in queries:
+        cands = []
+        if mode == "allpairs":
+            cands = list(range(n))
+        else:
+            seen = set()
+            for k in range(len(keys[q])):
+                for c in range(n):
+                    if keys[c][k] == keys[q][k] and c not in seen:
+                        seen.add(c)
+                        cands.append(c)
+        for c in cands:
+            if idents[c] == idents[q] or (deleted and deleted[c]):
+                continue
+            if mode == "linkage" and groups[c] == groups[q]:
+                continue
+            p = compare_records(props, records[q], records[c])
+            scored += 1
+            if p > threshold:
+                out.append((q, c, p, 1))
+            elif maybe != 0.0 and p > maybe:
+                out.append((q, c, p, 2))
+    return out, scored

@@ -1,0 +1,883 @@
+// dk_api.cpp — the C-ABI of libdukehip.so (include/dukehip.h): the device-resident record
+// index (Duke Database), the batch matcher (Processor.deduplicate's match loop) and the
+// result hand-back (MatchListener replay order).  Host-side C++; all per-pair work runs in
+// the gfx950 kernels of dk_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "dk_internal.h"
+
+using namespace dk;
+
+// ----------------------------------------------------------------------------------------
+// errors
+// ----------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      return fail(DK_E_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                  __FILE__, __LINE__);                                               \
+  } while (0)
+
+// ----------------------------------------------------------------------------------------
+// device buffers
+// ----------------------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  // grow to >= nb bytes (x1.5 headroom), preserving the first `keep` bytes
+  hipError_t reserve(size_t nb, size_t keep, hipStream_t s) {
+    if (nb <= bytes) return hipSuccess;
+    size_t cap = std::max(nb, bytes + bytes / 2);
+    cap = (cap + 255) & ~(size_t)255;
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, cap);
+    if (e != hipSuccess) return e;
+    if (keep && p) {
+      e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return e;
+      e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return e;
+    }
+    if (p) (void)hipFree(p);
+    p = q;
+    bytes = cap;
+    return hipSuccess;
+  }
+  template <typename T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t reserve(size_t nb) {
+    if (nb <= bytes) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    size_t cap = std::max(nb, bytes * 2);
+    hipError_t e = hipHostMalloc(&p, cap, hipHostMallocDefault);
+    bytes = e == hipSuccess ? cap : 0;
+    return e;
+  }
+  template <typename T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// ----------------------------------------------------------------------------------------
+// java.lang.Double.parseDouble for NumericComparator values (host side, at index time):
+// String.trim, [+-] then NaN | Infinity | hex 0x..p.. | decimal, optional [fFdD] suffix on
+// the numeric forms; correctly rounded through strtod.  Returns false on
+// NumberFormatException.
+// ----------------------------------------------------------------------------------------
+static bool is_hex(char c) {
+  return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
+}
+
+static bool java_parse_double(const uint16_t* u, size_t n, double* out) {
+  size_t a = 0, b = n;
+  while (a < b && u[a] <= 0x20) ++a;
+  while (b > a && u[b - 1] <= 0x20) --b;
+  if (a == b) return false;
+  std::string s;
+  s.reserve(b - a);
+  for (size_t i = a; i < b; ++i) {
+    if (u[i] > 0x7F) return false;
+    s.push_back((char)u[i]);
+  }
+  size_t i = 0;
+  bool neg = false;
+  if (s[i] == '+' || s[i] == '-') neg = s[i++] == '-';
+  const std::string body = s.substr(i);
+  if (body == "NaN") { *out = NAN; return true; }
+  if (body == "Infinity") { *out = neg ? -INFINITY : INFINITY; return true; }
+  std::string num = s;
+  if (body.size() > 1 && body[0] == '0' && (body[1] == 'x' || body[1] == 'X')) {
+    size_t j = i + 2, digits = 0;
+    while (j < s.size() && is_hex(s[j])) ++j, ++digits;
+    if (j < s.size() && s[j] == '.') {
+      ++j;
+      while (j < s.size() && is_hex(s[j])) ++j, ++digits;
+    }
+    if (!digits || j >= s.size() || (s[j] != 'p' && s[j] != 'P')) return false;
+    ++j;
+    if (j < s.size() && (s[j] == '+' || s[j] == '-')) ++j;
+    size_t ed = 0;
+    while (j < s.size() && s[j] >= '0' && s[j] <= '9') ++j, ++ed;
+    if (!ed) return false;
+    if (j < s.size() && strchr("fFdD", s[j])) num = s.substr(0, j++);
+    if (j != s.size()) return false;
+  } else {
+    size_t j = i, digits = 0;
+    while (j < s.size() && s[j] >= '0' && s[j] <= '9') ++j, ++digits;
+    if (j < s.size() && s[j] == '.') {
+      ++j;
+      while (j < s.size() && s[j] >= '0' && s[j] <= '9') ++j, ++digits;
+    }
+    if (!digits) return false;
+    if (j < s.size() && (s[j] == 'e' || s[j] == 'E')) {
+      ++j;
+      if (j < s.size() && (s[j] == '+' || s[j] == '-')) ++j;
+      size_t ed = 0;
+      while (j < s.size() && s[j] >= '0' && s[j] <= '9') ++j, ++ed;
+      if (!ed) return false;
+    }
+    if (j < s.size() && strchr("fFdD", s[j])) num = s.substr(0, j++);
+    if (j != s.size()) return false;
+  }
+  *out = strtod(num.c_str(), nullptr);
+  return true;
+}
+
+// q-gram set of one value: sorted unique 64-bit codes, 16 bits per code unit
+// (QGramComparator's HashSet<String> of substrings; POSITIONAL adds the index).
+static void qgram_codes(const uint16_t* u, int n, int q, int tokenizer, std::vector<uint64_t>& g) {
+  g.clear();
+  for (int ix = 0; ix + q <= n; ++ix) {
+    uint64_t c = 0;
+    for (int k = 0; k < q; ++k) c = (c << 16) | u[ix + k];
+    if (tokenizer == DK_QGRAM_POSITIONAL) c |= (uint64_t)ix << 48;
+    g.push_back(c);
+  }
+  std::sort(g.begin(), g.end());
+  g.erase(std::unique(g.begin(), g.end()), g.end());
+}
+
+// ----------------------------------------------------------------------------------------
+// context
+// ----------------------------------------------------------------------------------------
+struct PropState {
+  dk_property cfg{};
+  int width = 0;           // arena width; 0 until the first batch
+  uint64_t units_used = 0; // code units
+  uint64_t grams_used = 0;
+  int maxlen = 0;
+  DevBuf off, len, units, num, numok, goff, gcnt, grams;
+};
+
+struct ResultHolder {
+  dk_result r{};
+  std::vector<uint64_t> first;
+  std::vector<uint32_t> query, candidate;
+  std::vector<double> prob;
+  std::vector<uint8_t> kind;
+};
+
+struct dk_ctx {
+  dk_schema schema{};
+  std::vector<PropState> P;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t nrows = 0, cap = 0;
+  DevBuf ident, flags, group;
+  DevBuf keys[kMaxKeys];
+  std::unordered_map<uint64_t, uint32_t> ident_row;
+  std::vector<std::unordered_map<std::u16string, uint64_t>> intern;
+  int key_style = 0;  // 0 unset, 1 u64 keys, 2 interned strings
+  // match scratch
+  DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], srows[kMaxKeys], sgroup[kMaxKeys];
+  DevBuf ranges, counts, qoff, pq, pc, tmp;
+  DevBuf m_counters, m_slot, m_qidx, m_cand, m_prob, m_kind;
+  DevBuf s_slot, s_perm_in, s_perm, f_qidx, f_cand, f_prob, f_kind;
+  PinnedBuf h_counters;
+  uint64_t match_cap = 1u << 20;
+  // profiling (Processor.setPerformanceProfiling)
+  bool profiling = false;
+  dk_profile prof{};
+};
+
+static hipError_t grow_rows(dk_ctx* c, uint64_t need) {
+  if (need <= c->cap) return hipSuccess;
+  uint64_t nc = std::max<uint64_t>(need, std::max<uint64_t>(1024, c->cap * 2));
+  hipStream_t s = c->stream;
+  hipError_t e;
+  const uint64_t n = c->nrows;
+#define GROW(buf, T)                                              \
+  if ((e = (buf).reserve(nc * sizeof(T), n * sizeof(T), s)) != hipSuccess) return e;
+  GROW(c->ident, uint64_t);
+  GROW(c->flags, uint8_t);
+  GROW(c->group, uint8_t);
+  for (int k = 0; k < c->schema.nkeys; ++k) GROW(c->keys[k], uint64_t);
+  for (auto& p : c->P) {
+    GROW(p.off, uint32_t);
+    GROW(p.len, uint16_t);
+    if (p.cfg.comparator == DK_CMP_NUMERIC) {
+      GROW(p.num, double);
+      GROW(p.numok, uint8_t);
+    }
+    if (p.cfg.comparator == DK_CMP_QGRAM) {
+      GROW(p.goff, uint32_t);
+      GROW(p.gcnt, uint16_t);
+    }
+  }
+#undef GROW
+  c->cap = nc;
+  return hipSuccess;
+}
+
+static int validate_schema(const dk_schema* s) {
+  if (!s) return fail(DK_E_INVALID, "schema is NULL");
+  if (s->nprops < 0 || s->nprops > kMaxProps)
+    return fail(DK_E_INVALID, "nprops %d out of range [0, %d]", s->nprops, kMaxProps);
+  if (s->nprops > 0 && !s->props) return fail(DK_E_INVALID, "props is NULL");
+  if (s->mode < DK_MODE_DEDUP || s->mode > DK_MODE_ALLPAIRS)
+    return fail(DK_E_INVALID, "unknown mode %d", s->mode);
+  if (s->mode != DK_MODE_ALLPAIRS && (s->nkeys < 1 || s->nkeys > kMaxKeys))
+    return fail(DK_E_INVALID, "nkeys %d out of range [1, %d]", s->nkeys, kMaxKeys);
+  for (int i = 0; i < s->nprops; ++i) {
+    const dk_property& p = s->props[i];
+    switch (p.comparator) {
+      case DK_CMP_NONE:
+      case DK_CMP_LEVENSHTEIN:
+      case DK_CMP_JAROWINKLER:
+      case DK_CMP_EXACT:
+      case DK_CMP_NUMERIC:
+        break;
+      case DK_CMP_QGRAM:
+        if (p.qgram_q < 1 || p.qgram_q > 4)
+          return fail(DK_E_UNSUPPORTED, "property %d: QGramComparator q=%d (supported 1..4)", i,
+                      p.qgram_q);
+        if (p.qgram_tokenizer == DK_QGRAM_POSITIONAL && p.qgram_q > 3)
+          return fail(DK_E_UNSUPPORTED, "property %d: POSITIONAL tokenizer needs q <= 3", i);
+        if (p.qgram_tokenizer != DK_QGRAM_BASIC && p.qgram_tokenizer != DK_QGRAM_POSITIONAL)
+          return fail(DK_E_UNSUPPORTED, "property %d: q-gram tokenizer %d", i, p.qgram_tokenizer);
+        if (p.qgram_formula < DK_QGRAM_OVERLAP || p.qgram_formula > DK_QGRAM_DICE)
+          return fail(DK_E_UNSUPPORTED, "property %d: q-gram formula %d", i, p.qgram_formula);
+        break;
+      default:
+        return fail(DK_E_UNSUPPORTED, "property %d: comparator %d has no GPU kernel", i,
+                    p.comparator);
+    }
+  }
+  return DK_OK;
+}
+
+// Public entry points: C linkage comes from the declarations in dukehip.h.
+
+const char* dk_last_error(void) { return g_err.c_str(); }
+
+int dk_abi_version(void) { return DK_ABI_VERSION; }
+
+int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
+  if (!out) return fail(DK_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int rc = validate_schema(schema);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(DK_E_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= ndev)
+    return fail(DK_E_INVALID, "device %d out of range (%d visible)", device, ndev);
+  HIPCHK(hipSetDevice(device));
+  dk_ctx* c = new (std::nothrow) dk_ctx();
+  if (!c) return fail(DK_E_NOMEM, "out of host memory");
+  c->schema = *schema;
+  c->schema.props = nullptr;
+  c->P.resize(schema->nprops);
+  for (int i = 0; i < schema->nprops; ++i) c->P[i].cfg = schema->props[i];
+  if (c->schema.mode == DK_MODE_ALLPAIRS) c->schema.nkeys = 0;
+  c->intern.resize(c->schema.nkeys);
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(DK_E_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  if (c->m_counters.reserve(4 * sizeof(uint64_t), 0, c->stream) != hipSuccess ||
+      c->h_counters.reserve(4 * sizeof(uint64_t)) != hipSuccess) {
+    delete c;
+    return fail(DK_E_DEVICE, "counter allocation failed");
+  }
+  *out = c;
+  return DK_OK;
+}
+
+void dk_destroy(dk_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  hipStream_t s = c->stream;
+  delete c;
+  (void)hipStreamDestroy(s);
+}
+
+uint64_t dk_num_rows(const dk_ctx* c) { return c ? c->nrows : 0; }
+
+int dk_set_profiling(dk_ctx* c, int on) {
+  if (!c) return fail(DK_E_INVALID, "ctx is NULL");
+  c->profiling = on != 0;
+  return DK_OK;
+}
+
+int dk_get_profile(const dk_ctx* c, dk_profile* out) {
+  if (!c || !out) return fail(DK_E_INVALID, "NULL argument");
+  *out = c->prof;
+  return DK_OK;
+}
+
+int dk_reset_profile(dk_ctx* c) {
+  if (!c) return fail(DK_E_INVALID, "ctx is NULL");
+  c->prof = dk_profile{};
+  return DK_OK;
+}
+
+// ----------------------------------------------------------------------------------------
+// dk_upsert: Database.index(Record) for each record of the batch + Database.commit()
+// ----------------------------------------------------------------------------------------
+static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, uint64_t row0) {
+  PropState& P = c->P[pidx];
+  hipStream_t s = c->stream;
+  if (!col->offsets || (n && !col->units && col->offsets[n] != col->offsets[0]))
+    return fail(DK_E_INVALID, "property %d: offsets/units missing", pidx);
+  if (col->width != 1 && col->width != 2)
+    return fail(DK_E_INVALID, "property %d: width %d (1 or 2)", pidx, col->width);
+  int want = col->width;
+  if (P.width == 0) P.width = want;
+  if (want == 2 && P.width == 1) {
+    // widen the arena in place: strings keep their unit offsets (4-byte alignment holds)
+    DevBuf wide;
+    const uint64_t tot = P.units_used + 512;
+    HIPCHK(wide.reserve(P.units.bytes * 2 + 1024, 0, s));
+    HIPCHK(launch_widen_u8(P.units.as<uint8_t>(), wide.as<uint16_t>(), std::min<uint64_t>(tot, P.units.bytes), s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::swap(P.units.p, wide.p);
+    std::swap(P.units.bytes, wide.bytes);
+    P.width = 2;
+  }
+  const int W = P.width;
+  const uint64_t align = 4 / W;  // units per 4 bytes
+  std::vector<uint32_t> off(n);
+  std::vector<uint16_t> len(n);
+  std::vector<uint8_t> bytes;
+  uint64_t cur = P.units_used;
+  const bool is_lev = P.cfg.comparator == DK_CMP_LEVENSHTEIN;
+  std::vector<uint16_t> u16;
+  std::vector<double> num;
+  std::vector<uint8_t> numok;
+  std::vector<uint32_t> goff;
+  std::vector<uint16_t> gcnt;
+  std::vector<uint64_t> grams, g;
+  const bool is_num = P.cfg.comparator == DK_CMP_NUMERIC;
+  const bool is_qg = P.cfg.comparator == DK_CMP_QGRAM;
+  if (is_num) { num.assign(n, 0.0); numok.assign(n, 0); }
+  if (is_qg) { goff.assign(n, 0); gcnt.assign(n, 0); }
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t a = col->offsets[i], b = col->offsets[i + 1];
+    if (b < a) return fail(DK_E_INVALID, "property %d: offsets not monotone at %llu", pidx,
+                           (unsigned long long)i);
+    const bool present = !col->present || col->present[i];
+    const uint64_t L = b - a;
+    if (present && L >= kMissing)
+      return fail(DK_E_UNSUPPORTED, "property %d: value of %llu units (max %u)", pidx,
+                  (unsigned long long)L, (unsigned)kMissing - 1);
+    if (present && is_lev && L > (uint64_t)kMaxUnits)
+      return fail(DK_E_UNSUPPORTED,
+                  "property %d: Levenshtein value of %llu units (GPU limit %d)", pidx,
+                  (unsigned long long)L, kMaxUnits);
+    off[i] = (uint32_t)cur;
+    len[i] = present ? (uint16_t)L : kMissing;
+    if (!present) continue;
+    P.maxlen = std::max<int>(P.maxlen, (int)L);
+    u16.resize(L);
+    for (uint64_t k = 0; k < L; ++k)
+      u16[k] = col->width == 1 ? ((const uint8_t*)col->units)[a + k] : ((const uint16_t*)col->units)[a + k];
+    const uint64_t padded = (L + align - 1) / align * align;
+    const size_t at = bytes.size();
+    bytes.resize(at + padded * W, 0);
+    if (W == 1) for (uint64_t k = 0; k < L; ++k) bytes[at + k] = (uint8_t)u16[k];
+    else memcpy(bytes.data() + at, u16.data(), L * 2);
+    cur += padded;
+    if (is_num) {
+      double v = 0.0;
+      numok[i] = java_parse_double(u16.data(), L, &v) ? 1 : 0;
+      num[i] = v;
+    }
+    if (is_qg) {
+      qgram_codes(u16.data(), (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, g);
+      if (g.size() >= kMissing)
+        return fail(DK_E_UNSUPPORTED, "property %d: %zu q-grams", pidx, g.size());
+      goff[i] = (uint32_t)(P.grams_used + grams.size());
+      gcnt[i] = (uint16_t)g.size();
+      grams.insert(grams.end(), g.begin(), g.end());
+    }
+  }
+  if (cur >= (1ull << 32)) return fail(DK_E_UNSUPPORTED, "property %d: arena over 4G units", pidx);
+  // units arena: keep 512 bytes of zeroed tail for the kernels' fixed-width over-reads
+  const size_t used_b = P.units_used * W, add_b = bytes.size();
+  HIPCHK(P.units.reserve(used_b + add_b + 512, used_b, s));
+  if (add_b) HIPCHK(hipMemcpyAsync(P.units.as<uint8_t>() + used_b, bytes.data(), add_b, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(P.units.as<uint8_t>() + used_b + add_b, 0, 512, s));
+  P.units_used = cur;
+  HIPCHK(hipMemcpyAsync(P.off.as<uint32_t>() + row0, off.data(), n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P.len.as<uint16_t>() + row0, len.data(), n * 2, hipMemcpyHostToDevice, s));
+  if (is_num) {
+    HIPCHK(hipMemcpyAsync(P.num.as<double>() + row0, num.data(), n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(P.numok.as<uint8_t>() + row0, numok.data(), n, hipMemcpyHostToDevice, s));
+  }
+  if (is_qg) {
+    HIPCHK(hipMemcpyAsync(P.goff.as<uint32_t>() + row0, goff.data(), n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(P.gcnt.as<uint16_t>() + row0, gcnt.data(), n * 2, hipMemcpyHostToDevice, s));
+    HIPCHK(P.grams.reserve((P.grams_used + grams.size() + 64) * 8, P.grams_used * 8, s));
+    if (!grams.empty())
+      HIPCHK(hipMemcpyAsync(P.grams.as<uint64_t>() + P.grams_used, grams.data(), grams.size() * 8,
+                            hipMemcpyHostToDevice, s));
+    P.grams_used += grams.size();
+  }
+  HIPCHK(hipStreamSynchronize(s));  // host staging vectors go out of scope
+  return DK_OK;
+}
+
+int dk_upsert(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
+  if (!c || !b) return fail(DK_E_INVALID, "NULL argument");
+  if (b->n == 0) return DK_OK;
+  if (!b->ident) return fail(DK_E_INVALID, "batch.ident is NULL");
+  if (c->schema.nprops > 0 && !b->columns) return fail(DK_E_INVALID, "batch.columns is NULL");
+  if (c->schema.mode == DK_MODE_LINKAGE && !b->group)
+    return fail(DK_E_INVALID, "LINKAGE mode needs batch.group (dukeGroupNo)");
+  const int nk = c->schema.nkeys;
+  if (nk > 0) {
+    const int style = b->keys ? 1 : (b->key_columns ? 2 : 0);
+    if (!style) return fail(DK_E_INVALID, "batch has neither keys nor key_columns");
+    if (c->key_style && c->key_style != style)
+      return fail(DK_E_STATE, "key style changed between batches (u64 keys vs key strings)");
+    c->key_style = style;
+  }
+  if (c->nrows + b->n >= (1ull << kKeyShift))
+    return fail(DK_E_UNSUPPORTED, "index would exceed %u rows", 1u << kKeyShift);
+  HIPCHK(hipSetDevice(c->device));
+  const uint64_t n = b->n, row0 = c->nrows;
+  HIPCHK(grow_rows(c, row0 + n));
+  hipStream_t s = c->stream;
+
+  // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517)
+  std::vector<uint8_t> flags(n);
+  std::vector<uint32_t> dead;
+  for (uint64_t i = 0; i < n; ++i) {
+    flags[i] = kAlive | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
+    auto it = c->ident_row.find(b->ident[i]);
+    if (it != c->ident_row.end()) {
+      const uint32_t old = it->second;
+      if (old >= row0) flags[old - row0] &= (uint8_t)~kAlive;
+      else dead.push_back(old);
+      it->second = (uint32_t)(row0 + i);
+    } else {
+      c->ident_row.emplace(b->ident[i], (uint32_t)(row0 + i));
+    }
+  }
+  HIPCHK(hipMemcpyAsync(c->ident.as<uint64_t>() + row0, b->ident, n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->flags.as<uint8_t>() + row0, flags.data(), n, hipMemcpyHostToDevice, s));
+  if (b->group)
+    HIPCHK(hipMemcpyAsync(c->group.as<uint8_t>() + row0, b->group, n, hipMemcpyHostToDevice, s));
+  else
+    HIPCHK(hipMemsetAsync(c->group.as<uint8_t>() + row0, 0, n, s));
+  DevBuf d_dead;
+  if (!dead.empty()) {
+    HIPCHK(d_dead.reserve(dead.size() * 4, 0, s));
+    HIPCHK(hipMemcpyAsync(d_dead.p, dead.data(), dead.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_clear_flag(c->flags.as<uint8_t>(), d_dead.as<uint32_t>(), dead.size(), kAlive, s));
+  }
+  for (int p = 0; p < c->schema.nprops; ++p) {
+    int rc = upload_column(c, p, &b->columns[p], n, row0);
+    if (rc) return rc;
+  }
+  // key functions
+  std::vector<uint64_t> kv(n);
+  for (int k = 0; k < nk; ++k) {
+    const uint64_t* src;
+    if (c->key_style == 1) {
+      src = b->keys + (uint64_t)k * n;
+    } else {
+      const dk_column& kc = b->key_columns[k];
+      if (!kc.offsets || (kc.width != 1 && kc.width != 2))
+        return fail(DK_E_INVALID, "key function %d: bad key column", k);
+      auto& tab = c->intern[k];
+      std::u16string str;
+      for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t a = kc.offsets[i], e = kc.offsets[i + 1];
+        str.resize(e - a);
+        for (uint64_t j = a; j < e; ++j)
+          str[j - a] = kc.width == 1 ? ((const uint8_t*)kc.units)[j] : ((const uint16_t*)kc.units)[j];
+        auto it = tab.find(str);
+        if (it == tab.end()) it = tab.emplace(str, (uint64_t)tab.size()).first;
+        kv[i] = it->second;
+      }
+      src = kv.data();
+    }
+    HIPCHK(hipMemcpyAsync(c->keys[k].as<uint64_t>() + row0, src, n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  c->nrows += n;
+  if (rows_out)
+    for (uint64_t i = 0; i < n; ++i) rows_out[i] = (uint32_t)(row0 + i);
+  return DK_OK;
+}
+
+// ----------------------------------------------------------------------------------------
+// dk_match: Processor.deduplicate's match loop over the given query rows
+// ----------------------------------------------------------------------------------------
+namespace {
+struct Timer {
+  hipEvent_t a = nullptr, b = nullptr;
+  bool on;
+  hipStream_t s;
+  Timer(bool enabled, hipStream_t st) : on(enabled), s(st) {
+    if (on) {
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      (void)hipEventRecord(a, s);
+    }
+  }
+  double stop() {
+    if (!on) return 0.0;
+    (void)hipEventRecord(b, s);
+    (void)hipEventSynchronize(b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    return ms;
+  }
+  ~Timer() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+  }
+};
+
+uint64_t chunk_slots() {
+  const char* e = getenv("DK_CHUNK_SLOTS");
+  uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+  return v ? v : (1ull << 26);
+}
+}  // namespace
+
+static ScoreParams make_params(const dk_ctx* c) {
+  ScoreParams P{};
+  P.nprops = c->schema.nprops;
+  P.mode = c->schema.mode;
+  P.threshold = c->schema.threshold;
+  P.maybe = c->schema.maybe_threshold;
+  P.ident = c->ident.as<uint64_t>();
+  for (int i = 0; i < P.nprops; ++i) {
+    const PropState& S = c->P[i];
+    DevProp& D = P.props[i];
+    D.op = S.cfg.comparator;
+    D.width = S.width ? S.width : 1;
+    D.q = S.cfg.qgram_q;
+    D.formula = S.cfg.qgram_formula;
+    D.tokenizer = S.cfg.qgram_tokenizer;
+    D.low = S.cfg.low;
+    D.high = S.cfg.high;
+    D.min_ratio = S.cfg.min_ratio;
+    D.off = S.off.as<uint32_t>();
+    D.len = S.len.as<uint16_t>();
+    D.units = S.units.p;
+    D.num = S.num.as<double>();
+    D.numok = S.numok.as<uint8_t>();
+    D.goff = S.goff.as<uint32_t>();
+    D.gcnt = S.gcnt.as<uint16_t>();
+    D.grams = S.grams.as<uint64_t>();
+  }
+  return P;
+}
+
+template <typename F>
+static hipError_t with_tmp(dk_ctx* c, F&& f) {
+  size_t bytes = 0;
+  hipError_t e = f(nullptr, bytes);
+  if (e != hipSuccess) return e;
+  e = c->tmp.reserve(bytes + 16, 0, c->stream);
+  if (e != hipSuccess) return e;
+  return f(c->tmp.p, bytes);
+}
+
+// usable rows: alive && !deleted, ordered by (group, row) in LINKAGE, row otherwise
+static int build_usable(dk_ctx* c, uint64_t* m_out) {
+  hipStream_t s = c->stream;
+  const uint64_t N = c->nrows;
+  HIPCHK(c->sel.reserve(N * 4 + 4, 0, s));
+  HIPCHK(c->pos.reserve(N * 4 + 4, 0, s));
+  HIPCHK(c->usable.reserve(N * 4 + 4, 0, s));
+  const bool link = c->schema.mode == DK_MODE_LINKAGE;
+  uint64_t m = 0;
+  for (int pass = 0; pass < (link ? 2 : 1); ++pass) {
+    HIPCHK(launch_select_rows(c->flags.as<uint8_t>(), c->group.as<uint8_t>(), N, link ? pass + 1 : 0,
+                              c->sel.as<uint32_t>(), s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return exclusive_scan_u32(t, b, c->sel.as<uint32_t>(), c->pos.as<uint32_t>(), N, s);
+    }));
+    HIPCHK(launch_scatter_rows(c->sel.as<uint32_t>(), c->pos.as<uint32_t>(), N, (uint32_t)m,
+                               c->usable.as<uint32_t>(), s));
+    uint32_t last_pos = 0, last_sel = 0;
+    if (N) {
+      HIPCHK(hipMemcpyAsync(&last_pos, c->pos.as<uint32_t>() + N - 1, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(&last_sel, c->sel.as<uint32_t>() + N - 1, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    m += (uint64_t)last_pos + last_sel;
+  }
+  *m_out = m;
+  return DK_OK;
+}
+
+static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, ResultHolder* R) {
+  hipStream_t s = c->stream;
+  const bool prof = c->profiling;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int nk = c->schema.nkeys;
+  const bool allpairs = c->schema.mode == DK_MODE_ALLPAIRS;
+
+  HIPCHK(c->d_queries.reserve(nq * 4 + 4, 0, s));
+  HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
+
+  // ---- index: usable rows + per key function sort by (key, group, row) ----
+  Timer t_index(prof, s);
+  uint64_t M = 0;
+  int rc = build_usable(c, &M);
+  if (rc) return rc;
+  BlockTables T{};
+  T.nkeys = nk;
+  T.linkage = c->schema.mode == DK_MODE_LINKAGE;
+  T.group = c->group.as<uint8_t>();
+  for (int k = 0; k < nk; ++k) {
+    HIPCHK(c->gkeys.reserve(M * 8 + 8, 0, s));
+    HIPCHK(c->skeys[k].reserve(M * 8 + 8, 0, s));
+    HIPCHK(c->srows[k].reserve(M * 4 + 4, 0, s));
+    HIPCHK(launch_gather_keys(c->keys[k].as<uint64_t>(), c->usable.as<uint32_t>(), c->gkeys.as<uint64_t>(), M, s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return sort_pairs_u64_u32(t, b, c->gkeys.as<uint64_t>(), c->skeys[k].as<uint64_t>(),
+                                c->usable.as<uint32_t>(), c->srows[k].as<uint32_t>(), M, s);
+    }));
+    if (T.linkage) {
+      HIPCHK(c->sgroup[k].reserve(M + 8, 0, s));
+      HIPCHK(launch_gather_u8(c->group.as<uint8_t>(), c->srows[k].as<uint32_t>(), c->sgroup[k].as<uint8_t>(), M, s));
+    }
+    T.keys[k] = c->keys[k].as<uint64_t>();
+    T.skeys[k] = c->skeys[k].as<uint64_t>();
+    T.srows[k] = c->srows[k].as<uint32_t>();
+    T.sgroup[k] = c->sgroup[k].as<uint8_t>();
+    T.n[k] = M;
+  }
+  c->prof.ms_index += t_index.stop();
+
+  // ---- candidate counts per query -> slot offsets ----
+  Timer t_gen(prof, s);
+  std::vector<uint64_t>& qoff = R->first;  // reused: slot offsets first, entry offsets later
+  qoff.assign(nq + 1, 0);
+  uint64_t total = 0;
+  if (!allpairs) {
+    HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
+    HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
+    HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
+    HIPCHK(launch_count(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(), c->counts.as<uint64_t>(), s));
+    HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
+    }));
+    HIPCHK(hipMemcpyAsync(qoff.data(), c->qoff.p, (nq + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    total = qoff[nq];
+  } else {
+    for (uint64_t i = 0; i <= nq; ++i) qoff[i] = i * M;
+    total = nq * M;
+  }
+  c->prof.ms_generate += t_gen.stop();
+
+  const ScoreParams P = make_params(c);
+  const uint64_t CH = chunk_slots();
+  if (!allpairs) {
+    HIPCHK(c->pq.reserve(std::min(CH, total) * 4 + 4, 0, s));
+    HIPCHK(c->pc.reserve(std::min(CH, total) * 4 + 4, 0, s));
+  }
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    HIPCHK(c->m_slot.reserve(c->match_cap * 8, 0, s));
+    HIPCHK(c->m_qidx.reserve(c->match_cap * 4, 0, s));
+    HIPCHK(c->m_cand.reserve(c->match_cap * 4, 0, s));
+    HIPCHK(c->m_prob.reserve(c->match_cap * 8, 0, s));
+    HIPCHK(c->m_kind.reserve(c->match_cap, 0, s));
+    HIPCHK(hipMemsetAsync(c->m_counters.p, 0, 4 * sizeof(uint64_t), s));
+    MatchOut out{c->m_counters.as<uint64_t>(), c->match_cap, c->m_slot.as<uint64_t>(),
+                 c->m_qidx.as<uint32_t>(), c->m_cand.as<uint32_t>(), c->m_prob.as<double>(),
+                 c->m_kind.as<uint8_t>()};
+    for (uint64_t s0 = 0; s0 < total; s0 += CH) {
+      const uint64_t s1 = std::min(total, s0 + CH);
+      PairSource src{};
+      src.queries = c->d_queries.as<uint32_t>();
+      if (allpairs) {
+        src.allpairs = 1;
+        src.usable = c->usable.as<uint32_t>();
+        src.m = M;
+      } else {
+        Timer t_emit(prof, s);
+        const uint64_t q0 = (uint64_t)(std::upper_bound(qoff.begin(), qoff.end(), s0) - qoff.begin()) - 1;
+        const uint64_t q1 = (uint64_t)(std::lower_bound(qoff.begin(), qoff.end(), s1) - qoff.begin());
+        HIPCHK(launch_emit(c->d_queries.as<uint32_t>(), q0, std::min(q1, nq), c->qoff.as<uint64_t>(),
+                           c->ranges.as<uint2>(), nq, T, c->ident.as<uint64_t>(), s0, s1,
+                           c->pq.as<uint32_t>(), c->pc.as<uint32_t>(), s));
+        c->prof.ms_generate += t_emit.stop();
+        src.pq = c->pq.as<uint32_t>();
+        src.pc = c->pc.as<uint32_t>();
+      }
+      Timer t_score(prof, s);
+      HIPCHK(launch_score(P, src, s0, s1 - s0, out, s));
+      c->prof.ms_score += t_score.stop();
+      c->prof.score_launches += 1;
+    }
+    HIPCHK(hipMemcpyAsync(c->h_counters.p, c->m_counters.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint64_t* hc = c->h_counters.as<uint64_t>();
+    if (hc[0] <= c->match_cap) break;
+    if (attempt == 1) return fail(DK_E_STATE, "match list overflow after resize");
+    c->match_cap = hc[0] + hc[0] / 4 + 1024;  // rerun with room for every entry
+  }
+  const uint64_t* hc = c->h_counters.as<uint64_t>();
+  const uint64_t nm = hc[0];
+  R->r.pairs_scored = hc[1];
+  R->r.pairs_generated = total;
+  c->prof.pairs_scored += hc[1];
+  c->prof.pairs_generated += total;
+  c->prof.score_bytes += hc[2];
+
+  // ---- gather: order entries by slot (= query order, key fn, candidate order) ----
+  Timer t_gather(prof, s);
+  R->query.resize(nm);
+  R->candidate.resize(nm);
+  R->prob.resize(nm);
+  R->kind.resize(nm);
+  std::vector<uint32_t> qidx(nm);
+  if (nm) {
+    HIPCHK(c->s_slot.reserve(nm * 8, 0, s));
+    HIPCHK(c->s_perm_in.reserve(nm * 4, 0, s));
+    HIPCHK(c->s_perm.reserve(nm * 4, 0, s));
+    HIPCHK(c->f_qidx.reserve(nm * 4, 0, s));
+    HIPCHK(c->f_cand.reserve(nm * 4, 0, s));
+    HIPCHK(c->f_prob.reserve(nm * 8, 0, s));
+    HIPCHK(c->f_kind.reserve(nm, 0, s));
+    HIPCHK(launch_iota_u32(c->s_perm_in.as<uint32_t>(), nm, s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return sort_pairs_u64_u32(t, b, c->m_slot.as<uint64_t>(), c->s_slot.as<uint64_t>(),
+                                c->s_perm_in.as<uint32_t>(), c->s_perm.as<uint32_t>(), nm, s);
+    }));
+    MatchOut in{nullptr, 0, nullptr, c->m_qidx.as<uint32_t>(), c->m_cand.as<uint32_t>(),
+                c->m_prob.as<double>(), c->m_kind.as<uint8_t>()};
+    HIPCHK(launch_gather_matches(c->s_perm.as<uint32_t>(), nm, in, c->f_qidx.as<uint32_t>(),
+                                 c->f_cand.as<uint32_t>(), c->f_prob.as<double>(), c->f_kind.as<uint8_t>(), s));
+    HIPCHK(hipMemcpyAsync(qidx.data(), c->f_qidx.p, nm * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(R->candidate.data(), c->f_cand.p, nm * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(R->prob.data(), c->f_prob.p, nm * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(R->kind.data(), c->f_kind.p, nm, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  // entry offsets per query (entries are grouped by query index, ascending)
+  std::vector<uint64_t>& first = R->first;
+  first.assign(nq + 1, 0);
+  for (uint64_t i = 0; i < nm; ++i) {
+    first[qidx[i] + 1]++;
+    R->query[i] = query_rows[qidx[i]];
+  }
+  for (uint64_t i = 0; i < nq; ++i) first[i + 1] += first[i];
+  c->prof.ms_gather += t_gather.stop();
+
+  R->r.nqueries = nq;
+  R->r.first = first.data();
+  R->r.n = nm;
+  R->r.query = R->query.data();
+  R->r.candidate = R->candidate.data();
+  R->r.prob = R->prob.data();
+  R->r.kind = R->kind.data();
+  c->prof.ms_total +=
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return DK_OK;
+}
+
+int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, dk_result** out) {
+  if (!c || !out) return fail(DK_E_INVALID, "NULL argument");
+  *out = nullptr;
+  if (nq && !query_rows) return fail(DK_E_INVALID, "query_rows is NULL");
+  for (uint64_t i = 0; i < nq; ++i)
+    if (query_rows[i] >= c->nrows)
+      return fail(DK_E_INVALID, "query row %u not in the index (%llu rows)", query_rows[i],
+                  (unsigned long long)c->nrows);
+  if (nq >= (1ull << 32)) return fail(DK_E_UNSUPPORTED, "too many queries");
+  HIPCHK(hipSetDevice(c->device));
+  ResultHolder* R = new (std::nothrow) ResultHolder();
+  if (!R) return fail(DK_E_NOMEM, "out of host memory");
+  int rc = run_match(c, query_rows, nq, R);
+  if (rc) {
+    delete R;
+    return rc;
+  }
+  *out = &R->r;
+  return DK_OK;
+}
+
+void dk_free_result(dk_result* r) {
+  if (!r) return;
+  delete reinterpret_cast<ResultHolder*>(r);  // dk_result is the first member
+}
+
+int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
+  if (!c || !prob) return fail(DK_E_INVALID, "NULL argument");
+  if (r1 >= c->nrows || r2 >= c->nrows) return fail(DK_E_INVALID, "row out of range");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  DevBuf buf;
+  HIPCHK(buf.reserve(256, 0, s));
+  uint32_t host[3] = {r1, 0u, r2};
+  HIPCHK(hipMemcpyAsync(buf.p, host, sizeof host, hipMemcpyHostToDevice, s));
+  uint64_t* counters = reinterpret_cast<uint64_t*>(buf.as<uint8_t>() + 64);
+  HIPCHK(hipMemsetAsync(counters, 0, 64, s));
+  uint8_t* base = buf.as<uint8_t>() + 128;
+  MatchOut out{counters, 1, reinterpret_cast<uint64_t*>(base), reinterpret_cast<uint32_t*>(base + 8),
+               reinterpret_cast<uint32_t*>(base + 12), reinterpret_cast<double*>(base + 16),
+               base + 24};
+  ScoreParams P = make_params(c);
+  P.threshold = -INFINITY;  // every non-NaN probability is emitted
+  P.maybe = 0.0;
+  PairSource src{};
+  src.queries = buf.as<uint32_t>();
+  src.pq = buf.as<uint32_t>() + 1;
+  src.pc = buf.as<uint32_t>() + 2;
+  HIPCHK(launch_score(P, src, 0, 1, out, s));
+  uint64_t n = 0;
+  double p = NAN;
+  HIPCHK(hipMemcpyAsync(&n, counters, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&p, base + 16, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *prob = n ? p : NAN;
+  return DK_OK;
+}
+

@@ -1,0 +1,159 @@
+"""ctypes binding of libdukehip.so (include/dukehip.h).
+
+This is the product path: there is no CPU fallback.  If the shared library is missing or
+no GPU is visible, calls raise :class:`DukeHipError` loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("DUKEHIP_LIB", os.path.join(PKG_DIR, "build", "libdukehip.so"))
+
+DK_OK = 0
+DK_E_INVALID, DK_E_UNSUPPORTED, DK_E_NOMEM, DK_E_DEVICE, DK_E_STATE = -1, -2, -3, -4, -5
+
+CMP_NONE, CMP_LEVENSHTEIN, CMP_JAROWINKLER, CMP_QGRAM, CMP_EXACT, CMP_NUMERIC, CMP_WEIGHTED_LEVENSHTEIN = range(7)
+QGRAM_OVERLAP, QGRAM_JACCARD, QGRAM_DICE = 0, 1, 2
+QGRAM_BASIC, QGRAM_POSITIONAL = 0, 1
+MODE_DEDUP, MODE_LINKAGE, MODE_ALLPAIRS = 0, 1, 2
+KIND_MATCH, KIND_MAYBE = 1, 2
+
+EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_match", "dk_free_result",
+           "dk_compare_rows", "dk_num_rows", "dk_set_profiling", "dk_get_profile",
+           "dk_reset_profile", "dk_last_error", "dk_abi_version")
+
+
+class DukeHipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"dukehip error {code}: {msg}")
+        self.code = code
+
+
+class dk_property(C.Structure):
+    _fields_ = [("comparator", C.c_int32), ("qgram_q", C.c_int32), ("qgram_formula", C.c_int32),
+                ("qgram_tokenizer", C.c_int32), ("low", C.c_double), ("high", C.c_double),
+                ("min_ratio", C.c_double)]
+
+
+class dk_schema(C.Structure):
+    _fields_ = [("nprops", C.c_int32), ("props", C.POINTER(dk_property)),
+                ("threshold", C.c_double), ("maybe_threshold", C.c_double),
+                ("mode", C.c_int32), ("nkeys", C.c_int32)]
+
+
+class dk_column(C.Structure):
+    _fields_ = [("offsets", C.c_void_p), ("units", C.c_void_p), ("width", C.c_int32),
+                ("present", C.c_void_p)]
+
+
+class dk_batch(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("ident", C.c_void_p), ("group", C.c_void_p),
+                ("deleted", C.c_void_p), ("columns", C.POINTER(dk_column)),
+                ("keys", C.c_void_p), ("key_columns", C.POINTER(dk_column))]
+
+
+class dk_result(C.Structure):
+    _fields_ = [("nqueries", C.c_uint64), ("first", C.POINTER(C.c_uint64)), ("n", C.c_uint64),
+                ("query", C.POINTER(C.c_uint32)), ("candidate", C.POINTER(C.c_uint32)),
+                ("prob", C.POINTER(C.c_double)), ("kind", C.POINTER(C.c_uint8)),
+                ("pairs_scored", C.c_uint64), ("pairs_generated", C.c_uint64)]
+
+
+class dk_profile(C.Structure):
+    _fields_ = [("ms_index", C.c_double), ("ms_generate", C.c_double), ("ms_score", C.c_double),
+                ("ms_gather", C.c_double), ("ms_total", C.c_double),
+                ("score_launches", C.c_uint64), ("pairs_scored", C.c_uint64),
+                ("pairs_generated", C.c_uint64), ("score_bytes", C.c_uint64)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+_lib = None
+
+
+def load():
+    """Load libdukehip.so (built by __graft_entry__.build() / `make -C csrc`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DukeHipError(DK_E_STATE, f"{LIB_PATH} not built: run `make -C "
+                           f"{os.path.join(PKG_DIR, 'csrc')}` or __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.dk_create.argtypes = [C.POINTER(dk_schema), C.c_int, C.POINTER(vp)]
+    L.dk_destroy.argtypes = [vp]
+    L.dk_destroy.restype = None
+    L.dk_upsert.argtypes = [vp, C.POINTER(dk_batch), vp]
+    L.dk_match.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.POINTER(dk_result))]
+    L.dk_free_result.argtypes = [C.POINTER(dk_result)]
+    L.dk_free_result.restype = None
+    L.dk_compare_rows.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
+    L.dk_num_rows.argtypes = [vp]
+    L.dk_num_rows.restype = C.c_uint64
+    L.dk_set_profiling.argtypes = [vp, C.c_int]
+    L.dk_get_profile.argtypes = [vp, C.POINTER(dk_profile)]
+    L.dk_reset_profile.argtypes = [vp]
+    L.dk_last_error.restype = C.c_char_p
+    L.dk_abi_version.restype = C.c_int
+    for f in ("dk_create", "dk_upsert", "dk_match", "dk_compare_rows", "dk_set_profiling",
+              "dk_get_profile", "dk_reset_profile"):
+        getattr(L, f).restype = C.c_int
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != DK_OK:
+        raise DukeHipError(rc, load().dk_last_error().decode("utf-8", "replace"))
+    return rc
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class Column:
+    """Packed values of one property for a batch (owns its numpy buffers)."""
+
+    def __init__(self, offsets, units, present=None):
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        self.units = np.ascontiguousarray(units)
+        if self.units.dtype not in (np.uint8, np.uint16):
+            raise ValueError("units must be uint8 or uint16")
+        if self.units.size == 0:
+            self.units = np.zeros(1, dtype=self.units.dtype)
+        self.present = None if present is None else np.ascontiguousarray(present, dtype=np.uint8)
+
+    @classmethod
+    def from_strings(cls, values):
+        """values: iterable of str or None.  Latin-1-only columns pack one byte per unit."""
+        vals = list(values)
+        enc = []
+        wide = False
+        for v in vals:
+            if v is None:
+                enc.append(None)
+                continue
+            b = v.encode("utf-16-le", "surrogatepass")
+            u = np.frombuffer(b, dtype=np.uint16)
+            if u.size and int(u.max()) > 0xFF:
+                wide = True
+            enc.append(u)
+        dt = np.uint16 if wide else np.uint8
+        lens = np.array([0 if u is None else u.size for u in enc], dtype=np.int64)
+        offs = np.zeros(len(vals) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        units = np.concatenate([u for u in enc if u is not None]).astype(dt) if any(
+            u is not None and u.size for u in enc) else np.zeros(1, dtype=dt)
+        present = np.array([u is not None for u in enc], dtype=np.uint8)
+        return cls(offs, units, None if present.all() else present)
+
+    def c(self):
+        return dk_column(ptr(self.offsets), ptr(self.units), self.units.itemsize,
+                         ptr(self.present))

@@ -1,0 +1,298 @@
+"""Host mirror of the Duke contracts the microservice drives, backed by libdukehip.so.
+
+* ``GpuBlockingDatabase``  <- Duke ``Database`` as IncrementalLuceneDatabase implements it
+  (setConfiguration :90, setOverwrite :99, isInMemory :139, commit :146,
+  findRecordById :170, close :186, index :498): records are column-packed into the
+  device-resident index; upsert by ID; key-function blocking replaces the Lucene query.
+* ``GpuProcessor``         <- ``no.priv.garshol.duke.Processor`` as constructed and driven
+  at App.java:342-345, 354, 1005, 1159: ``deduplicate(records)`` runs the whole batch on the
+  GPU and replays the MatchListener callbacks in Duke's order on the calling thread.
+* ``MatchListener``        <- the 7 callbacks of BaseLinkDatabaseMatchListener.java:53-109.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi as A
+from .config import DukeConfig, ID_PROPERTY, GROUP_NO_PROPERTY_NAME, DELETED_PROPERTY_NAME
+from .records import Record
+
+
+class MatchListener:
+    """[Duke 1.2] matchers.MatchListener."""
+
+    def batch_ready(self, size):
+        pass
+
+    def batch_done(self):
+        pass
+
+    def matches(self, r1, r2, confidence):
+        pass
+
+    def matches_perhaps(self, r1, r2, confidence):
+        pass
+
+    def no_match_for(self, record):
+        pass
+
+    def start_processing(self):
+        pass
+
+    def end_processing(self):
+        pass
+
+
+class CollectingListener(MatchListener):
+    """Records every callback in order (what the reference's listeners observe)."""
+
+    def __init__(self):
+        self.events = []
+
+    def batch_ready(self, size):
+        self.events.append(("batchReady", size))
+
+    def batch_done(self):
+        self.events.append(("batchDone",))
+
+    def matches(self, r1, r2, confidence):
+        self.events.append(("matches", r1.get_value(ID_PROPERTY), r2.get_value(ID_PROPERTY), confidence))
+
+    def matches_perhaps(self, r1, r2, confidence):
+        self.events.append(("matchesPerhaps", r1.get_value(ID_PROPERTY), r2.get_value(ID_PROPERTY), confidence))
+
+    def no_match_for(self, record):
+        self.events.append(("noMatchFor", record.get_value(ID_PROPERTY)))
+
+
+class MatchResult:
+    """Host copy of a dk_result: entries grouped per query (batch order)."""
+
+    def __init__(self, res):
+        r = res.contents
+        n, nq = r.n, r.nqueries
+        self.n, self.nqueries = n, nq
+        self.pairs_scored, self.pairs_generated = r.pairs_scored, r.pairs_generated
+        as_np = np.ctypeslib.as_array
+        self.first = as_np(r.first, (nq + 1,)).copy() if nq + 1 else np.zeros(1, np.uint64)
+        self.query = as_np(r.query, (n,)).copy() if n else np.zeros(0, np.uint32)
+        self.candidate = as_np(r.candidate, (n,)).copy() if n else np.zeros(0, np.uint32)
+        self.prob = as_np(r.prob, (n,)).copy() if n else np.zeros(0, np.float64)
+        self.kind = as_np(r.kind, (n,)).copy() if n else np.zeros(0, np.uint8)
+
+
+class GpuEngine:
+    """Thin owner of one dk_ctx (one pipeline, one device)."""
+
+    def __init__(self, schema, device=0):
+        self.lib = A.load()
+        self.ctx = C.c_void_p()
+        A.check(self.lib.dk_create(C.byref(schema), int(device), C.byref(self.ctx)))
+        self._schema = schema
+
+    def close(self):
+        if self.ctx:
+            self.lib.dk_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def num_rows(self):
+        return int(self.lib.dk_num_rows(self.ctx))
+
+    def upsert(self, n, ident, columns, group=None, deleted=None, keys=None, key_columns=None):
+        """columns: list of A.Column (schema order); keys: uint64 array [nkeys, n] or
+        key_columns: list of A.Column.  Returns the assigned rows."""
+        ident = np.ascontiguousarray(ident, dtype=np.uint64)
+        group = None if group is None else np.ascontiguousarray(group, dtype=np.uint8)
+        deleted = None if deleted is None else np.ascontiguousarray(deleted, dtype=np.uint8)
+        cols = (A.dk_column * max(1, len(columns)))(*[c.c() for c in columns])
+        kc = None
+        kptr = None
+        if keys is not None:
+            keys = np.ascontiguousarray(keys, dtype=np.uint64)
+            kptr = keys.ctypes.data
+        if key_columns is not None:
+            kc = (A.dk_column * max(1, len(key_columns)))(*[c.c() for c in key_columns])
+        b = A.dk_batch(n, ident.ctypes.data, A.ptr(group), A.ptr(deleted), cols, kptr, kc)
+        rows = np.zeros(max(1, n), dtype=np.uint32)
+        A.check(self.lib.dk_upsert(self.ctx, C.byref(b), rows.ctypes.data))
+        return rows[:n]
+
+    def match(self, query_rows):
+        q = np.ascontiguousarray(query_rows, dtype=np.uint32)
+        res = C.POINTER(A.dk_result)()
+        A.check(self.lib.dk_match(self.ctx, q.ctypes.data if q.size else None, q.size, C.byref(res)))
+        try:
+            return MatchResult(res)
+        finally:
+            self.lib.dk_free_result(res)
+
+    def compare_rows(self, r1, r2):
+        out = C.c_double()
+        A.check(self.lib.dk_compare_rows(self.ctx, int(r1), int(r2), C.byref(out)))
+        return out.value
+
+    def set_profiling(self, on):
+        A.check(self.lib.dk_set_profiling(self.ctx, 1 if on else 0))
+
+    def profile(self):
+        p = A.dk_profile()
+        A.check(self.lib.dk_get_profile(self.ctx, C.byref(p)))
+        return p.as_dict()
+
+    def reset_profile(self):
+        A.check(self.lib.dk_reset_profile(self.ctx))
+
+
+class GpuBlockingDatabase:
+    """Duke ``Database`` with key-function blocking, resident in HBM.
+
+    ``index`` buffers records; ``commit`` upserts them (delete-by-ID then add,
+    IncrementalLuceneDatabase.java:516-517, 578-590).  Records marked
+    dukeDeleted=true stay indexed but are never candidates (:478)."""
+
+    def __init__(self, config: DukeConfig, key_functions, mode=None, device=0):
+        self.config = config
+        self.key_functions = list(key_functions)
+        if mode is None:
+            mode = A.MODE_LINKAGE if config.linkage else A.MODE_DEDUP
+        self.mode = mode
+        nkeys = 0 if mode == A.MODE_ALLPAIRS else len(self.key_functions)
+        self.schema, self.props = config.to_schema(mode, nkeys)
+        self.engine = GpuEngine(self.schema, device)
+        self.pending = []
+        self.rows = []          # row -> Record
+        self.by_id = {}         # ID -> row of the live version
+        self._ident = {}        # ID string -> dense identity number
+        self.overwrite = False
+
+    # --- Database API (IncrementalLuceneDatabase.java) ---
+    def set_overwrite(self, overwrite):
+        self.overwrite = bool(overwrite)
+
+    def is_in_memory(self):
+        return True
+
+    def index(self, record: Record):
+        self.pending.append(record)
+
+    def commit(self):
+        recs, self.pending = self.pending, []
+        return self.index_batch(recs)
+
+    def find_record_by_id(self, rid):
+        row = self.by_id.get(rid)
+        return None if row is None else self.rows[row]
+
+    def close(self):
+        self.engine.close()
+
+    # --- bulk path ---
+    def index_batch(self, records):
+        n = len(records)
+        if n == 0:
+            return np.zeros(0, np.uint32)
+        ident = np.empty(n, dtype=np.uint64)
+        for i, r in enumerate(records):
+            rid = r.get_value(ID_PROPERTY)
+            if rid is None:
+                raise ValueError("record without ID property")
+            ident[i] = self._ident.setdefault(rid, len(self._ident))
+        cols = []
+        for p in self.props:
+            vals = []
+            for r in records:
+                vs = r.get_values(p.name)
+                if len(vs) > 1:
+                    raise ValueError(f"property {p.name}: {len(vs)} values (GPU path holds one)")
+                vals.append(vs[0] if vs else None)
+            cols.append(A.Column.from_strings(vals))
+        group = None
+        if self.mode == A.MODE_LINKAGE:
+            group = np.array([int(r.get_value(GROUP_NO_PROPERTY_NAME) or 0) for r in records],
+                             dtype=np.uint8)
+        deleted = np.array([r.get_value(DELETED_PROPERTY_NAME) == "true" for r in records],
+                           dtype=np.uint8)
+        key_cols = None
+        if self.mode != A.MODE_ALLPAIRS:
+            key_cols = [A.Column.from_strings([kf.make_key(r) for r in records])
+                        for kf in self.key_functions]
+        rows = self.engine.upsert(n, ident, cols, group=group, deleted=deleted,
+                                  key_columns=key_cols)
+        for r, row in zip(records, rows):
+            self.rows.append(r)
+            self.by_id[r.get_value(ID_PROPERTY)] = int(row)
+        return rows
+
+
+class GpuProcessor:
+    """``no.priv.garshol.duke.Processor`` with the matching loop on the GPU."""
+
+    def __init__(self, config: DukeConfig, database: GpuBlockingDatabase):
+        self.config = config
+        self.database = database
+        self.listeners = []
+        self.threads = 1
+        self.profiling = False
+
+    def add_match_listener(self, listener):
+        self.listeners.append(listener)
+
+    def get_database(self):
+        return self.database
+
+    def set_threads(self, n):
+        self.threads = int(n)  # the GPU path does not use host threads for matching
+
+    def set_performance_profiling(self, on):
+        self.profiling = bool(on)
+        self.database.engine.set_profiling(on)
+
+    def get_profile(self):
+        return self.database.engine.profile()
+
+    def deduplicate(self, records):
+        """[Duke 1.2] Processor.deduplicate(Collection<Record>): batchReady, index +
+        commit every record, match each against the index (matchall), batchDone."""
+        records = list(records)
+        for l in self.listeners:
+            l.batch_ready(len(records))
+        rows = self.database.index_batch(records)
+        res = self.database.engine.match(rows)
+        self._replay(records, res)
+        for l in self.listeners:
+            l.batch_done()
+        return res
+
+    def _replay(self, records, res: MatchResult):
+        rows = self.database.rows
+        for i, r in enumerate(records):
+            a, b = int(res.first[i]), int(res.first[i + 1])
+            if a == b:
+                for l in self.listeners:
+                    l.no_match_for(r)
+                continue
+            for e in range(a, b):
+                cand = rows[int(res.candidate[e])]
+                p = float(res.prob[e])
+                for l in self.listeners:
+                    if res.kind[e] == A.KIND_MATCH:
+                        l.matches(r, cand, p)
+                    else:
+                        l.matches_perhaps(r, cand, p)
+
+    def compare(self, r1: Record, r2: Record):
+        """[Duke 1.2] Processor.compare for two indexed records."""
+        a = self.database.by_id.get(r1.get_value(ID_PROPERTY))
+        b = self.database.by_id.get(r2.get_value(ID_PROPERTY))
+        if a is None or b is None:
+            raise ValueError("GpuProcessor.compare needs both records indexed")
+        return self.database.engine.compare_rows(a, b)

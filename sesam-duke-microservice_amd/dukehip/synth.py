@@ -1,0 +1,146 @@
+"""Deterministic synthetic person records (SURVEY §8d `synth_persons`).
+
+No dataset can be fetched, so names, streets and cities are built from syllables with a
+seeded PCG64 generator: 5,000 given names (Zipf s=1.1), 20,000 surnames (Zipf s=1.07),
+3,000 streets, 1,000 cities, dob uniform 1930-01-01..2010-12-31.  Duplicates copy an
+original and corrupt each field with p=0.3 by 1-2 edits (substitution / insertion /
+deletion / adjacent swap over a-z); dob gets a day<->month swap with p=0.1.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+
+import numpy as np
+
+from ._abi import Column
+
+SEED = 20261015
+_CONS = list("bcdfghjklmnprstvwz") + ["ch", "sh", "th", "br", "tr", "st", "kr", "gr", "l", "n"]
+_VOW = list("aeiou") + ["ai", "ea", "ou", "ie", "y"]
+_SUFFIX = ["street", "avenue", "road", "lane", "drive", "way", "court", "place", "gate", "vei"]
+
+
+def _vocab(rng, n, syl_lo, syl_hi, cap=True):
+    out, seen = [], set()
+    while len(out) < n:
+        k = int(rng.integers(syl_lo, syl_hi + 1))
+        w = "".join(_CONS[int(rng.integers(len(_CONS)))] + _VOW[int(rng.integers(len(_VOW)))]
+                    for _ in range(k))
+        if rng.random() < 0.4:
+            w += _CONS[int(rng.integers(len(_CONS)))]
+        if w in seen:
+            continue
+        seen.add(w)
+        out.append(w.capitalize() if cap else w)
+    return out
+
+
+def _zipf_choice(rng, n_items, s, size):
+    w = 1.0 / np.arange(1, n_items + 1, dtype=np.float64) ** s
+    w /= w.sum()
+    return rng.choice(n_items, size=size, p=w)
+
+
+def _corrupt(rng, s):
+    """1-2 random edits over a-z."""
+    for _ in range(int(rng.integers(1, 3))):
+        op = int(rng.integers(4))
+        ch = chr(ord("a") + int(rng.integers(26)))
+        if not s:
+            s = ch
+            continue
+        i = int(rng.integers(len(s)))
+        if op == 0:
+            s = s[:i] + ch + s[i + 1:]
+        elif op == 1:
+            s = s[:i] + ch + s[i:]
+        elif op == 2 and len(s) > 1:
+            s = s[:i] + s[i + 1:]
+        elif op == 3 and len(s) > 1:
+            j = min(i + 1, len(s) - 1)
+            i = j - 1
+            s = s[:i] + s[j] + s[i] + s[j + 1:]
+    return s
+
+
+def persons(n_orig, n_dup, seed=SEED, utf16_frac=0.0, shuffle=True):
+    """Returns dict with lists given/surname/name/address/dob and `orig` (index of the
+    original each record duplicates, -1 for originals)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    given_v = _vocab(rng, 5000, 1, 3)
+    sur_v = _vocab(rng, 20000, 2, 3)
+    street_v = _vocab(rng, 3000, 2, 3)
+    city_v = _vocab(rng, 1000, 2, 3)
+    if utf16_frac > 0:
+        # a slice of non-Latin-1 names, one with a surrogate pair (UTF-16 parity cases)
+        k = max(1, int(len(given_v) * utf16_frac))
+        for i in range(k):
+            given_v[-1 - i] = given_v[-1 - i][:-1] + ("ł" if i % 3 else "\U0001F600")
+    gi = _zipf_choice(rng, len(given_v), 1.1, n_orig)
+    si = _zipf_choice(rng, len(sur_v), 1.07, n_orig)
+    num = rng.integers(1, 1000, n_orig)
+    sti = rng.integers(0, len(street_v), n_orig)
+    suf = rng.integers(0, len(_SUFFIX), n_orig)
+    ci = rng.integers(0, len(city_v), n_orig)
+    d0 = _dt.date(1930, 1, 1).toordinal()
+    d1 = _dt.date(2010, 12, 31).toordinal()
+    dob_ord = rng.integers(d0, d1 + 1, n_orig)
+
+    given = [given_v[i] for i in gi]
+    surname = [sur_v[i] for i in si]
+    address = [f"{n} {street_v[s]} {_SUFFIX[x]} {city_v[c]}" for n, s, x, c in zip(num, sti, suf, ci)]
+    dob = [_dt.date.fromordinal(int(o)).isoformat() for o in dob_ord]
+    orig = [-1] * n_orig
+
+    src = rng.integers(0, n_orig, n_dup)
+    for j in range(n_dup):
+        i = int(src[j])
+        g, s, a, d = given[i], surname[i], address[i], dob[i]
+        if rng.random() < 0.3:
+            g = _corrupt(rng, g)
+        if rng.random() < 0.3:
+            s = _corrupt(rng, s)
+        if rng.random() < 0.3:
+            a = _corrupt(rng, a)
+        if rng.random() < 0.1:
+            d = f"{d[:4]}-{d[8:10]}-{d[5:7]}"
+        given.append(g)
+        surname.append(s)
+        address.append(a)
+        dob.append(d)
+        orig.append(i)
+    n = n_orig + n_dup
+    perm = rng.permutation(n) if shuffle else np.arange(n)
+    pick = lambda xs: [xs[i] for i in perm]
+    out = {"given": pick(given), "surname": pick(surname), "address": pick(address),
+           "dob": pick(dob)}
+    inv = np.empty(n, dtype=np.int64)
+    inv[perm] = np.arange(n)
+    o = np.asarray(orig)[perm]
+    out["orig"] = np.where(o >= 0, inv[np.maximum(o, 0)], -1)
+    out["name"] = [f"{g} {s}" for g, s in zip(out["given"], out["surname"])]
+    return out
+
+
+def keys_config2(p):
+    """K1 = surname[0:3] + dob[0:4]; K2 = given[0:2] + dob[5:10]."""
+    k1 = [s[:3] + d[:4] for s, d in zip(p["surname"], p["dob"])]
+    k2 = [g[:2] + d[5:10] for g, d in zip(p["given"], p["dob"])]
+    return [k1, k2]
+
+
+def ascii_column(values):
+    """Fast packing of a list of str (Latin-1 only) into a width-1 Column."""
+    enc = [v.encode("latin-1") for v in values]
+    lens = np.fromiter((len(b) for b in enc), dtype=np.int64, count=len(enc))
+    offs = np.zeros(len(enc) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offs[1:])
+    units = np.frombuffer(b"".join(enc), dtype=np.uint8) if offs[-1] else np.zeros(1, np.uint8)
+    return Column(offs, units)
+
+
+def column(values):
+    try:
+        return ascii_column(values)
+    except UnicodeEncodeError:
+        return Column.from_strings(values)

@@ -1,0 +1,256 @@
+"""GPU parity: libdukehip.so (through its C-ABI) against the CPU oracle on the same
+seeded inputs.  Integers / decisions / candidate sets bit-exact; probabilities compared
+bit-exact as well (same operation order, no FMA) — the north star allows 1e-12 relative.
+
+Oracle: oracle/duke_oracle.c, PARITY UNPINNED against Duke 1.2 itself (see its header).
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+import dukehip as dh
+from dukehip import _abi as A
+from dukehip import synth
+
+pytestmark = pytest.mark.gpu
+
+LEV, JW, QG, EX, NUM = A.CMP_LEVENSHTEIN, A.CMP_JAROWINKLER, A.CMP_QGRAM, A.CMP_EXACT, A.CMP_NUMERIC
+MODES = {"dedup": A.MODE_DEDUP, "linkage": A.MODE_LINKAGE, "allpairs": A.MODE_ALLPAIRS}
+
+
+def schema_of(props, threshold, maybe, mode, nkeys):
+    arr = (A.dk_property * max(1, len(props)))()
+    for i, p in enumerate(props):
+        arr[i] = A.dk_property(p["comparator"], p.get("q", 2), p.get("formula", 0),
+                               p.get("tokenizer", 0), p["low"], p["high"], p.get("min_ratio", 0.0))
+    s = A.dk_schema(len(props), arr, threshold, maybe, MODES[mode], nkeys)
+    s._keep = arr
+    return s
+
+
+def run_both(props, values, keys=(), mode="dedup", group=None, deleted=None, ident=None,
+             threshold=0.9, maybe=0.0, queries=None, batches=None):
+    n = len(values[0])
+    ident = np.arange(n, dtype=np.uint64) if ident is None else np.asarray(ident, np.uint64)
+    eng = dh.GpuEngine(schema_of(props, threshold, maybe, mode, len(keys)))
+    bounds = batches or [(0, n)]
+    for a, b in bounds:
+        eng.upsert(b - a, ident[a:b], [dh.Column.from_strings(v[a:b]) for v in values],
+                   group=None if group is None else np.asarray(group[a:b], np.uint8),
+                   deleted=None if deleted is None else np.asarray(deleted[a:b], np.uint8),
+                   key_columns=[dh.Column.from_strings(k[a:b]) for k in keys] if keys else None)
+    q = np.arange(n, dtype=np.uint32) if queries is None else np.asarray(queries, np.uint32)
+    res = eng.match(q)
+    # oracle: rows superseded by a later upsert of the same identity are not alive
+    alive = np.ones(n, np.uint8)
+    last = {}
+    for r in range(n):
+        if int(ident[r]) in last:
+            alive[last[int(ident[r])]] = 0
+        last[int(ident[r])] = r
+    ot = O.OracleTable(props, values, keys=list(keys), ident=ident, group=group, deleted=deleted,
+                       alive=alive, threshold=threshold, maybe=maybe, mode=mode)
+    ref = ot.match(q)
+    eng.close()
+    return res, ref
+
+
+def assert_same(res, ref):
+    assert res.pairs_scored == ref["pairs_scored"]
+    assert res.n == len(ref["query"])
+    assert np.array_equal(res.query, ref["query"])
+    assert np.array_equal(res.candidate, ref["candidate"])
+    assert np.array_equal(res.kind, ref["kind"])
+    a, b = res.prob, ref["prob"]
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    if not same.all():
+        i = int(np.argmin(same))
+        raise AssertionError(f"prob differs at {i}: {a[i]!r} vs {b[i]!r}")
+
+
+def rand_strings(rng, n, alpha, lo, hi, none_frac=0.0, empty_frac=0.0):
+    out = []
+    for _ in range(n):
+        r = rng.random()
+        if r < none_frac:
+            out.append(None)
+        elif r < none_frac + empty_frac:
+            out.append("")
+        else:
+            out.append("".join(rng.choice(alpha) for _ in range(rng.randint(lo, hi))))
+    return out
+
+
+def allpairs_single(prop, vals):
+    """Every ordered pair through the fused kernel with one property; threshold -1 so
+    every non-NaN probability comes back."""
+    return run_both([prop], [vals], mode="allpairs", threshold=-1.0)
+
+
+@pytest.mark.parametrize("lo,hi", [(1, 3), (1, 16), (10, 32), (30, 64)])
+def test_levenshtein_allpairs(lo, hi):
+    rng = random.Random(lo * 100 + hi)
+    vals = rand_strings(rng, 160, "abcd", lo, hi)
+    res, ref = allpairs_single({"comparator": LEV, "low": 0.1, "high": 0.9}, vals)
+    assert_same(res, ref)
+
+
+def test_levenshtein_quirks():
+    vals = ["a", "b", "ab", "aab", "kitten", "sitting", "x" * 64, "x" * 63 + "y", "abcdefgh",
+            "badcfehg", "zz", "ba"]
+    res, ref = allpairs_single({"comparator": LEV, "low": 0.0, "high": 1.0}, vals)
+    assert_same(res, ref)
+
+
+@pytest.mark.parametrize("alpha", ["ab", "abcdefgh", "abcdefghijklmnopqrstuvwxyz"])
+def test_jarowinkler_allpairs(alpha):
+    rng = random.Random(len(alpha))
+    vals = rand_strings(rng, 150, alpha, 1, 24)
+    res, ref = allpairs_single({"comparator": JW, "low": 0.1, "high": 0.95}, vals)
+    assert_same(res, ref)
+
+
+@pytest.mark.parametrize("q,formula,tok", [(2, 0, 0), (2, 1, 0), (2, 2, 0), (3, 1, 0), (1, 2, 0),
+                                           (4, 0, 0), (2, 0, 1), (3, 2, 1)])
+def test_qgram_allpairs(q, formula, tok):
+    rng = random.Random(q * 10 + formula + 100 * tok)
+    vals = rand_strings(rng, 120, "abc", 0, 12)
+    vals = [v for v in vals if v] + ["a"]
+    res, ref = allpairs_single({"comparator": QG, "low": 0.2, "high": 0.8, "q": q,
+                                "formula": formula, "tokenizer": tok}, vals)
+    assert_same(res, ref)
+
+
+def test_numeric_and_exact():
+    nums = ["1", "2", "0", "-0", "0.0", "-3", "-4.5", "1e3", "1000", "abc", " 7 ", "7f", "NaN",
+            "Infinity", "-Infinity", "0x1p3", "8", "1e", "", "1.", ".5", "0.5d", "3.3", "3.30"]
+    res, ref = allpairs_single({"comparator": NUM, "low": 0.04, "high": 0.73, "min_ratio": 0.0}, nums)
+    assert_same(res, ref)
+    res, ref = allpairs_single({"comparator": NUM, "low": 0.04, "high": 0.73, "min_ratio": 0.7}, nums)
+    assert_same(res, ref)
+    res, ref = allpairs_single({"comparator": EX, "low": 0.3, "high": 0.9}, nums)
+    assert_same(res, ref)
+
+
+def test_utf16_and_surrogates():
+    rng = random.Random(5)
+    alpha = ["a", "b", "ł", "\U0001F600", "é"]
+    vals = ["".join(rng.choice(alpha) for _ in range(rng.randint(1, 10))) for _ in range(80)]
+    for prop in ({"comparator": LEV, "low": 0.1, "high": 0.9},
+                 {"comparator": JW, "low": 0.1, "high": 0.9},
+                 {"comparator": QG, "low": 0.1, "high": 0.9, "q": 2, "formula": 1}):
+        res, ref = allpairs_single(prop, vals)
+        assert_same(res, ref)
+
+
+def test_missing_and_empty_values():
+    rng = random.Random(9)
+    props = [{"comparator": LEV, "low": 0.1, "high": 0.9},
+             {"comparator": JW, "low": 0.2, "high": 0.8},
+             {"comparator": NUM, "low": 0.3, "high": 0.7}]
+    n = 120
+    vals = [rand_strings(rng, n, "ab", 1, 6, none_frac=0.2, empty_frac=0.1),
+            rand_strings(rng, n, "ab", 1, 6, none_frac=0.2, empty_frac=0.1),
+            [None if rng.random() < 0.2 else str(rng.randint(0, 5)) for _ in range(n)]]
+    res, ref = run_both(props, vals, mode="allpairs", threshold=0.6, maybe=0.4)
+    assert_same(res, ref)
+
+
+def persons_case(n_orig, n_dup, seed):
+    p = synth.persons(n_orig, n_dup, seed=seed)
+    props = [{"comparator": JW, "low": 0.1, "high": 0.95},
+             {"comparator": LEV, "low": 0.2, "high": 0.8},
+             {"comparator": LEV, "low": 0.1, "high": 0.85}]
+    return p, props, [p["name"], p["address"], p["dob"]], synth.keys_config2(p)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_dedup_blocking_persons(seed):
+    p, props, vals, keys = persons_case(1500, 500, seed)
+    res, ref = run_both(props, vals, keys, threshold=0.9, maybe=0.7)
+    assert res.n > 0
+    assert_same(res, ref)
+
+
+def test_dedup_deleted_and_upsert_batches():
+    p, props, vals, keys = persons_case(700, 300, 3)
+    n = len(vals[0])
+    rng = np.random.default_rng(3)
+    deleted = (rng.random(n) < 0.05).astype(np.uint8)
+    ident = np.arange(n, dtype=np.uint64)
+    ident[-50:] = ident[:50]   # later batch re-upserts 50 IDs (delete-then-add)
+    res, ref = run_both(props, vals, keys, deleted=deleted, ident=ident, threshold=0.9,
+                        maybe=0.7, batches=[(0, 400), (400, 750), (750, n)],
+                        queries=np.arange(750, n))
+    assert_same(res, ref)
+
+
+def test_linkage_blocking():
+    p, props, vals, keys = persons_case(800, 400, 4)
+    n = len(vals[0])
+    group = np.where(np.arange(n) % 3 == 0, 1, 2).astype(np.uint8)
+    res, ref = run_both(props, vals, keys, mode="linkage", group=group, threshold=0.9, maybe=0.7)
+    assert res.n > 0
+    assert_same(res, ref)
+
+
+def test_allpairs_short_strings():
+    rng = random.Random(11)
+    vals = rand_strings(rng, 400, "abcdefghij", 4, 16)
+    res, ref = run_both([{"comparator": LEV, "low": 0.05, "high": 0.95}], [vals],
+                        mode="allpairs", threshold=0.85)
+    assert_same(res, ref)
+
+
+def test_small_chunks_match_single_chunk(monkeypatch):
+    p, props, vals, keys = persons_case(600, 200, 5)
+    monkeypatch.setenv("DK_CHUNK_SLOTS", "1000")
+    res, ref = run_both(props, vals, keys, threshold=0.9, maybe=0.7)
+    assert_same(res, ref)
+
+
+def test_empty_batch_and_no_candidates():
+    props = [{"comparator": LEV, "low": 0.1, "high": 0.9}]
+    res, ref = run_both(props, [["abc", "abd", "xyz"]], [["k1", "k2", "k3"]])
+    assert res.pairs_scored == 0 and res.n == 0
+    assert_same(res, ref)
+
+
+def test_compare_rows_matches_oracle():
+    p, props, vals, keys = persons_case(50, 20, 6)
+    eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", 2))
+    n = len(vals[0])
+    eng.upsert(n, np.arange(n), [dh.Column.from_strings(v) for v in vals],
+               key_columns=[dh.Column.from_strings(k) for k in keys])
+    ot = O.OracleTable(props, vals, keys=keys)
+    for a, b in [(0, 1), (3, 7), (10, 10), (60, 2)]:
+        assert eng.compare_rows(a, b) == ot.compare_rows(a, b)
+    eng.close()
+
+
+def test_processor_replay_order():
+    """GpuProcessor.deduplicate replays batchReady / per-record callbacks / batchDone."""
+    cfg = dh.DukeConfig([dh.Property("NAME", dh.Comparator("no.priv.garshol.duke.comparators.Levenshtein"), 0.1, 0.9)],
+                        threshold=0.6, maybe_threshold=0.5)
+    recs = [dh.Record({"ID": f"d__{i}", "NAME": v}) for i, v in
+            enumerate(["anna", "anne", "bob", "anna", "annie"])]
+    db = dh.GpuBlockingDatabase(cfg, [dh.PartsKey(("NAME", None, 0, 1))])
+    proc = dh.GpuProcessor(cfg, db)
+    lis = dh.CollectingListener()
+    proc.add_match_listener(lis)
+    proc.deduplicate(recs)
+    ev = lis.events
+    assert ev[0] == ("batchReady", 5) and ev[-1] == ("batchDone",)
+    assert ("noMatchFor", "d__2") in ev
+    qs = [e[1] for e in ev[1:-1]]
+    assert qs == sorted(qs, key=lambda x: int(x.split("__")[1]))  # grouped in batch order
+    db.close()
+
+
+def test_unsupported_levenshtein_length():
+    eng = dh.GpuEngine(schema_of([{"comparator": LEV, "low": 0.1, "high": 0.9}], 0.9, 0.0, "dedup", 1))
+    with pytest.raises(dh.DukeHipError):
+        eng.upsert(1, [0], [dh.Column.from_strings(["x" * 65])], key_columns=[dh.Column.from_strings(["k"])])
+    eng.close()
