@@ -15,6 +15,13 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+
+static double now_ms(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
 
 static inline int imin(int a, int b) { return a < b ? a : b; }
 static inline int imax(int a, int b) { return a > b ? a : b; }
@@ -500,6 +507,7 @@ int dko_match(const dko_schema* s, const dko_table* t, const uint32_t* queries, 
               int nthreads, dko_result* out) {
   memset(out, 0, sizeof(*out));
   if (nthreads < 1) nthreads = 1;
+  const double t0 = now_ms();
   int nk = s->mode == DKO_MODE_ALLPAIRS ? 0 : s->nkeys;
   block_index* bi = (block_index*)calloc((size_t)(nk > 0 ? nk : 1), sizeof(block_index));
   for (int k = 0; k < nk; k++) {
@@ -541,6 +549,7 @@ int dko_match(const dko_schema* s, const dko_table* t, const uint32_t* queries, 
     }
   }
 
+  const double t1 = now_ms();
   work* ws = (work*)calloc((size_t)nthreads, sizeof(work));
   pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
   for (int i = 0; i < nthreads; i++) {
@@ -553,6 +562,9 @@ int dko_match(const dko_schema* s, const dko_table* t, const uint32_t* queries, 
     for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, worker, &ws[i]);
     for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
   }
+  const double t2 = now_ms();
+  out->ms_index = t1 - t0;
+  out->ms_score = t2 - t1;
   uint64_t total = 0;
   for (int i = 0; i < nthreads; i++) { total += ws[i].res.n; out->pairs_scored += ws[i].res.pairs_scored; }
   out->n = total;

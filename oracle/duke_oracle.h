@@ -102,6 +102,8 @@ typedef struct dko_result {
   double* prob;
   uint8_t* kind;
   uint64_t pairs_scored;       /* Processor.compare calls */
+  double ms_index;             /* blocking-index build (wall) */
+  double ms_score;             /* candidate walk + compare + threshold (wall) */
 } dko_result;
 
 /* Processor.deduplicate's match loop for the given query rows (batch order): candidate

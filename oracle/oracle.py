@@ -41,7 +41,8 @@ class Table(C.Structure):
 class Result(C.Structure):
     _fields_ = [("n", C.c_uint64), ("query", C.POINTER(C.c_uint32)),
                 ("candidate", C.POINTER(C.c_uint32)), ("prob", C.POINTER(C.c_double)),
-                ("kind", C.POINTER(C.c_uint8)), ("pairs_scored", C.c_uint64)]
+                ("kind", C.POINTER(C.c_uint8)), ("pairs_scored", C.c_uint64),
+                ("ms_index", C.c_double), ("ms_score", C.c_double)]
 
 
 _lib = None
@@ -169,6 +170,18 @@ class OracleTable:
         self.schema = Schema(len(props), self.props, threshold, maybe, MODE[mode], len(keys))
 
         def pack(col):
+            if all(v is not None for v in col):
+                try:  # fast path: Latin-1 strings
+                    enc = [v.encode("latin-1") for v in col]
+                    lens = np.fromiter((len(b) for b in enc), dtype=np.int64, count=n)
+                    offs = np.zeros(n + 1, dtype=np.uint32)
+                    np.cumsum(lens, out=offs[1:])
+                    chars = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8).astype(np.uint16)
+                    pres = np.ones(n, dtype=np.uint8)
+                    self._keep += [offs, chars, pres]
+                    return offs, chars, pres
+                except (UnicodeEncodeError, AttributeError):
+                    pass
             offs = np.zeros(n + 1, dtype=np.uint32)
             parts = []
             pres = np.zeros(n, dtype=np.uint8)
@@ -227,6 +240,8 @@ class OracleTable:
             "prob": np.ctypeslib.as_array(res.prob, (n,)).copy() if n else np.zeros(0, np.float64),
             "kind": np.ctypeslib.as_array(res.kind, (n,)).copy() if n else np.zeros(0, np.uint8),
             "pairs_scored": res.pairs_scored,
+            "ms_index": res.ms_index,
+            "ms_score": res.ms_score,
         }
         lib().dko_free_result(C.byref(res))
         return out
