@@ -92,24 +92,34 @@ def main():
     q0, q1 = n * rank // world, n * (rank + 1) // world
     queries = np.arange(q0, q1, dtype=np.uint32)
 
+    nq_max = max(n * (r + 1) // world - n * r // world for r in range(world))
+
     def step():
-        res = eng.match(queries)
-        scored = res.pairs_scored
-        if dist is not None:
-            # RCCL: all-gather per-rank counts, then gather match lists to rank 0
-            cnt = torch.tensor([res.n, scored], dtype=torch.int64, device=dev)
-            allc = [torch.zeros_like(cnt) for _ in range(world)]
-            dist.all_gather(allc, cnt)
-            mx = int(max(int(c[0]) for c in allc))
-            buf = torch.zeros((max(mx, 1), 3), dtype=torch.int64, device=dev)
-            if res.n:
-                packed = np.stack([res.query.astype(np.int64) << 32 | res.candidate.astype(np.int64),
-                                   res.prob.view(np.int64), res.kind.astype(np.int64)], 1)
-                buf[:res.n] = torch.from_numpy(packed).to(dev)
-            gath = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
-            dist.gather(buf, gath, dst=0)
-            scored = int(sum(int(c[1]) for c in allc))
-        return res, scored
+        if dist is None:
+            res = eng.match(queries)          # entries land in pinned host memory
+            return res, res.pairs_scored
+        # N>1: entries stay in HBM; RCCL all-gathers the per-rank counts, then gathers
+        # every rank's match list (first / candidate / prob / kind) to rank 0 over xGMI,
+        # which moves the node's list to the host.
+        res = eng.match(queries, on_device=True)
+        cnt = torch.tensor([res.n, res.pairs_scored], dtype=torch.int64, device=dev)
+        allc = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(allc, cnt)
+        mx = max(1, int(max(int(c[0]) for c in allc)))
+        first = torch.zeros(nq_max + 1, dtype=torch.int64, device=dev)
+        cand = torch.zeros(mx, dtype=torch.int32, device=dev)
+        prob = torch.zeros(mx, dtype=torch.float64, device=dev)
+        kind = torch.zeros(mx, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        res.copy_to_device(first.data_ptr(), cand.data_ptr(), prob.data_ptr(), kind.data_ptr())
+        for t in (first, cand, prob, kind):
+            lst = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+            dist.gather(t, lst, dst=0)
+            if rank == 0:
+                for r, g in enumerate(lst):
+                    g[: (int(allc[r][0]) if t is not first else nq_max + 1)].cpu()
+        res.close()
+        return res, int(sum(int(c[1]) for c in allc))
 
     for _ in range(args.warmup):
         step()
@@ -204,7 +214,8 @@ def cpu_baseline(p, keys, order, spec, gpu_res, args):
     s = int(min(n, max(probe, args.cpu_seconds * rate / max(per_q, 1e-9))))
     r = ot.match(np.arange(s, dtype=np.uint32), nthreads=threads)
     e = int(gpu_res.first[s])
-    ok = (np.array_equal(r["query"], gpu_res.query[:e]) and np.array_equal(r["candidate"], gpu_res.candidate[:e])
+    gq = np.repeat(np.arange(s, dtype=np.uint32), np.diff(gpu_res.first[: s + 1]).astype(np.int64))
+    ok = (np.array_equal(r["query"], gq) and np.array_equal(r["candidate"], gpu_res.candidate[:e])
           and np.array_equal(r["prob"], gpu_res.prob[:e]) and np.array_equal(r["kind"], gpu_res.kind[:e]))
     cpu = ""
     try:

@@ -20,7 +20,8 @@
  *                       key-function blocking contract of SURVEY §8a-5, then
  *                       Processor.compareCandidatesSimple -> compare -> threshold.
  *   dk_result        <- the MatchListener callbacks (BaseLinkDatabaseMatchListener.java:53-109):
- *                       entries grouped per query in batch order, candidate order inside.
+ *                       entries grouped per query in batch order, candidate order inside;
+ *                       result memory is pooled per ctx and recycled by dk_free_result.
  *   dk_compare_rows  <- `Processor.compare(Record, Record)` for one pair.
  *   dk_set_profiling <- `Processor.setPerformanceProfiling` (App.java:345, 466).
  *   dk_last_error    <- DukeException / RuntimeException text (App.java:1007-1009).
@@ -113,16 +114,25 @@ typedef struct dk_batch {
   const dk_column* key_columns;
 } dk_batch;
 
+/* dk_match flags */
+#define DK_MATCH_HOST 0   /* entries copied to (pinned) host memory: first/candidate/prob/kind */
+#define DK_MATCH_DEVICE 1 /* entries stay in HBM only (host arrays NULL); fetch them with
+                             dk_result_copy_to_device, e.g. into buffers an RCCL gather sends */
+
+/* Match list of one dk_match call, grouped per query record in query order; inside a
+ * query, candidates in key-function order then index order (SURVEY §8a-5 contract).
+ * Entry e of query i (first[i] <= e < first[i+1]) is one MatchListener callback
+ * matches(r1 = query_rows[i], r2 = candidate[e], prob[e]) or matchesPerhaps(...);
+ * a query with no entry gets noMatchFor(r1). */
 typedef struct dk_result {
-  uint64_t nqueries;       /* queries passed to dk_match */
-  const uint64_t* first;   /* nqueries+1: entries of query i are [first[i], first[i+1]) */
-  uint64_t n;              /* match + maybe entries */
-  const uint32_t* query;   /* row of r1 (the query record) */
+  uint64_t nqueries;         /* queries passed to dk_match */
+  uint64_t n;                /* match + maybe entries */
+  const uint64_t* first;     /* nqueries+1 entry offsets */
   const uint32_t* candidate; /* row of r2 */
-  const double* prob;      /* Processor.compare(r1, r2) */
-  const uint8_t* kind;     /* DK_KIND_MATCH / DK_KIND_MAYBE */
-  uint64_t pairs_scored;   /* Processor.compare calls made (candidates after filters) */
-  uint64_t pairs_generated; /* candidate slots produced by blocking, before filters */
+  const double* prob;        /* Processor.compare(r1, r2) */
+  const uint8_t* kind;       /* DK_KIND_MATCH / DK_KIND_MAYBE */
+  uint64_t pairs_scored;     /* Processor.compare calls made (candidates after filters) */
+  uint64_t pairs_generated;  /* candidate slots produced by blocking, before filters */
 } dk_result;
 
 typedef struct dk_profile {
@@ -142,7 +152,11 @@ typedef struct dk_ctx dk_ctx;
 int dk_create(const dk_schema* schema, int device, dk_ctx** out);
 void dk_destroy(dk_ctx* ctx);
 int dk_upsert(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
-int dk_match(dk_ctx* ctx, const uint32_t* query_rows, uint64_t nq, dk_result** out);
+int dk_match(dk_ctx* ctx, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out);
+/* device-to-device copy of a result's entries (any of the pointers may be NULL); the
+ * destination buffers live on the ctx's device */
+int dk_result_copy_to_device(const dk_result* result, uint64_t* first, uint32_t* candidate,
+                             double* prob, uint8_t* kind);
 void dk_free_result(dk_result* result);
 int dk_compare_rows(dk_ctx* ctx, uint32_t r1, uint32_t r2, double* prob);
 uint64_t dk_num_rows(const dk_ctx* ctx);

@@ -11,6 +11,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -190,12 +192,35 @@ struct PropState {
   DevBuf off, len, units, num, numok, goff, gcnt, grams;
 };
 
+// Result memory (device list + pinned host copy), pooled per ctx and handed back by
+// dk_free_result, so steady-state batches allocate nothing.
+struct ResultBufs {
+  DevBuf d_cand, d_kind, d_prob, d_qidx, d_first;
+  PinnedBuf h_first, h_cand, h_prob, h_kind;
+};
+
+struct ResultPool {
+  std::mutex m;
+  std::vector<std::unique_ptr<ResultBufs>> free;
+  std::unique_ptr<ResultBufs> take() {
+    std::lock_guard<std::mutex> g(m);
+    if (free.empty()) return std::unique_ptr<ResultBufs>(new ResultBufs());
+    auto b = std::move(free.back());
+    free.pop_back();
+    return b;
+  }
+  void give(std::unique_ptr<ResultBufs> b) {
+    std::lock_guard<std::mutex> g(m);
+    if (free.size() < 4) free.push_back(std::move(b));
+  }
+};
+
 struct ResultHolder {
-  dk_result r{};
-  std::vector<uint64_t> first;
-  std::vector<uint32_t> query, candidate;
-  std::vector<double> prob;
-  std::vector<uint8_t> kind;
+  dk_result r{};  // first member: dk_result* <-> ResultHolder*
+  std::shared_ptr<ResultPool> pool;
+  std::unique_ptr<ResultBufs> bufs;
+  int device = 0;
+  hipStream_t stream = nullptr;
 };
 
 struct dk_ctx {
@@ -212,10 +237,9 @@ struct dk_ctx {
   // match scratch
   DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], srows[kMaxKeys], sgroup[kMaxKeys];
   DevBuf ranges, counts, qoff, pq, pc, tmp;
-  DevBuf m_counters, m_slot, m_qidx, m_cand, m_prob, m_kind;
-  DevBuf s_slot, s_perm_in, s_perm, f_qidx, f_cand, f_prob, f_kind;
-  PinnedBuf h_counters;
-  uint64_t match_cap = 1u << 20;
+  DevBuf counters, st_bcnt, st_boff, st_prob, st_cand, st_qidx;
+  PinnedBuf h_small;
+  std::shared_ptr<ResultPool> pool = std::make_shared<ResultPool>();
   // profiling (Processor.setPerformanceProfiling)
   bool profiling = false;
   dk_profile prof{};
@@ -318,8 +342,8 @@ int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
     delete c;
     return fail(DK_E_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
   }
-  if (c->m_counters.reserve(4 * sizeof(uint64_t), 0, c->stream) != hipSuccess ||
-      c->h_counters.reserve(4 * sizeof(uint64_t)) != hipSuccess) {
+  if (c->counters.reserve(4 * sizeof(uint64_t), 0, c->stream) != hipSuccess ||
+      c->h_small.reserve(64) != hipSuccess) {
     delete c;
     return fail(DK_E_DEVICE, "counter allocation failed");
   }
@@ -653,7 +677,8 @@ static int build_usable(dk_ctx* c, uint64_t* m_out) {
   return DK_OK;
 }
 
-static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, ResultHolder* R) {
+static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
+                     ResultHolder* R) {
   hipStream_t s = c->stream;
   const bool prof = c->profiling;
   const auto t0 = std::chrono::steady_clock::now();
@@ -695,8 +720,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, ResultH
 
   // ---- candidate counts per query -> slot offsets ----
   Timer t_gen(prof, s);
-  std::vector<uint64_t>& qoff = R->first;  // reused: slot offsets first, entry offsets later
-  qoff.assign(nq + 1, 0);
+  std::vector<uint64_t> qoff(nq + 1, 0);
   uint64_t total = 0;
   if (!allpairs) {
     HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
@@ -717,116 +741,115 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, ResultH
   c->prof.ms_generate += t_gen.stop();
 
   const ScoreParams P = make_params(c);
-  const uint64_t CH = chunk_slots();
+  const uint64_t CH = (chunk_slots() + kScoreBlock - 1) / kScoreBlock * kScoreBlock;
+  const uint64_t chunk = std::min(CH, std::max<uint64_t>(total, 1));
+  const uint64_t nblk_max = (chunk + kScoreBlock - 1) / kScoreBlock;
   if (!allpairs) {
-    HIPCHK(c->pq.reserve(std::min(CH, total) * 4 + 4, 0, s));
-    HIPCHK(c->pc.reserve(std::min(CH, total) * 4 + 4, 0, s));
+    HIPCHK(c->pq.reserve(chunk * 4 + 4, 0, s));
+    HIPCHK(c->pc.reserve(chunk * 4 + 4, 0, s));
   }
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    HIPCHK(c->m_slot.reserve(c->match_cap * 8, 0, s));
-    HIPCHK(c->m_qidx.reserve(c->match_cap * 4, 0, s));
-    HIPCHK(c->m_cand.reserve(c->match_cap * 4, 0, s));
-    HIPCHK(c->m_prob.reserve(c->match_cap * 8, 0, s));
-    HIPCHK(c->m_kind.reserve(c->match_cap, 0, s));
-    HIPCHK(hipMemsetAsync(c->m_counters.p, 0, 4 * sizeof(uint64_t), s));
-    MatchOut out{c->m_counters.as<uint64_t>(), c->match_cap, c->m_slot.as<uint64_t>(),
-                 c->m_qidx.as<uint32_t>(), c->m_cand.as<uint32_t>(), c->m_prob.as<double>(),
-                 c->m_kind.as<uint8_t>()};
-    for (uint64_t s0 = 0; s0 < total; s0 += CH) {
-      const uint64_t s1 = std::min(total, s0 + CH);
-      PairSource src{};
-      src.queries = c->d_queries.as<uint32_t>();
-      if (allpairs) {
-        src.allpairs = 1;
-        src.usable = c->usable.as<uint32_t>();
-        src.m = M;
-      } else {
-        Timer t_emit(prof, s);
-        const uint64_t q0 = (uint64_t)(std::upper_bound(qoff.begin(), qoff.end(), s0) - qoff.begin()) - 1;
-        const uint64_t q1 = (uint64_t)(std::lower_bound(qoff.begin(), qoff.end(), s1) - qoff.begin());
-        HIPCHK(launch_emit(c->d_queries.as<uint32_t>(), q0, std::min(q1, nq), c->qoff.as<uint64_t>(),
-                           c->ranges.as<uint2>(), nq, T, c->ident.as<uint64_t>(), s0, s1,
-                           c->pq.as<uint32_t>(), c->pc.as<uint32_t>(), s));
-        c->prof.ms_generate += t_emit.stop();
-        src.pq = c->pq.as<uint32_t>();
-        src.pc = c->pc.as<uint32_t>();
-      }
-      Timer t_score(prof, s);
-      HIPCHK(launch_score(P, src, s0, s1 - s0, out, s));
-      c->prof.ms_score += t_score.stop();
-      c->prof.score_launches += 1;
+  HIPCHK(c->st_bcnt.reserve(nblk_max * 4 + 4, 0, s));
+  HIPCHK(c->st_boff.reserve(nblk_max * 8 + 8, 0, s));
+  HIPCHK(c->st_prob.reserve(nblk_max * kScoreBlock * 8, 0, s));
+  HIPCHK(c->st_cand.reserve(nblk_max * kScoreBlock * 4, 0, s));
+  HIPCHK(c->st_qidx.reserve(nblk_max * kScoreBlock * 4, 0, s));
+  HIPCHK(hipMemsetAsync(c->counters.p, 0, 4 * sizeof(uint64_t), s));
+  StageOut st{c->counters.as<uint64_t>(), c->st_bcnt.as<uint32_t>(), c->st_prob.as<double>(),
+              c->st_cand.as<uint32_t>(), c->st_qidx.as<uint32_t>()};
+  ResultBufs& B = *R->bufs;
+  uint64_t nm = 0;  // entries so far
+  for (uint64_t s0 = 0; s0 < total; s0 += CH) {
+    const uint64_t s1 = std::min(total, s0 + CH);
+    const uint64_t nblk = (s1 - s0 + kScoreBlock - 1) / kScoreBlock;
+    PairSource src{};
+    src.queries = c->d_queries.as<uint32_t>();
+    if (allpairs) {
+      src.allpairs = 1;
+      src.usable = c->usable.as<uint32_t>();
+      src.m = M;
+    } else {
+      Timer t_emit(prof, s);
+      const uint64_t q0 = (uint64_t)(std::upper_bound(qoff.begin(), qoff.end(), s0) - qoff.begin()) - 1;
+      const uint64_t q1 = (uint64_t)(std::lower_bound(qoff.begin(), qoff.end(), s1) - qoff.begin());
+      HIPCHK(launch_emit(c->d_queries.as<uint32_t>(), q0, std::min(q1, nq), c->qoff.as<uint64_t>(),
+                         c->ranges.as<uint2>(), nq, T, c->ident.as<uint64_t>(), s0, s1,
+                         c->pq.as<uint32_t>(), c->pc.as<uint32_t>(), s));
+      c->prof.ms_generate += t_emit.stop();
+      src.pq = c->pq.as<uint32_t>();
+      src.pc = c->pc.as<uint32_t>();
     }
-    HIPCHK(hipMemcpyAsync(c->h_counters.p, c->m_counters.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    const uint64_t* hc = c->h_counters.as<uint64_t>();
-    if (hc[0] <= c->match_cap) break;
-    if (attempt == 1) return fail(DK_E_STATE, "match list overflow after resize");
-    c->match_cap = hc[0] + hc[0] / 4 + 1024;  // rerun with room for every entry
-  }
-  const uint64_t* hc = c->h_counters.as<uint64_t>();
-  const uint64_t nm = hc[0];
-  R->r.pairs_scored = hc[1];
-  R->r.pairs_generated = total;
-  c->prof.pairs_scored += hc[1];
-  c->prof.pairs_generated += total;
-  c->prof.score_bytes += hc[2];
-
-  // ---- gather: order entries by slot (= query order, key fn, candidate order) ----
-  Timer t_gather(prof, s);
-  R->query.resize(nm);
-  R->candidate.resize(nm);
-  R->prob.resize(nm);
-  R->kind.resize(nm);
-  std::vector<uint32_t> qidx(nm);
-  if (nm) {
-    HIPCHK(c->s_slot.reserve(nm * 8, 0, s));
-    HIPCHK(c->s_perm_in.reserve(nm * 4, 0, s));
-    HIPCHK(c->s_perm.reserve(nm * 4, 0, s));
-    HIPCHK(c->f_qidx.reserve(nm * 4, 0, s));
-    HIPCHK(c->f_cand.reserve(nm * 4, 0, s));
-    HIPCHK(c->f_prob.reserve(nm * 8, 0, s));
-    HIPCHK(c->f_kind.reserve(nm, 0, s));
-    HIPCHK(launch_iota_u32(c->s_perm_in.as<uint32_t>(), nm, s));
+    Timer t_score(prof, s);
+    HIPCHK(launch_score(P, src, s0, s1 - s0, st, s));
+    c->prof.ms_score += t_score.stop();
+    c->prof.score_launches += 1;
+    // block-ordered compaction of this chunk's entries onto the match list
+    Timer t_gather(prof, s);
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
-      return sort_pairs_u64_u32(t, b, c->m_slot.as<uint64_t>(), c->s_slot.as<uint64_t>(),
-                                c->s_perm_in.as<uint32_t>(), c->s_perm.as<uint32_t>(), nm, s);
+      return exclusive_scan_u32_u64(t, b, c->st_bcnt.as<uint32_t>(), c->st_boff.as<uint64_t>(), nblk, s);
     }));
-    MatchOut in{nullptr, 0, nullptr, c->m_qidx.as<uint32_t>(), c->m_cand.as<uint32_t>(),
-                c->m_prob.as<double>(), c->m_kind.as<uint8_t>()};
-    HIPCHK(launch_gather_matches(c->s_perm.as<uint32_t>(), nm, in, c->f_qidx.as<uint32_t>(),
-                                 c->f_cand.as<uint32_t>(), c->f_prob.as<double>(), c->f_kind.as<uint8_t>(), s));
-    HIPCHK(hipMemcpyAsync(qidx.data(), c->f_qidx.p, nm * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(R->candidate.data(), c->f_cand.p, nm * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(R->prob.data(), c->f_prob.p, nm * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(R->kind.data(), c->f_kind.p, nm, hipMemcpyDeviceToHost, s));
+    uint64_t* hs = c->h_small.as<uint64_t>();
+    hs[1] = 0;
+    HIPCHK(hipMemcpyAsync(&hs[0], c->st_boff.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&hs[1], c->st_bcnt.as<uint32_t>() + nblk - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint64_t add = hs[0] + (hs[1] & 0xFFFFFFFFu);
+    if (add) {
+      const uint64_t need = nm + add;
+      HIPCHK(B.d_cand.reserve(need * 4, nm * 4, s));
+      HIPCHK(B.d_kind.reserve(need, nm, s));
+      HIPCHK(B.d_prob.reserve(need * 8, nm * 8, s));
+      HIPCHK(B.d_qidx.reserve(need * 4, nm * 4, s));
+      MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(),
+                   B.d_qidx.as<uint32_t>()};
+      HIPCHK(launch_compact(st, c->st_boff.as<uint64_t>(), nblk, nm, ml, s));
+      nm = need;
+    }
+    c->prof.ms_gather += t_gather.stop();
+  }
+  HIPCHK(hipMemcpyAsync(c->h_small.p, c->counters.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint64_t scored = c->h_small.as<uint64_t>()[0];
+  const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
+  R->r.pairs_scored = scored;
+  R->r.pairs_generated = total;
+  c->prof.pairs_scored += scored;
+  c->prof.pairs_generated += total;
+  c->prof.score_bytes += sbytes;
+
+  // ---- per-query entry offsets, then (DK_MATCH_HOST) the copy into pinned host memory ----
+  Timer t_gather(prof, s);
+  HIPCHK(B.d_first.reserve((nq + 1) * 8, 0, s));
+  HIPCHK(launch_first(B.d_qidx.as<uint32_t>(), nm, nq, B.d_first.as<uint64_t>(), s));
+  R->r.nqueries = nq;
+  R->r.n = nm;
+  if (!(flags & DK_MATCH_DEVICE)) {
+    HIPCHK(B.h_first.reserve((nq + 1) * 8));
+    HIPCHK(B.h_cand.reserve(nm * 4 + 4));
+    HIPCHK(B.h_prob.reserve(nm * 8 + 8));
+    HIPCHK(B.h_kind.reserve(nm + 1));
+    HIPCHK(hipMemcpyAsync(B.h_first.p, B.d_first.p, (nq + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (nm) {
+      HIPCHK(hipMemcpyAsync(B.h_cand.p, B.d_cand.p, nm * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(B.h_prob.p, B.d_prob.p, nm * 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(B.h_kind.p, B.d_kind.p, nm, hipMemcpyDeviceToHost, s));
+    }
+    R->r.first = B.h_first.as<uint64_t>();
+    R->r.candidate = B.h_cand.as<uint32_t>();
+    R->r.prob = B.h_prob.as<double>();
+    R->r.kind = B.h_kind.as<uint8_t>();
   }
   HIPCHK(hipStreamSynchronize(s));
-  // entry offsets per query (entries are grouped by query index, ascending)
-  std::vector<uint64_t>& first = R->first;
-  first.assign(nq + 1, 0);
-  for (uint64_t i = 0; i < nm; ++i) {
-    first[qidx[i] + 1]++;
-    R->query[i] = query_rows[qidx[i]];
-  }
-  for (uint64_t i = 0; i < nq; ++i) first[i + 1] += first[i];
   c->prof.ms_gather += t_gather.stop();
-
-  R->r.nqueries = nq;
-  R->r.first = first.data();
-  R->r.n = nm;
-  R->r.query = R->query.data();
-  R->r.candidate = R->candidate.data();
-  R->r.prob = R->prob.data();
-  R->r.kind = R->kind.data();
   c->prof.ms_total +=
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return DK_OK;
 }
 
-int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, dk_result** out) {
+int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out) {
   if (!c || !out) return fail(DK_E_INVALID, "NULL argument");
   *out = nullptr;
   if (nq && !query_rows) return fail(DK_E_INVALID, "query_rows is NULL");
+  if (flags & ~DK_MATCH_DEVICE) return fail(DK_E_INVALID, "unknown flags 0x%x", flags);
   for (uint64_t i = 0; i < nq; ++i)
     if (query_rows[i] >= c->nrows)
       return fail(DK_E_INVALID, "query row %u not in the index (%llu rows)", query_rows[i],
@@ -835,8 +858,13 @@ int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, dk_result** out
   HIPCHK(hipSetDevice(c->device));
   ResultHolder* R = new (std::nothrow) ResultHolder();
   if (!R) return fail(DK_E_NOMEM, "out of host memory");
-  int rc = run_match(c, query_rows, nq, R);
+  R->pool = c->pool;
+  R->bufs = c->pool->take();
+  R->device = c->device;
+  R->stream = c->stream;
+  int rc = run_match(c, query_rows, nq, flags, R);
   if (rc) {
+    R->pool->give(std::move(R->bufs));
     delete R;
     return rc;
   }
@@ -844,9 +872,29 @@ int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, dk_result** out
   return DK_OK;
 }
 
+int dk_result_copy_to_device(const dk_result* r, uint64_t* first, uint32_t* candidate,
+                             double* prob, uint8_t* kind) {
+  if (!r) return fail(DK_E_INVALID, "result is NULL");
+  const ResultHolder* R = reinterpret_cast<const ResultHolder*>(r);
+  HIPCHK(hipSetDevice(R->device));
+  const ResultBufs& B = *R->bufs;
+  hipStream_t s = R->stream;
+  if (first) HIPCHK(hipMemcpyAsync(first, B.d_first.p, (r->nqueries + 1) * 8, hipMemcpyDeviceToDevice, s));
+  if (r->n) {
+    if (candidate) HIPCHK(hipMemcpyAsync(candidate, B.d_cand.p, r->n * 4, hipMemcpyDeviceToDevice, s));
+    if (prob) HIPCHK(hipMemcpyAsync(prob, B.d_prob.p, r->n * 8, hipMemcpyDeviceToDevice, s));
+    if (kind) HIPCHK(hipMemcpyAsync(kind, B.d_kind.p, r->n, hipMemcpyDeviceToDevice, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  return DK_OK;
+}
+
 void dk_free_result(dk_result* r) {
   if (!r) return;
-  delete reinterpret_cast<ResultHolder*>(r);  // dk_result is the first member
+  ResultHolder* R = reinterpret_cast<ResultHolder*>(r);  // dk_result is the first member
+  (void)hipSetDevice(R->device);
+  R->pool->give(std::move(R->bufs));
+  delete R;
 }
 
 int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
@@ -854,16 +902,15 @@ int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
   if (r1 >= c->nrows || r2 >= c->nrows) return fail(DK_E_INVALID, "row out of range");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  DevBuf buf;
-  HIPCHK(buf.reserve(256, 0, s));
+  DevBuf buf;  // [0..2] query row, query index, candidate; staging for one block after
+  HIPCHK(buf.reserve(4096, 0, s));
   uint32_t host[3] = {r1, 0u, r2};
+  HIPCHK(hipMemsetAsync(buf.p, 0, 4096, s));
   HIPCHK(hipMemcpyAsync(buf.p, host, sizeof host, hipMemcpyHostToDevice, s));
-  uint64_t* counters = reinterpret_cast<uint64_t*>(buf.as<uint8_t>() + 64);
-  HIPCHK(hipMemsetAsync(counters, 0, 64, s));
-  uint8_t* base = buf.as<uint8_t>() + 128;
-  MatchOut out{counters, 1, reinterpret_cast<uint64_t*>(base), reinterpret_cast<uint32_t*>(base + 8),
-               reinterpret_cast<uint32_t*>(base + 12), reinterpret_cast<double*>(base + 16),
-               base + 24};
+  uint8_t* base = buf.as<uint8_t>();
+  StageOut st{reinterpret_cast<uint64_t*>(base + 64), reinterpret_cast<uint32_t*>(base + 96),
+              reinterpret_cast<double*>(base + 128), reinterpret_cast<uint32_t*>(base + 2176),
+              reinterpret_cast<uint32_t*>(base + 3200)};
   ScoreParams P = make_params(c);
   P.threshold = -INFINITY;  // every non-NaN probability is emitted
   P.maybe = 0.0;
@@ -871,13 +918,12 @@ int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
   src.queries = buf.as<uint32_t>();
   src.pq = buf.as<uint32_t>() + 1;
   src.pc = buf.as<uint32_t>() + 2;
-  HIPCHK(launch_score(P, src, 0, 1, out, s));
-  uint64_t n = 0;
+  HIPCHK(launch_score(P, src, 0, 1, st, s));
+  uint32_t n = 0;
   double p = NAN;
-  HIPCHK(hipMemcpyAsync(&n, counters, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&p, base + 16, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&n, base + 96, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&p, base + 128, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   *prob = n ? p : NAN;
   return DK_OK;
 }
-

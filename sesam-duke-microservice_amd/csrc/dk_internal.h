@@ -57,14 +57,26 @@ struct PairSource {
   int32_t allpairs;
 };
 
-struct MatchOut {
-  uint64_t* counters;  // [0] entries, [1] pairs scored, [2] operand bytes
-  uint64_t cap;
-  uint64_t* slot;      // global slot index (sort key: query order, key fn, candidate order)
-  uint32_t* qidx;      // query index
-  uint32_t* cand;      // candidate row
+// Per-chunk staging of the score kernel.  Block b (256 slots) writes its emitted entries,
+// in slot order, to [b*256, b*256 + bcnt[b]); k_compact then concatenates the blocks in
+// block order, so the final list is in slot order (query, key function, candidate)
+// without a sort or any atomic on the entries.
+constexpr int kScoreBlock = 256;
+constexpr int kKindShift = 30;  // staged candidate word = row | kind << 30
+struct StageOut {
+  uint64_t* counters;  // [0] pairs scored, [1] operand bytes
+  uint32_t* bcnt;      // per block: emitted entries
   double* prob;
+  uint32_t* cand;
+  uint32_t* qidx;
+};
+
+// Device-resident match list of one dk_match call.
+struct MatchList {
+  uint32_t* cand;
   uint8_t* kind;
+  double* prob;
+  uint32_t* qidx;
 };
 
 // ---- launchers (dk_kernels.hip) ----
@@ -99,12 +111,13 @@ hipError_t launch_emit(const uint32_t* queries, uint64_t q0, uint64_t q1, const 
                        const uint64_t* ident, uint64_t s0, uint64_t s1, uint32_t* pq,
                        uint32_t* pc, hipStream_t s);
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
-                        uint64_t nslots, const MatchOut& out, hipStream_t s);
+                        uint64_t nslots, const StageOut& out, hipStream_t s);
+hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nblocks,
+                          uint64_t base, const MatchList& out, hipStream_t s);
+hipError_t launch_first(const uint32_t* qidx, uint64_t n, uint64_t nq, uint64_t* first,
+                        hipStream_t s);
 hipError_t launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s);
 hipError_t launch_iota_u32(uint32_t* p, uint64_t n, hipStream_t s);
-hipError_t launch_gather_matches(const uint32_t* perm, uint64_t n, const MatchOut& in,
-                                 uint32_t* qidx, uint32_t* cand, double* prob, uint8_t* kind,
-                                 hipStream_t s);
 
 // rocPRIM wrappers (dk_kernels.hip)
 hipError_t sort_pairs_u64_u32(void* tmp, size_t& tmp_bytes, const uint64_t* kin, uint64_t* kout,
@@ -113,5 +126,7 @@ hipError_t exclusive_scan_u64(void* tmp, size_t& tmp_bytes, const uint64_t* in, 
                               uint64_t n, hipStream_t s);
 hipError_t exclusive_scan_u32(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint32_t* out,
                               uint64_t n, hipStream_t s);
+hipError_t exclusive_scan_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint64_t* out,
+                                  uint64_t n, hipStream_t s);
 
 }  // namespace dk

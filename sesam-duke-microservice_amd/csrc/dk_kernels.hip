@@ -205,7 +205,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint32_t q, uint3
 }
 
 __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSource S,
-                                               uint64_t slot0, uint64_t nslots, MatchOut out) {
+                                               uint64_t slot0, uint64_t nslots, StageOut out) {
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = idx < nslots;
   uint32_t qi = 0, q = 0, c = 0;
@@ -263,38 +263,71 @@ __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSo
   }
 
   // [Duke 1.2] Processor.compareCandidatesSimple: strict thresholds
-  uint8_t kind = 0;
+  uint32_t kind = 0;
   if (valid) {
     if (prob > P.threshold) kind = DK_KIND_MATCH;
     else if (P.maybe != 0.0 && prob > P.maybe) kind = DK_KIND_MAYBE;
   }
 
-  // wave-ballot compaction of the emitted entries; one atomic per wave
+  // block-ordered compaction: wave ballots -> per-wave counts in LDS -> slot-ordered
+  // entries at the block's staging region; no atomics on entries
+  __shared__ uint32_t wcount[kScoreBlock / 64];
   const uint64_t em = __ballot(kind != 0);
   const uint64_t vm = __ballot(valid);
+  const uint32_t wave = threadIdx.x >> 6;
   uint32_t wbytes = bytes;
   for (int o = 32; o > 0; o >>= 1) wbytes += __shfl_xor(wbytes, o);
-  uint64_t base = 0;
   if (lane_id() == 0) {
-    if (em) base = atomicAdd((unsigned long long*)&out.counters[0], (unsigned long long)__popcll(em));
+    wcount[wave] = (uint32_t)__popcll(em);
     if (vm) {
-      atomicAdd((unsigned long long*)&out.counters[1], (unsigned long long)__popcll(vm));
-      atomicAdd((unsigned long long*)&out.counters[2], (unsigned long long)wbytes);
+      atomicAdd((unsigned long long*)&out.counters[0], (unsigned long long)__popcll(vm));
+      atomicAdd((unsigned long long*)&out.counters[1], (unsigned long long)wbytes);
     }
   }
-  if (em) {
-    base = __shfl(base, 0);
-    if (kind != 0) {
-      const uint64_t e = base + mask_rank(em);
-      if (e < out.cap) {
-        out.slot[e] = slot0 + idx;
-        out.qidx[e] = qi;
-        out.cand[e] = c;
-        out.prob[e] = prob;
-        out.kind[e] = kind;
-      }
-    }
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kScoreBlock / 64; ++w) {
+    const uint32_t cw = wcount[w];
+    before += (uint32_t)w < wave ? cw : 0u;
+    total += cw;
   }
+  if (kind != 0) {
+    const uint64_t e = (uint64_t)blockIdx.x * kScoreBlock + before + mask_rank(em);
+    out.prob[e] = prob;
+    out.cand[e] = c | (kind << kKindShift);
+    out.qidx[e] = qi;
+  }
+  if (threadIdx.x == 0) out.bcnt[blockIdx.x] = total;
+}
+
+// Concatenate the per-block staged entries in block order (one block per score block).
+__global__ __launch_bounds__(256) void k_compact(const StageOut st, const uint64_t* __restrict__ boff,
+                                                 uint64_t base, MatchList out) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t n = st.bcnt[b];
+  const uint32_t i = threadIdx.x;
+  if (i >= n) return;
+  const uint64_t src = (uint64_t)b * kScoreBlock + i;
+  const uint64_t dst = base + boff[b] + i;
+  const uint32_t w = st.cand[src];
+  out.cand[dst] = w & ((1u << kKindShift) - 1u);
+  out.kind[dst] = (uint8_t)(w >> kKindShift);
+  out.prob[dst] = st.prob[src];
+  out.qidx[dst] = st.qidx[src];
+}
+
+// first[i] = first entry of query i (entries are grouped by query index, ascending)
+__global__ void k_first(const uint32_t* __restrict__ qidx, uint64_t n, uint64_t nq,
+                        uint64_t* __restrict__ first) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nq) return;
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if ((uint64_t)qidx[mid] < i) lo = mid + 1; else hi = mid;
+  }
+  first[i] = lo;
 }
 
 // ------------------------------------------------------------------------------------
@@ -438,18 +471,6 @@ __global__ void k_iota_u32(uint32_t* p, uint64_t n) {
   if (i < n) p[i] = (uint32_t)i;
 }
 
-__global__ void k_gather_matches(const uint32_t* __restrict__ perm, uint64_t n, const MatchOut in,
-                                 uint32_t* __restrict__ qidx, uint32_t* __restrict__ cand,
-                                 double* __restrict__ prob, uint8_t* __restrict__ kind) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t j = perm[i];
-  qidx[i] = in.qidx[j];
-  cand[i] = in.cand[j];
-  prob[i] = in.prob[j];
-  kind[i] = in.kind[j];
-}
-
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
@@ -520,9 +541,22 @@ hipError_t launch_emit(const uint32_t* queries, uint64_t q0, uint64_t q1, const 
 }
 
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
-                        uint64_t nslots, const MatchOut& out, hipStream_t s) {
+                        uint64_t nslots, const StageOut& out, hipStream_t s) {
   DK_LAUNCH_GUARD(nslots);
-  k_score<<<grid1d(nslots), 256, 0, s>>>(P, src, slot0, nslots, out);
+  k_score<<<grid1d(nslots, kScoreBlock), kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nblocks,
+                          uint64_t base, const MatchList& out, hipStream_t s) {
+  DK_LAUNCH_GUARD(nblocks);
+  k_compact<<<(unsigned)nblocks, kScoreBlock, 0, s>>>(st, boff, base, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_first(const uint32_t* qidx, uint64_t n, uint64_t nq, uint64_t* first,
+                        hipStream_t s) {
+  k_first<<<grid1d(nq + 1), 256, 0, s>>>(qidx, n, nq, first);
   return hipGetLastError();
 }
 
@@ -538,14 +572,6 @@ hipError_t launch_iota_u32(uint32_t* p, uint64_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_gather_matches(const uint32_t* perm, uint64_t n, const MatchOut& in,
-                                 uint32_t* qidx, uint32_t* cand, double* prob, uint8_t* kind,
-                                 hipStream_t s) {
-  DK_LAUNCH_GUARD(n);
-  k_gather_matches<<<grid1d(n), 256, 0, s>>>(perm, n, in, qidx, cand, prob, kind);
-  return hipGetLastError();
-}
-
 hipError_t sort_pairs_u64_u32(void* tmp, size_t& tmp_bytes, const uint64_t* kin, uint64_t* kout,
                               const uint32_t* vin, uint32_t* vout, uint64_t n, hipStream_t s) {
   return rocprim::radix_sort_pairs(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)n, 0, 64, s);
@@ -553,6 +579,12 @@ hipError_t sort_pairs_u64_u32(void* tmp, size_t& tmp_bytes, const uint64_t* kin,
 
 hipError_t exclusive_scan_u64(void* tmp, size_t& tmp_bytes, const uint64_t* in, uint64_t* out,
                               uint64_t n, hipStream_t s) {
+  return rocprim::exclusive_scan(tmp, tmp_bytes, in, out, (uint64_t)0, (size_t)n,
+                                 rocprim::plus<uint64_t>(), s);
+}
+
+hipError_t exclusive_scan_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint64_t* out,
+                                  uint64_t n, hipStream_t s) {
   return rocprim::exclusive_scan(tmp, tmp_bytes, in, out, (uint64_t)0, (size_t)n,
                                  rocprim::plus<uint64_t>(), s);
 }

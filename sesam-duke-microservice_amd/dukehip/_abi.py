@@ -22,7 +22,10 @@ QGRAM_BASIC, QGRAM_POSITIONAL = 0, 1
 MODE_DEDUP, MODE_LINKAGE, MODE_ALLPAIRS = 0, 1, 2
 KIND_MATCH, KIND_MAYBE = 1, 2
 
-EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_match", "dk_free_result",
+MATCH_HOST, MATCH_DEVICE = 0, 1
+
+EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_match", "dk_result_copy_to_device",
+           "dk_free_result",
            "dk_compare_rows", "dk_num_rows", "dk_set_profiling", "dk_get_profile",
            "dk_reset_profile", "dk_last_error", "dk_abi_version")
 
@@ -57,10 +60,10 @@ class dk_batch(C.Structure):
 
 
 class dk_result(C.Structure):
-    _fields_ = [("nqueries", C.c_uint64), ("first", C.POINTER(C.c_uint64)), ("n", C.c_uint64),
-                ("query", C.POINTER(C.c_uint32)), ("candidate", C.POINTER(C.c_uint32)),
-                ("prob", C.POINTER(C.c_double)), ("kind", C.POINTER(C.c_uint8)),
-                ("pairs_scored", C.c_uint64), ("pairs_generated", C.c_uint64)]
+    _fields_ = [("nqueries", C.c_uint64), ("n", C.c_uint64), ("first", C.POINTER(C.c_uint64)),
+                ("candidate", C.POINTER(C.c_uint32)), ("prob", C.POINTER(C.c_double)),
+                ("kind", C.POINTER(C.c_uint8)), ("pairs_scored", C.c_uint64),
+                ("pairs_generated", C.c_uint64)]
 
 
 class dk_profile(C.Structure):
@@ -90,7 +93,9 @@ def load():
     L.dk_destroy.argtypes = [vp]
     L.dk_destroy.restype = None
     L.dk_upsert.argtypes = [vp, C.POINTER(dk_batch), vp]
-    L.dk_match.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.POINTER(dk_result))]
+    L.dk_match.argtypes = [vp, vp, C.c_uint64, C.c_int, C.POINTER(C.POINTER(dk_result))]
+    L.dk_result_copy_to_device.argtypes = [C.POINTER(dk_result), vp, vp, vp, vp]
+    L.dk_result_copy_to_device.restype = C.c_int
     L.dk_free_result.argtypes = [C.POINTER(dk_result)]
     L.dk_free_result.restype = None
     L.dk_compare_rows.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]

@@ -68,19 +68,47 @@ class CollectingListener(MatchListener):
 
 
 class MatchResult:
-    """Host copy of a dk_result: entries grouped per query (batch order)."""
+    """A dk_result: entries grouped per query (query order).  The arrays are zero-copy
+    views of the library's pinned result memory, valid until :meth:`close` (called on
+    garbage collection), which hands the memory back to the ctx's pool."""
 
-    def __init__(self, res):
+    def __init__(self, lib, res, queries):
+        self._lib, self._res = lib, res
         r = res.contents
         n, nq = r.n, r.nqueries
         self.n, self.nqueries = n, nq
+        self.queries = queries
         self.pairs_scored, self.pairs_generated = r.pairs_scored, r.pairs_generated
-        as_np = np.ctypeslib.as_array
-        self.first = as_np(r.first, (nq + 1,)).copy() if nq + 1 else np.zeros(1, np.uint64)
-        self.query = as_np(r.query, (n,)).copy() if n else np.zeros(0, np.uint32)
-        self.candidate = as_np(r.candidate, (n,)).copy() if n else np.zeros(0, np.uint32)
-        self.prob = as_np(r.prob, (n,)).copy() if n else np.zeros(0, np.float64)
-        self.kind = as_np(r.kind, (n,)).copy() if n else np.zeros(0, np.uint8)
+        self.on_device = not bool(r.first)
+        view = np.ctypeslib.as_array
+        if self.on_device:
+            self.first = self.candidate = self.prob = self.kind = None
+        else:
+            self.first = view(r.first, (nq + 1,))
+            self.candidate = view(r.candidate, (n,)) if n else np.zeros(0, np.uint32)
+            self.prob = view(r.prob, (n,)) if n else np.zeros(0, np.float64)
+            self.kind = view(r.kind, (n,)) if n else np.zeros(0, np.uint8)
+
+    @property
+    def query(self):
+        """Row of r1 for every entry (expanded from `first`)."""
+        return np.repeat(np.asarray(self.queries, np.uint32), np.diff(self.first).astype(np.int64))
+
+    def copy_to_device(self, first=None, candidate=None, prob=None, kind=None):
+        """Device-to-device copy into caller buffers (device pointers as ints)."""
+        A.check(self._lib.dk_result_copy_to_device(self._res, first, candidate, prob, kind))
+
+    def close(self):
+        if self._res is not None:
+            self.first = self.candidate = self.prob = self.kind = None
+            self._lib.dk_free_result(self._res)
+            self._res = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class GpuEngine:
@@ -126,14 +154,12 @@ class GpuEngine:
         A.check(self.lib.dk_upsert(self.ctx, C.byref(b), rows.ctypes.data))
         return rows[:n]
 
-    def match(self, query_rows):
+    def match(self, query_rows, on_device=False):
         q = np.ascontiguousarray(query_rows, dtype=np.uint32)
         res = C.POINTER(A.dk_result)()
-        A.check(self.lib.dk_match(self.ctx, q.ctypes.data if q.size else None, q.size, C.byref(res)))
-        try:
-            return MatchResult(res)
-        finally:
-            self.lib.dk_free_result(res)
+        A.check(self.lib.dk_match(self.ctx, q.ctypes.data if q.size else None, q.size,
+                                  A.MATCH_DEVICE if on_device else A.MATCH_HOST, C.byref(res)))
+        return MatchResult(self.lib, res, q)
 
     def compare_rows(self, r1, r2):
         out = C.c_double()

@@ -53,7 +53,7 @@ int main(void) {
   S(dk_column) F(dk_column, offsets) F(dk_column, units) F(dk_column, width) F(dk_column, present)
   S(dk_batch) F(dk_batch, n) F(dk_batch, ident) F(dk_batch, group) F(dk_batch, deleted)
   F(dk_batch, columns) F(dk_batch, keys) F(dk_batch, key_columns)
-  S(dk_result) F(dk_result, nqueries) F(dk_result, first) F(dk_result, n) F(dk_result, query)
+  S(dk_result) F(dk_result, nqueries) F(dk_result, first) F(dk_result, n)
   F(dk_result, candidate) F(dk_result, prob) F(dk_result, kind) F(dk_result, pairs_scored)
   F(dk_result, pairs_generated)
   S(dk_profile) F(dk_profile, ms_index) F(dk_profile, ms_generate) F(dk_profile, ms_score)
