@@ -92,34 +92,31 @@ def main():
     q0, q1 = n * rank // world, n * (rank + 1) // world
     queries = np.arange(q0, q1, dtype=np.uint32)
 
-    nq_max = max(n * (r + 1) // world - n * r // world for r in range(world))
+    from dukehip import dist as dshard
+    nq_max = dshard.max_tile(n, world)
+    holder = {}
 
     def step():
+        old = holder.pop("res", None)
+        if old is not None:
+            old.close()                       # hand the result memory back to the pool
         if dist is None:
             res = eng.match(queries)          # entries land in pinned host memory
+            holder["res"] = res
             return res, res.pairs_scored
         # N>1: entries stay in HBM; RCCL all-gathers the per-rank counts, then gathers
         # every rank's match list (first / candidate / prob / kind) to rank 0 over xGMI,
         # which moves the node's list to the host.
         res = eng.match(queries, on_device=True)
-        cnt = torch.tensor([res.n, res.pairs_scored], dtype=torch.int64, device=dev)
-        allc = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(allc, cnt)
-        mx = max(1, int(max(int(c[0]) for c in allc)))
-        first = torch.zeros(nq_max + 1, dtype=torch.int64, device=dev)
-        cand = torch.zeros(mx, dtype=torch.int32, device=dev)
-        prob = torch.zeros(mx, dtype=torch.float64, device=dev)
-        kind = torch.zeros(mx, dtype=torch.uint8, device=dev)
-        torch.cuda.synchronize()
-        res.copy_to_device(first.data_ptr(), cand.data_ptr(), prob.data_ptr(), kind.data_ptr())
-        for t in (first, cand, prob, kind):
-            lst = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
-            dist.gather(t, lst, dst=0)
-            if rank == 0:
-                for r, g in enumerate(lst):
-                    g[: (int(allc[r][0]) if t is not first else nq_max + 1)].cpu()
-        res.close()
-        return res, int(sum(int(c[1]) for c in allc))
+
+        def fill(first, cand, prob, kind):
+            torch.cuda.synchronize()
+            res.copy_to_device(first.data_ptr(), cand.data_ptr(), prob.data_ptr(), kind.data_ptr())
+
+        _, total = dshard.gather_matches(dist, torch, dev, len(queries), res.n, res.pairs_scored,
+                                         fill, world, rank, nq_max)
+        holder["res"] = res
+        return res, total
 
     for _ in range(args.warmup):
         step()

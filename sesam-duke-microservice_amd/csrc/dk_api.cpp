@@ -88,14 +88,18 @@ struct PinnedBuf {
   ~PinnedBuf() {
     if (p) (void)hipHostFree(p);
   }
-  hipError_t reserve(size_t nb) {
+  // grow to >= nb bytes (x2 headroom), preserving the first `keep` bytes
+  hipError_t reserve(size_t nb, size_t keep = 0) {
     if (nb <= bytes) return hipSuccess;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
     size_t cap = std::max(nb, bytes * 2);
-    hipError_t e = hipHostMalloc(&p, cap, hipHostMallocDefault);
-    bytes = e == hipSuccess ? cap : 0;
-    return e;
+    void* q = nullptr;
+    hipError_t e = hipHostMalloc(&q, cap, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    if (keep && p) memcpy(q, p, keep);
+    if (p) (void)hipHostFree(p);
+    p = q;
+    bytes = cap;
+    return hipSuccess;
   }
   template <typename T>
   T* as() const { return reinterpret_cast<T*>(p); }
@@ -190,6 +194,9 @@ struct PropState {
   uint64_t grams_used = 0;
   int maxlen = 0;
   DevBuf off, len, units, num, numok, goff, gcnt, grams;
+  // candidate replica of the current dk_match (see dk_internal.h)
+  int rlmax = 0;
+  DevBuf rlen, runits, rnum, rnumok, rgoff, rgcnt;
 };
 
 // Result memory (device list + pinned host copy), pooled per ctx and handed back by
@@ -228,6 +235,8 @@ struct dk_ctx {
   std::vector<PropState> P;
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // device->host copies of finished chunks
+  hipEvent_t chunk_done = nullptr;
   uint64_t nrows = 0, cap = 0;
   DevBuf ident, flags, group;
   DevBuf keys[kMaxKeys];
@@ -235,9 +244,11 @@ struct dk_ctx {
   std::vector<std::unordered_map<std::u16string, uint64_t>> intern;
   int key_style = 0;  // 0 unset, 1 u64 keys, 2 interned strings
   // match scratch
-  DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], srows[kMaxKeys], sgroup[kMaxKeys];
+  DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], rowof, sgroup[kMaxKeys];
+  const uint32_t* rowof_p = nullptr;  // replica position -> row (rowof, or usable in ALLPAIRS)
+  uint64_t rstride = 0;               // replica positions
   DevBuf ranges, counts, qoff, pq, pc, tmp;
-  DevBuf counters, st_bcnt, st_boff, st_prob, st_cand, st_qidx;
+  DevBuf counters, st_bcnt, st_bscored, st_bbytes, st_boff, st_prob, st_cand, st_qidx;
   PinnedBuf h_small;
   std::shared_ptr<ResultPool> pool = std::make_shared<ResultPool>();
   // profiling (Processor.setPerformanceProfiling)
@@ -338,6 +349,8 @@ int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
   c->intern.resize(c->schema.nkeys);
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->chunk_done, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
     return fail(DK_E_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -355,8 +368,12 @@ void dk_destroy(dk_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  hipStream_t s = c->stream;
+  (void)hipStreamSynchronize(c->copy_stream);
+  hipStream_t s = c->stream, cs = c->copy_stream;
+  hipEvent_t ev = c->chunk_done;
   delete c;
+  if (ev) (void)hipEventDestroy(ev);
+  if (cs) (void)hipStreamDestroy(cs);
   (void)hipStreamDestroy(s);
 }
 
@@ -501,8 +518,9 @@ int dk_upsert(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
       return fail(DK_E_STATE, "key style changed between batches (u64 keys vs key strings)");
     c->key_style = style;
   }
-  if (c->nrows + b->n >= (1ull << kKeyShift))
-    return fail(DK_E_UNSUPPORTED, "index would exceed %u rows", 1u << kKeyShift);
+  // rows < 2^29: K (<= 8) sorted tables of replica positions stay below the u32 sentinel
+  if (c->nrows + b->n >= (1ull << 29))
+    return fail(DK_E_UNSUPPORTED, "index would exceed %u rows", 1u << 29);
   HIPCHK(hipSetDevice(c->device));
   const uint64_t n = b->n, row0 = c->nrows;
   HIPCHK(grow_rows(c, row0 + n));
@@ -615,6 +633,8 @@ static ScoreParams make_params(const dk_ctx* c) {
   P.threshold = c->schema.threshold;
   P.maybe = c->schema.maybe_threshold;
   P.ident = c->ident.as<uint64_t>();
+  P.rowof = c->rowof_p;
+  P.rstride = c->rstride;
   for (int i = 0; i < P.nprops; ++i) {
     const PropState& S = c->P[i];
     DevProp& D = P.props[i];
@@ -634,8 +654,62 @@ static ScoreParams make_params(const dk_ctx* c) {
     D.goff = S.goff.as<uint32_t>();
     D.gcnt = S.gcnt.as<uint16_t>();
     D.grams = S.grams.as<uint64_t>();
+    D.rlmax = S.rlmax;
+    D.rlen = S.rlen.as<uint16_t>();
+    D.runits = S.runits.p;
+    D.rnum = S.rnum.as<double>();
+    D.rnumok = S.rnumok.as<uint8_t>();
+    D.rgoff = S.rgoff.as<uint32_t>();
+    D.rgcnt = S.rgcnt.as<uint16_t>();
   }
   return P;
+}
+
+// Candidate replica: every property's candidate-side values in replica order, units
+// transposed ([unit][position]) for values of at most kMaxReplicaUnits units.
+static int build_replica(dk_ctx* c, const uint32_t* rowof, uint64_t npos) {
+  hipStream_t s = c->stream;
+  c->rowof_p = rowof;
+  c->rstride = npos;
+  for (auto& S : c->P) {
+    const int op = S.cfg.comparator;
+    const bool strcmp_ = op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER ||
+                         op == DK_CMP_EXACT || op == DK_CMP_QGRAM;
+    const int W = S.width ? S.width : 1;
+    S.rlmax = strcmp_ && S.maxlen <= kMaxReplicaUnits ? ((std::max(S.maxlen, 1) + 3) & ~3) : 0;
+    HIPCHK(S.rlen.reserve(npos * 2 + 8, 0, s));
+    if (S.rlmax) HIPCHK(S.runits.reserve(npos * (uint64_t)S.rlmax * W + 64, 0, s));
+    const bool num = op == DK_CMP_NUMERIC, qg = op == DK_CMP_QGRAM;
+    if (num) {
+      HIPCHK(S.rnum.reserve(npos * 8 + 8, 0, s));
+      HIPCHK(S.rnumok.reserve(npos + 8, 0, s));
+    }
+    if (qg) {
+      HIPCHK(S.rgoff.reserve(npos * 4 + 8, 0, s));
+      HIPCHK(S.rgcnt.reserve(npos * 2 + 8, 0, s));
+    }
+    ReplicaJob J{};
+    J.width = W;
+    J.rlmax = S.rlmax;
+    J.has_num = num;
+    J.has_qgram = qg;
+    J.stride = npos;
+    J.off = S.off.as<uint32_t>();
+    J.len = S.len.as<uint16_t>();
+    J.units = S.units.p;
+    J.num = S.num.as<double>();
+    J.numok = S.numok.as<uint8_t>();
+    J.goff = S.goff.as<uint32_t>();
+    J.gcnt = S.gcnt.as<uint16_t>();
+    J.rlen = S.rlen.as<uint16_t>();
+    J.runits = S.runits.p;
+    J.rnum = S.rnum.as<double>();
+    J.rnumok = S.rnumok.as<uint8_t>();
+    J.rgoff = S.rgoff.as<uint32_t>();
+    J.rgcnt = S.rgcnt.as<uint16_t>();
+    HIPCHK(launch_replicate(J, rowof, npos, s));
+  }
+  return DK_OK;
 }
 
 template <typename F>
@@ -697,46 +771,57 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   T.nkeys = nk;
   T.linkage = c->schema.mode == DK_MODE_LINKAGE;
   T.group = c->group.as<uint8_t>();
+  T.m = M;
+  HIPCHK(c->rowof.reserve((uint64_t)std::max(nk, 1) * M * 4 + 4, 0, s));
   for (int k = 0; k < nk; ++k) {
+    uint32_t* rows_k = c->rowof.as<uint32_t>() + (uint64_t)k * M;
     HIPCHK(c->gkeys.reserve(M * 8 + 8, 0, s));
     HIPCHK(c->skeys[k].reserve(M * 8 + 8, 0, s));
-    HIPCHK(c->srows[k].reserve(M * 4 + 4, 0, s));
     HIPCHK(launch_gather_keys(c->keys[k].as<uint64_t>(), c->usable.as<uint32_t>(), c->gkeys.as<uint64_t>(), M, s));
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return sort_pairs_u64_u32(t, b, c->gkeys.as<uint64_t>(), c->skeys[k].as<uint64_t>(),
-                                c->usable.as<uint32_t>(), c->srows[k].as<uint32_t>(), M, s);
+                                c->usable.as<uint32_t>(), rows_k, M, s);
     }));
     if (T.linkage) {
       HIPCHK(c->sgroup[k].reserve(M + 8, 0, s));
-      HIPCHK(launch_gather_u8(c->group.as<uint8_t>(), c->srows[k].as<uint32_t>(), c->sgroup[k].as<uint8_t>(), M, s));
+      HIPCHK(launch_gather_u8(c->group.as<uint8_t>(), rows_k, c->sgroup[k].as<uint8_t>(), M, s));
     }
     T.keys[k] = c->keys[k].as<uint64_t>();
     T.skeys[k] = c->skeys[k].as<uint64_t>();
-    T.srows[k] = c->srows[k].as<uint32_t>();
     T.sgroup[k] = c->sgroup[k].as<uint8_t>();
-    T.n[k] = M;
   }
+  T.rowof = c->rowof.as<uint32_t>();
+  // candidate replica in slot-position order: the K sorted tables, or the usable rows
+  rc = allpairs ? build_replica(c, c->usable.as<uint32_t>(), M)
+                : build_replica(c, c->rowof.as<uint32_t>(), (uint64_t)nk * M);
+  if (rc) return rc;
   c->prof.ms_index += t_index.stop();
 
   // ---- candidate counts per query -> slot offsets ----
   Timer t_gen(prof, s);
   std::vector<uint64_t> qoff(nq + 1, 0);
-  uint64_t total = 0;
+  uint64_t total = 0, generated = 0, mpad = 0;
   if (!allpairs) {
     HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
     HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
-    HIPCHK(launch_count(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(), c->counts.as<uint64_t>(), s));
+    HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
+    HIPCHK(launch_count(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(), c->counts.as<uint64_t>(),
+                        c->counters.as<uint64_t>() + 2, s));
     HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
     }));
     HIPCHK(hipMemcpyAsync(qoff.data(), c->qoff.p, (nq + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->h_small.as<uint64_t>() + 2, c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     total = qoff[nq];
+    generated = c->h_small.as<uint64_t>()[2];
   } else {
-    for (uint64_t i = 0; i <= nq; ++i) qoff[i] = i * M;
-    total = nq * M;
+    mpad = (M + 63) & ~(uint64_t)63;
+    for (uint64_t i = 0; i <= nq; ++i) qoff[i] = i * mpad;
+    total = nq * mpad;
+    generated = nq * M;
   }
   c->prof.ms_generate += t_gen.stop();
 
@@ -749,13 +834,16 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(c->pc.reserve(chunk * 4 + 4, 0, s));
   }
   HIPCHK(c->st_bcnt.reserve(nblk_max * 4 + 4, 0, s));
+  HIPCHK(c->st_bscored.reserve(nblk_max * 4 + 4, 0, s));
+  HIPCHK(c->st_bbytes.reserve(nblk_max * 4 + 4, 0, s));
   HIPCHK(c->st_boff.reserve(nblk_max * 8 + 8, 0, s));
   HIPCHK(c->st_prob.reserve(nblk_max * kScoreBlock * 8, 0, s));
   HIPCHK(c->st_cand.reserve(nblk_max * kScoreBlock * 4, 0, s));
   HIPCHK(c->st_qidx.reserve(nblk_max * kScoreBlock * 4, 0, s));
-  HIPCHK(hipMemsetAsync(c->counters.p, 0, 4 * sizeof(uint64_t), s));
-  StageOut st{c->counters.as<uint64_t>(), c->st_bcnt.as<uint32_t>(), c->st_prob.as<double>(),
-              c->st_cand.as<uint32_t>(), c->st_qidx.as<uint32_t>()};
+  HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * sizeof(uint64_t), s));
+  StageOut st{c->counters.as<uint64_t>(), c->st_bcnt.as<uint32_t>(), c->st_bscored.as<uint32_t>(),
+              c->st_bbytes.as<uint32_t>(), c->st_prob.as<double>(), c->st_cand.as<uint32_t>(),
+              c->st_qidx.as<uint32_t>()};
   ResultBufs& B = *R->bufs;
   uint64_t nm = 0;  // entries so far
   for (uint64_t s0 = 0; s0 < total; s0 += CH) {
@@ -765,8 +853,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     src.queries = c->d_queries.as<uint32_t>();
     if (allpairs) {
       src.allpairs = 1;
-      src.usable = c->usable.as<uint32_t>();
       src.m = M;
+      src.mpad = mpad;
     } else {
       Timer t_emit(prof, s);
       const uint64_t q0 = (uint64_t)(std::upper_bound(qoff.begin(), qoff.end(), s0) - qoff.begin()) - 1;
@@ -781,6 +869,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     Timer t_score(prof, s);
     HIPCHK(launch_score(P, src, s0, s1 - s0, st, s));
     c->prof.ms_score += t_score.stop();
+    HIPCHK(launch_reduce_blocks(st, nblk, s));
     c->prof.score_launches += 1;
     // block-ordered compaction of this chunk's entries onto the match list
     Timer t_gather(prof, s);
@@ -802,6 +891,22 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(),
                    B.d_qidx.as<uint32_t>()};
       HIPCHK(launch_compact(st, c->st_boff.as<uint64_t>(), nblk, nm, ml, s));
+      if (!(flags & DK_MATCH_DEVICE)) {
+        // overlap: this chunk's entries go to pinned host memory on the copy stream while
+        // the next chunk scores
+        if (need * 8 > B.h_prob.bytes || need * 4 > B.h_cand.bytes || need > B.h_kind.bytes) {
+          HIPCHK(hipStreamSynchronize(c->copy_stream));
+          HIPCHK(B.h_cand.reserve(need * 4, nm * 4));
+          HIPCHK(B.h_prob.reserve(need * 8, nm * 8));
+          HIPCHK(B.h_kind.reserve(need, nm));
+        }
+        HIPCHK(hipEventRecord(c->chunk_done, s));
+        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->chunk_done, 0));
+        hipStream_t cs = c->copy_stream;
+        HIPCHK(hipMemcpyAsync(B.h_cand.as<uint32_t>() + nm, B.d_cand.as<uint32_t>() + nm, add * 4, hipMemcpyDeviceToHost, cs));
+        HIPCHK(hipMemcpyAsync(B.h_prob.as<double>() + nm, B.d_prob.as<double>() + nm, add * 8, hipMemcpyDeviceToHost, cs));
+        HIPCHK(hipMemcpyAsync(B.h_kind.as<uint8_t>() + nm, B.d_kind.as<uint8_t>() + nm, add, hipMemcpyDeviceToHost, cs));
+      }
       nm = need;
     }
     c->prof.ms_gather += t_gather.stop();
@@ -811,9 +916,9 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   const uint64_t scored = c->h_small.as<uint64_t>()[0];
   const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
   R->r.pairs_scored = scored;
-  R->r.pairs_generated = total;
+  R->r.pairs_generated = generated;
   c->prof.pairs_scored += scored;
-  c->prof.pairs_generated += total;
+  c->prof.pairs_generated += generated;
   c->prof.score_bytes += sbytes;
 
   // ---- per-query entry offsets, then (DK_MATCH_HOST) the copy into pinned host memory ----
@@ -823,16 +928,12 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   R->r.nqueries = nq;
   R->r.n = nm;
   if (!(flags & DK_MATCH_DEVICE)) {
+    HIPCHK(hipStreamSynchronize(c->copy_stream));  // chunk copies landed
     HIPCHK(B.h_first.reserve((nq + 1) * 8));
-    HIPCHK(B.h_cand.reserve(nm * 4 + 4));
-    HIPCHK(B.h_prob.reserve(nm * 8 + 8));
-    HIPCHK(B.h_kind.reserve(nm + 1));
+    HIPCHK(B.h_cand.reserve(nm * 4 + 4, nm * 4));
+    HIPCHK(B.h_prob.reserve(nm * 8 + 8, nm * 8));
+    HIPCHK(B.h_kind.reserve(nm + 1, nm));
     HIPCHK(hipMemcpyAsync(B.h_first.p, B.d_first.p, (nq + 1) * 8, hipMemcpyDeviceToHost, s));
-    if (nm) {
-      HIPCHK(hipMemcpyAsync(B.h_cand.p, B.d_cand.p, nm * 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(B.h_prob.p, B.d_prob.p, nm * 8, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(B.h_kind.p, B.d_kind.p, nm, hipMemcpyDeviceToHost, s));
-    }
     R->r.first = B.h_first.as<uint64_t>();
     R->r.candidate = B.h_cand.as<uint32_t>();
     R->r.prob = B.h_prob.as<double>();
@@ -902,15 +1003,18 @@ int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
   if (r1 >= c->nrows || r2 >= c->nrows) return fail(DK_E_INVALID, "row out of range");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  DevBuf buf;  // [0..2] query row, query index, candidate; staging for one block after
-  HIPCHK(buf.reserve(4096, 0, s));
-  uint32_t host[3] = {r1, 0u, r2};
-  HIPCHK(hipMemsetAsync(buf.p, 0, 4096, s));
+  DevBuf buf;  // [0..3] query row, query index, replica position 0, rowof[0]; then staging
+  HIPCHK(buf.reserve(8192, 0, s));
+  uint32_t host[4] = {r1, 0u, 0u, r2};
+  HIPCHK(hipMemsetAsync(buf.p, 0, 8192, s));
   HIPCHK(hipMemcpyAsync(buf.p, host, sizeof host, hipMemcpyHostToDevice, s));
   uint8_t* base = buf.as<uint8_t>();
   StageOut st{reinterpret_cast<uint64_t*>(base + 64), reinterpret_cast<uint32_t*>(base + 96),
+              reinterpret_cast<uint32_t*>(base + 100), reinterpret_cast<uint32_t*>(base + 104),
               reinterpret_cast<double*>(base + 128), reinterpret_cast<uint32_t*>(base + 2176),
               reinterpret_cast<uint32_t*>(base + 3200)};
+  int rc = build_replica(c, buf.as<uint32_t>() + 3, 1);  // one-position candidate replica
+  if (rc) return rc;
   ScoreParams P = make_params(c);
   P.threshold = -INFINITY;  // every non-NaN probability is emitted
   P.maybe = 0.0;

@@ -12,28 +12,50 @@ namespace dk {
 constexpr int kMaxProps = 16;
 constexpr int kMaxKeys = 8;
 constexpr uint16_t kMissing = 0xFFFF;  // length sentinel: record has no value
-constexpr int kMaxUnits = 64;          // per-value limit of the lane-per-pair kernels
+constexpr int kMaxUnits = 64;          // Levenshtein value limit of the lane-per-pair kernel
+constexpr int kMaxReplicaUnits = 64;   // longer columns are read in place (canonical arena)
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // filtered candidate slot
-constexpr int kKeyShift = 29;          // candidate word = row | (key function << 29)
-constexpr uint32_t kRowMask = (1u << kKeyShift) - 1u;
 
 constexpr uint8_t kAlive = 1;    // not superseded by a later upsert of the same ID
 constexpr uint8_t kDeleted = 2;  // dukeDeleted == "true" (IncrementalLuceneDatabase.java:478)
 
-// One scored property as the fused kernel sees it (HBM SoA, row-indexed).
+// ---------------------------------------------------------------------------------------
+// HBM layout
+//  canonical index (row-indexed, grows with dk_upsert):
+//    per property: off[row] (first code unit, 4-byte aligned), len[row] (kMissing = no
+//    value), units arena (u8 or u16, zero padded), num/numok (NUMERIC), goff/gcnt/grams
+//    (QGRAM, sorted unique packed grams); per row: ident, flags, group; per key function
+//    keys[k][row].
+//  candidate replica (rebuilt by every dk_match after the blocking sort): the K key
+//    functions' sorted candidate lists concatenated — position g = k * M + i holds row
+//    rowof[g] = k-th table's i-th row — and per property its values in that order:
+//    rlen[g], runits transposed [unit j][g] (so the 64 lanes of a wave, which hold 64
+//    consecutive candidates, read unit j of their values as 64 consecutive elements),
+//    rnum/rnumok, rgoff/rgcnt.
+// ---------------------------------------------------------------------------------------
+
 struct DevProp {
   int32_t op;         // DK_CMP_*
   int32_t width;      // 1 or 2 bytes per code unit in `units`
-  int32_t q, formula, tokenizer, pad;
+  int32_t q, formula, tokenizer;
+  int32_t rlmax;      // replica units per value (0 = read candidates in place)
   double low, high, min_ratio;
-  const uint32_t* off;   // row -> first code unit (4-byte aligned string starts)
-  const uint16_t* len;   // row -> code units, kMissing = no value
-  const void* units;     // arena, zero-padded, tail-padded for over-reads
-  const double* num;     // NUMERIC: parsed Double.parseDouble value
-  const uint8_t* numok;  // NUMERIC: 1 = parsed, 0 = NumberFormatException
-  const uint32_t* goff;  // QGRAM: row -> first gram
-  const uint16_t* gcnt;  // QGRAM: row -> unique grams
-  const uint64_t* grams; // QGRAM: sorted unique packed grams
+  // canonical (query side; candidate side when rlmax == 0)
+  const uint32_t* off;
+  const uint16_t* len;
+  const void* units;
+  const double* num;
+  const uint8_t* numok;
+  const uint32_t* goff;
+  const uint16_t* gcnt;
+  const uint64_t* grams;
+  // replica (candidate side), indexed by replica position
+  const uint16_t* rlen;
+  const void* runits;     // [j * rstride + g]
+  const double* rnum;
+  const uint8_t* rnumok;
+  const uint32_t* rgoff;
+  const uint16_t* rgcnt;
 };
 
 struct ScoreParams {
@@ -42,18 +64,21 @@ struct ScoreParams {
   double threshold;
   double maybe;
   const uint64_t* ident;
+  const uint32_t* rowof;  // replica position -> row
+  uint64_t rstride;       // replica positions (K * M)
   DevProp props[kMaxProps];
 };
 
-// Where the (query, candidate) of a slot comes from.
+// Where the (query, candidate) of a slot comes from.  Every query's slots are padded to
+// a multiple of 64, so each wave of k_score holds exactly one query.
 struct PairSource {
   // blocked modes: materialised chunk of slots
   const uint32_t* pq;  // query index (into the query list)
-  const uint32_t* pc;  // candidate word (row | k << 29) or kSentinel
-  // ALLPAIRS: implicit slots s -> (s / m, usable[s % m])
+  const uint32_t* pc;  // replica position of the candidate, or kSentinel
+  // ALLPAIRS: implicit slots s -> (s / mpad, replica position s % mpad if < m)
   const uint32_t* queries;  // query rows
-  const uint32_t* usable;   // candidate rows
   uint64_t m;
+  uint64_t mpad;            // m rounded up to a wave (64)
   int32_t allpairs;
 };
 
@@ -64,8 +89,10 @@ struct PairSource {
 constexpr int kScoreBlock = 256;
 constexpr int kKindShift = 30;  // staged candidate word = row | kind << 30
 struct StageOut {
-  uint64_t* counters;  // [0] pairs scored, [1] operand bytes
+  uint64_t* counters;  // [0] pairs scored, [1] operand bytes (summed by k_reduce_blocks)
   uint32_t* bcnt;      // per block: emitted entries
+  uint32_t* bscored;   // per block: pairs scored
+  uint32_t* bbytes;    // per block: algorithmic operand bytes
   double* prob;
   uint32_t* cand;
   uint32_t* qidx;
@@ -77,6 +104,41 @@ struct MatchList {
   uint8_t* kind;
   double* prob;
   uint32_t* qidx;
+};
+
+// Blocking tables of one dk_match call: per key function, the usable rows (alive, not
+// deleted) sorted by (key, group, row); table k occupies rowof[k * M, (k + 1) * M).
+struct BlockTables {
+  int32_t nkeys;
+  int32_t linkage;
+  uint64_t m;                       // usable rows
+  const uint64_t* keys[kMaxKeys];   // per key function, per row
+  const uint8_t* group;             // per row (LINKAGE)
+  const uint64_t* skeys[kMaxKeys];  // sorted keys of table k
+  const uint8_t* sgroup[kMaxKeys];  // group of table k's entries (LINKAGE)
+  const uint32_t* rowof;            // K * M
+};
+
+// One property's replica build.
+struct ReplicaJob {
+  int32_t width;
+  int32_t rlmax;      // 0: no unit replica (long values, or non-string comparator)
+  int32_t has_num;
+  int32_t has_qgram;
+  uint64_t stride;    // replica positions
+  const uint32_t* off;
+  const uint16_t* len;
+  const void* units;
+  const double* num;
+  const uint8_t* numok;
+  const uint32_t* goff;
+  const uint16_t* gcnt;
+  uint16_t* rlen;
+  void* runits;
+  double* rnum;
+  uint8_t* rnumok;
+  uint32_t* rgoff;
+  uint16_t* rgcnt;
 };
 
 // ---- launchers (dk_kernels.hip) ----
@@ -91,27 +153,19 @@ hipError_t launch_select_rows(const uint8_t* flags, const uint8_t* group, uint64
                               int want_group, uint32_t* flag_out, hipStream_t s);
 hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64_t nrows,
                                uint32_t base, uint32_t* rows_out, hipStream_t s);
-// Blocking tables of one dk_match call: per key function, the usable rows (alive, not
-// deleted) sorted by (key, group, row).
-struct BlockTables {
-  int32_t nkeys;
-  int32_t linkage;
-  const uint64_t* keys[kMaxKeys];  // per key function, per row
-  const uint8_t* group;  // per row (LINKAGE)
-  const uint64_t* skeys[kMaxKeys];
-  const uint32_t* srows[kMaxKeys];
-  const uint8_t* sgroup[kMaxKeys];
-  uint64_t n[kMaxKeys];
-};
-
+hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t npos,
+                            hipStream_t s);
+// counts[i] = candidate slots of query i rounded up to 64 (one query per score wave);
+// real[0] += the unpadded total
 hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint2* ranges,
-                        uint64_t* counts, hipStream_t s);
+                        uint64_t* counts, uint64_t* real, hipStream_t s);
 hipError_t launch_emit(const uint32_t* queries, uint64_t q0, uint64_t q1, const uint64_t* qoff,
                        const uint2* ranges, uint64_t nq, const BlockTables& T,
                        const uint64_t* ident, uint64_t s0, uint64_t s1, uint32_t* pq,
                        uint32_t* pc, hipStream_t s);
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                         uint64_t nslots, const StageOut& out, hipStream_t s);
+hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s);
 hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nblocks,
                           uint64_t base, const MatchList& out, hipStream_t s);
 hipError_t launch_first(const uint32_t* qidx, uint64_t n, uint64_t nq, uint64_t* first,

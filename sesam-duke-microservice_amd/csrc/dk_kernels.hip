@@ -4,9 +4,11 @@
 // single IEEE round-to-nearest operation, as in the JVM, so probabilities reproduce
 // Duke's bit for bit when evaluated in the same order.
 //
-// Hot path (SURVEY §3.1 loops 2-4): k_score — one lane per (query, candidate) slot,
-// all properties fused: comparator -> PropertyImpl low/high mapping -> computeBayes ->
-// strict threshold -> wave-ballot compaction of match / maybe entries.
+// Hot path (SURVEY §3.1 loops 2-4): k_score — one lane per (query, candidate) slot and
+// one query per wave, all properties fused: comparator -> PropertyImpl low/high mapping
+// -> computeBayes -> strict threshold -> block-ordered compaction of match / maybe
+// entries.  Candidate values are read from the per-match replica (dk_internal.h), where
+// the 64 lanes of a wave read 64 consecutive elements.
 #include <cstring>
 
 #include <algorithm>
@@ -42,90 +44,160 @@ __device__ __forceinline__ double compute_bayes(double p1, double p2) {
   return (p1 * p2) / ((p1 * p2) + ((1.0 - p1) * (1.0 - p2)));
 }
 
+// A Java String's code units at a stride: 1 in the canonical arena, the replica's
+// position count in the transposed candidate replica.
 template <typename CT>
-__device__ __forceinline__ bool units_equal(const CT* a, int na, const CT* b, int nb) {
+struct Str {
+  const CT* p;
+  uint64_t stride;
+  __device__ __forceinline__ uint32_t operator[](int j) const { return p[(uint64_t)j * stride]; }
+};
+
+template <typename CT>
+__device__ __forceinline__ bool str_equal(const Str<CT>& a, int na, const Str<CT>& b, int nb) {
   if (na != nb) return false;
-  // strings start 4-byte aligned and are zero padded to a 4-byte multiple
-  const uint32_t* wa = reinterpret_cast<const uint32_t*>(a);
-  const uint32_t* wb = reinterpret_cast<const uint32_t*>(b);
-  const int nw = (na * (int)sizeof(CT) + 3) >> 2;
-  for (int i = 0; i < nw; ++i)
-    if (wa[i] != wb[i]) return false;
+  for (int j = 0; j < na; ++j)
+    if (a[j] != b[j]) return false;
   return true;
 }
 
 // ------------------------------------------------------------------------------------
-// [Duke 1.2] comparators.Levenshtein.compactDistance, lane per pair.
-// s1 (the query value, Processor.compare's r1) indexes the DP column, kept in VGPRs and
-// unrolled to MAXM rows; s2 (candidate) streams one code unit per column.  Rows past
-// n1 compute garbage that never feeds rows <= n1 (the recurrence only looks up and
-// left); they are excluded from the cutoff minimum.  Preconditions: 1 <= n1 <= MAXM,
-// n2 >= 1, arena over-read of MAXM units past s1 is in bounds (tail padding).
+// Per-wave query tables.  Every wave of k_score holds ONE query record (the candidate
+// slots of a query are padded to a multiple of 64), so the query's value of a property
+// is wave-uniform.  For it the wave builds, in its LDS slice, the position-mask table
+// Peq[c] = {i : q[i] == c} (Myers' "Peq"): 256 entries for Latin-1 units; UTF-16 units
+// use a low-byte and a high-byte table whose AND is exact.  A candidate code unit x then
+// yields all query positions holding x with one or two LDS reads.
 // ------------------------------------------------------------------------------------
-template <int MAXM, typename CT>
-__device__ __forceinline__ int compact_distance(const CT* __restrict__ s1, int n1,
-                                                const CT* __restrict__ s2, int n2) {
-  uint32_t a[MAXM];
-#pragma unroll
-  for (int i = 0; i < MAXM; ++i) a[i] = s1[i];
-  int col[MAXM + 1];
-  const int maxdist = min(n1, n2) >> 1;
-  uint32_t ch = s2[0];
-  col[0] = 1;  // virtual first row
-#pragma unroll
-  for (int i = 1; i <= MAXM; ++i) col[i] = min(col[i - 1], i - 1) + (a[i - 1] != ch ? 1 : 0);
-  int above = 0;
-  int result = -1;
-  for (int j = 1; j < n2; ++j) {
-    ch = s2[j];
-    above = j + 1;  // virtual first row
-    int smallest = 2 * n1;
-#pragma unroll
-    for (int i = 1; i <= MAXM; ++i) {
-      const int v = imin3(above, col[i - 1], col[i]) + (a[i - 1] != ch ? 1 : 0);
-      col[i - 1] = above;
-      above = v;
-      smallest = (i <= n1) ? min(smallest, v) : smallest;
-    }
-    col[MAXM] = above;
-    if (smallest > maxdist) {
-      result = smallest;
-      break;
+constexpr int kPeqEntries = 512;  // per wave: [0,256) low byte, [256,512) high byte
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // orders this wave's LDS accesses (no other wave touches its slice)
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <typename CT>
+__device__ __forceinline__ void peq_set(uint64_t* peq, const CT* s, int n, bool on) {
+  const int lane = (int)lane_id();
+  if (lane < n) {
+    const uint32_t ch = s[lane];
+    const uint64_t bit = 1ull << lane;
+    if (sizeof(CT) == 1) {
+      if (on) atomicOr((unsigned long long*)&peq[ch], (unsigned long long)bit);
+      else peq[ch] = 0;
+    } else {
+      if (on) {
+        atomicOr((unsigned long long*)&peq[ch & 0xFF], (unsigned long long)bit);
+        atomicOr((unsigned long long*)&peq[256 + (ch >> 8)], (unsigned long long)bit);
+      } else {
+        peq[ch & 0xFF] = 0;
+        peq[256 + (ch >> 8)] = 0;
+      }
     }
   }
-  if (result < 0) {
-    if (n2 == 1) return 0;  // Duke returns its initial `above` when |s2| == 1
-    // D[n1][n2-1] was parked in col[n1] (written at unrolled row n1+1, or row MAXM above)
-    int r = col[0];
+  wave_lds_sync();
+}
+
+template <typename CT>
+__device__ __forceinline__ uint64_t peq_eq(const uint64_t* peq, uint32_t x) {
+  if (sizeof(CT) == 1) return peq[x];
+  return peq[x & 0xFF] & peq[256 + (x >> 8)];
+}
+
+__device__ __forceinline__ uint64_t range_mask(int lo, int hi) {  // bits [lo, hi), 0<=lo<=hi<=64
+  const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+  const uint64_t dn = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+  return up & ~dn;
+}
+
+__device__ __forceinline__ int ffs64(uint64_t m) { return (int)__builtin_ctzll(m); }
+
+// ------------------------------------------------------------------------------------
+// [Duke 1.2] comparators.Levenshtein.compactDistance with a wave-uniform s1 (the query
+// value, Processor.compare's r1).  One lane per candidate s2; the DP column over s1's
+// rows lives in VGPRs, unrolled to MAXM and cut at the uniform n1 by scalar branches.
+// The cell is Duke's min(above, aboveleft, left) + cost; the cost bit of row i in column
+// j is bit i of ~Peq[s2[j]].  Per cell: one v_bfe, one v_min3, one add, a min for the
+// cutoff.  Preconditions: 1 <= n1 <= MAXM; act lanes have n2 >= 1.
+// ------------------------------------------------------------------------------------
+template <int MAXM, typename CT>
+__device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1, const Str<CT>& s2,
+                                                    int n2, bool act) {
+  int col[MAXM + 1];
+  const int maxdist = min(n1, n2) >> 1;
+  // first column: min(column[ix1-1], ix1-1) + cost
+  uint64_t ne = act ? ~peq_eq<CT>(peq, s2[0]) : ~0ull;
+  int prev = 1;
 #pragma unroll
-    for (int i = 1; i <= MAXM; ++i) r = (i == n1) ? col[i] : r;
-    result = r;
+  for (int i = 1; i <= MAXM; ++i) {
+    if (i <= n1) {  // n1 is wave-uniform: a scalar branch, not a lane mask
+      const int v = min(prev, i - 1) + (int)((ne >> (i - 1)) & 1ull);
+      col[i] = v;
+      prev = v;
+    }
+  }
+  int result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
+  bool live = act && n2 > 1;
+  uint64_t ne_next = live ? ~peq_eq<CT>(peq, s2[1]) : ~0ull;
+  for (int j = 1; live; ++j) {
+    ne = ne_next;
+    if (j + 1 < n2) ne_next = ~peq_eq<CT>(peq, s2[j + 1]);
+    int above = j + 1, diag = j, smallest = 2 * n1;
+#pragma unroll
+    for (int i = 1; i <= MAXM; ++i) {
+      if (i <= n1) {
+        const int left = col[i];
+        const int v = imin3(above, diag, left) + (int)((ne >> (i - 1)) & 1ull);
+        diag = left;
+        col[i] = v;
+        above = v;
+        smallest = min(smallest, v);
+      }
+    }
+    if (smallest > maxdist) {
+      result = smallest;
+      live = false;
+    } else if (j + 1 >= n2) {
+      result = above;
+      live = false;
+    }
   }
   return result;
 }
 
 // [Duke 1.2] comparators.Levenshtein.compare
 template <typename CT>
-__device__ __forceinline__ double levenshtein(const CT* s1, int n1, const CT* s2, int n2,
-                                              int bucket) {
+__device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str<CT>& s1, int n1,
+                                                  const Str<CT>& s2, int n2, bool act) {
   const int len = min(n1, n2);
   const int maxlen = max(n1, n2);
-  if ((double)len / (double)maxlen <= 0.5) return 0.0;
-  if (len == maxlen && units_equal(s1, n1, s2, n2)) return 1.0;
+  double r = 0.0;
+  bool run = act;
+  if (act) {
+    // (double)len / maxlen <= 0.5  <=>  2 * len <= maxlen: for ints below 2^52 the
+    // quotient is either exactly 0.5 or 1/(2*maxlen) away from it, far beyond rounding
+    if (2 * len <= maxlen) run = false;
+    else if (len == maxlen && str_equal(s1, n1, s2, n2)) { r = 1.0; run = false; }
+  }
   int d;
-  if (bucket <= 16) d = compact_distance<16>(s1, n1, s2, n2);
-  else if (bucket <= 32) d = compact_distance<32>(s1, n1, s2, n2);
-  else d = compact_distance<64>(s1, n1, s2, n2);
-  const int dist = min(d, len);
-  return 1.0 - ((double)dist / (double)len);
+  if (n1 <= 16) d = compact_distance_peq<16>(peq, n1, s2, n2, run);
+  else if (n1 <= 32) d = compact_distance_peq<32>(peq, n1, s2, n2, run);
+  else d = compact_distance_peq<64>(peq, n1, s2, n2, run);
+  if (run) {
+    const int dist = min(d, len);
+    r = 1.0 - ((double)dist / (double)len);
+  }
+  return r;
 }
 
-// [Duke 1.2] comparators.JaroWinkler.similarity
+// [Duke 1.2] comparators.JaroWinkler.similarity — per-lane form for values over 64 units
 template <typename CT>
-__device__ __forceinline__ double jarowinkler(const CT* s1, int n1, const CT* s2, int n2) {
-  if (units_equal(s1, n1, s2, n2)) return 1.0;
+__device__ __forceinline__ double jarowinkler(Str<CT> s1, int n1, Str<CT> s2, int n2) {
+  if (str_equal(s1, n1, s2, n2)) return 1.0;
   if (n1 > n2) {
-    const CT* ts = s2; s2 = s1; s1 = ts;
+    const Str<CT> ts = s2; s2 = s1; s1 = ts;
     int tn = n2; n2 = n1; n1 = tn;
   }
   const int maxdist = n2 >> 1;
@@ -134,7 +206,7 @@ __device__ __forceinline__ double jarowinkler(const CT* s1, int n1, const CT* s2
     const uint32_t ch = s1[ix];
     const int hi = min(n2, ix + maxdist);
     for (int ix2 = max(0, ix - maxdist); ix2 < hi; ++ix2) {
-      if (ch == (uint32_t)s2[ix2]) {
+      if (ch == s2[ix2]) {
         ++c;
         if (prevpos != -1 && ix2 < prevpos) ++t;
         prevpos = ix2;
@@ -143,6 +215,83 @@ __device__ __forceinline__ double jarowinkler(const CT* s1, int n1, const CT* s2
     }
   }
   if (c == 0) return 0.0;
+  double score = ((c / (double)n1) + (c / (double)n2) + ((c - t) / (double)c)) / 3.0;
+  int p = 0;
+  const int last = min(4, n1);
+  while (p < last && s1[p] == s2[p]) ++p;
+  score += ((p * (1 - score)) / 10);
+  return score;
+}
+
+// [Duke 1.2] comparators.JaroWinkler.similarity with the query's Peq table (both values
+// <= 64 units).  s1 is the shorter value (the query on a tie).
+//  * candidate shorter (rows = candidate units): row i's first match is the lowest set
+//    bit of Peq[cand[i]] inside the window over the query — one LDS read per row.
+//  * query shorter or equal (rows = query units): sweep the candidate's units j in order;
+//    Peq[cand[j]] gives every query row holding that unit, masked to the rows whose
+//    window contains j and not yet matched; the found step j is kept in six bit-planes,
+//    read back row by row for the transposition count.
+template <typename CT>
+__device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str<CT>& qs, int nq,
+                                                  const Str<CT>& cs, int nc, bool act) {
+  if (act && str_equal(qs, nq, cs, nc)) act = false;  // 1.0 below
+  const bool rows_cand = act && nc < nq;
+  const bool rows_query = act && !rows_cand;
+  int c = 0, t = 0;
+  {
+    const int md = nq >> 1;
+    int prev = -1;
+    for (int i = 0; rows_cand && i < nc; ++i) {
+      const uint64_t e = peq_eq<CT>(peq, cs[i]);
+      const uint64_t m = e & range_mask(max(0, i - md), min(nq, i + md));
+      if (m) {
+        const int j = ffs64(m);
+        ++c;
+        if (prev != -1 && j < prev) ++t;
+        prev = j;
+      }
+    }
+  }
+  if (__ballot(rows_query)) {
+    const int md = nc >> 1;
+    uint64_t found = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
+    const int maxn = rows_query ? nc : 0;
+    int wmax = maxn;
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
+    for (int j = 0; j < wmax; ++j) {
+      uint64_t m = 0;
+      if (j < maxn) {
+        const uint64_t r = peq_eq<CT>(peq, cs[j]);
+        m = r & range_mask(max(0, j - md + 1), min(nq, j + md + 1)) & ~found;
+      }
+      found |= m;
+      if (j & 1) p0 |= m;
+      if (j & 2) p1 |= m;
+      if (j & 4) p2 |= m;
+      if (j & 8) p3 |= m;
+      if (j & 16) p4 |= m;
+      if (j & 32) p5 |= m;
+    }
+    if (rows_query) {
+      c = __popcll(found);
+      int prev = -1;
+      uint64_t f = found;
+      while (f) {
+        const int i = ffs64(f);
+        f &= f - 1ull;
+        const int p = (int)((p0 >> i) & 1ull) | (int)(((p1 >> i) & 1ull) << 1) |
+                      (int)(((p2 >> i) & 1ull) << 2) | (int)(((p3 >> i) & 1ull) << 3) |
+                      (int)(((p4 >> i) & 1ull) << 4) | (int)(((p5 >> i) & 1ull) << 5);
+        if (prev != -1 && p < prev) ++t;
+        prev = p;
+      }
+    }
+  }
+  if (!act) return 1.0;  // equal values (inactive lanes discard the result)
+  if (c == 0) return 0.0;
+  const Str<CT>& s1 = rows_cand ? cs : qs;
+  const Str<CT>& s2 = rows_cand ? qs : cs;
+  const int n1 = rows_cand ? nc : nq, n2 = rows_cand ? nq : nc;
   double score = ((c / (double)n1) + (c / (double)n2) + ((c - t) / (double)c)) / 3.0;
   int p = 0;
   const int last = min(4, n1);
@@ -181,78 +330,107 @@ __device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool o
 }
 
 // ------------------------------------------------------------------------------------
-// The fused scoring kernel.
+// The fused scoring kernel.  One lane per slot, one query per wave.
 // ------------------------------------------------------------------------------------
 template <typename CT>
-__device__ __forceinline__ double string_sim(const DevProp& D, uint32_t q, uint32_t c, int lq,
-                                             int lc, int bucket) {
+__device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
+                                             uint32_t q, uint32_t g, uint32_t crow, int lq,
+                                             int lc, bool cmp) {
   const CT* base = reinterpret_cast<const CT*>(D.units);
-  const CT* s1 = base + D.off[q];
-  const CT* s2 = base + D.off[c];
+  const Str<CT> s1{base + D.off[q], 1};
+  const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const CT*>(D.runits) + g, rstride}
+                             : Str<CT>{base + D.off[crow], 1};
+  double sim = 0.0;
   switch (D.op) {
-    case DK_CMP_LEVENSHTEIN: return levenshtein(s1, lq, s2, lc, bucket);
-    case DK_CMP_JAROWINKLER: return jarowinkler(s1, lq, s2, lc);
-    case DK_CMP_EXACT: return units_equal(s1, lq, s2, lc) ? 1.0 : 0.0;
-    case DK_CMP_QGRAM: {
-      if (units_equal(s1, lq, s2, lc)) return 1.0;
-      const int m1 = D.gcnt[q], m2 = D.gcnt[c];
-      if (m1 == 0 || m2 == 0) return 0.0;
-      const int common = intersect_sorted(D.grams + D.goff[q], m1, D.grams + D.goff[c], m2);
-      return qgram_formula(common, m1, m2, D.formula);
+    case DK_CMP_LEVENSHTEIN:
+    case DK_CMP_JAROWINKLER: {
+      const bool table = lq <= 64 && (D.op == DK_CMP_LEVENSHTEIN || __ballot(cmp && lc > 64) == 0);
+      if (table) {
+        peq_set(peq, s1.p, lq, true);
+        sim = D.op == DK_CMP_LEVENSHTEIN ? levenshtein_peq(peq, s1, lq, s2, lc, cmp)
+                                         : jarowinkler_peq(peq, s1, lq, s2, lc, cmp);
+        peq_set(peq, s1.p, lq, false);
+      } else if (cmp) {
+        sim = jarowinkler(s1, lq, s2, lc);
+      }
+      break;
     }
-    default: return 0.5;
+    case DK_CMP_EXACT:
+      if (cmp) sim = str_equal(s1, lq, s2, lc) ? 1.0 : 0.0;
+      break;
+    case DK_CMP_QGRAM:
+      if (cmp) {
+        if (str_equal(s1, lq, s2, lc)) {
+          sim = 1.0;
+        } else {
+          const int m1 = D.gcnt[q], m2 = D.rgcnt[g];
+          if (m1 == 0 || m2 == 0) sim = 0.0;
+          else sim = qgram_formula(intersect_sorted(D.grams + D.goff[q], m1, D.grams + D.rgoff[g], m2),
+                                   m1, m2, D.formula);
+        }
+      }
+      break;
+    default:
+      break;
   }
+  return sim;
 }
 
 __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSource S,
                                                uint64_t slot0, uint64_t nslots, StageOut out) {
+  __shared__ uint64_t peq_all[kScoreBlock / 64][kPeqEntries];
+  __shared__ uint32_t wcount[kScoreBlock / 64], wscored[kScoreBlock / 64], wbytes[kScoreBlock / 64];
+  const uint32_t wave = threadIdx.x >> 6;
+  uint64_t* peq = peq_all[wave];
+  for (int e = (int)lane_id(); e < kPeqEntries; e += 64) peq[e] = 0;
+
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = idx < nslots;
-  uint32_t qi = 0, q = 0, c = 0;
-  if (valid) {
-    if (S.allpairs) {
-      const uint64_t g = slot0 + idx;
-      qi = (uint32_t)(g / S.m);
-      c = S.usable[g - (uint64_t)qi * S.m];
-      q = S.queries[qi];
-      valid = P.ident[c] != P.ident[q];  // Processor.isSameAs
-    } else {
-      qi = S.pq[idx];
-      const uint32_t w = S.pc[idx];
-      valid = w != kSentinel;
-      c = w & kRowMask;
-      q = S.queries[qi];
-    }
+  uint32_t qi = 0, g = 0;
+  if (S.allpairs) {
+    // slots of a query: [qi * mpad, qi * mpad + m), mpad = m rounded up to 64
+    const uint64_t s = slot0 + min(idx, nslots - 1);
+    qi = (uint32_t)(s / S.mpad);
+    const uint64_t t = s - (uint64_t)qi * S.mpad;
+    valid = valid && t < S.m;
+    g = valid ? (uint32_t)t : 0u;
+  } else {
+    qi = S.pq[min(idx, nslots - 1)];
+    const uint32_t w = valid ? S.pc[idx] : kSentinel;
+    valid = w != kSentinel;
+    g = valid ? w : 0u;  // lanes without a pair read replica position 0 (always in range)
   }
+  // one query per wave by construction (padded slot layout)
+  qi = __builtin_amdgcn_readfirstlane(qi);
+  const uint32_t q = __builtin_amdgcn_readfirstlane(S.queries[qi]);
+  const uint32_t crow = P.rowof[g];
+  if (S.allpairs) valid = valid && P.ident[crow] != P.ident[q];  // Processor.isSameAs
+  wave_lds_sync();
 
   double prob = 0.5;
   uint32_t bytes = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
   for (int p = 0; p < P.nprops; ++p) {
     const DevProp& D = P.props[p];
-    const int lq = valid ? (int)D.len[q] : (int)kMissing;
-    const int lc = valid ? (int)D.len[c] : (int)kMissing;
-    const bool present = lq != (int)kMissing && lc != (int)kMissing;
+    const int lq = (int)__builtin_amdgcn_readfirstlane((uint32_t)D.len[q]);
+    if (lq == (int)kMissing) continue;  // r1 has no value: property skipped for the wave
+    const int lc = valid ? (int)D.rlen[g] : (int)kMissing;
+    const bool present = lc != (int)kMissing;
     const bool cmp = present && lq > 0 && lc > 0;
-    int bucket = 64;
-    if (D.op == DK_CMP_LEVENSHTEIN) {
-      // wave-uniform row bucket for the DP column: the longest query value in the wave
-      bucket = __ballot(cmp && lq > 32) ? 64 : (__ballot(cmp && lq > 16) ? 32 : 16);
+    double sim = 0.0;
+    if (D.op == DK_CMP_NUMERIC) {
+      if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
+      if (cmp) bytes += 16;
+    } else if (D.op != DK_CMP_NONE) {
+      sim = D.width == 1 ? string_sim<uint8_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp)
+                         : string_sim<uint16_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp);
+      if (cmp) {
+        bytes += 8u + (uint32_t)(lq + lc) * (uint32_t)D.width;
+        if (D.op == DK_CMP_QGRAM) bytes += 8u + 8u * (uint32_t)(D.gcnt[q] + D.rgcnt[g]);
+      }
     }
     if (present) {
       double high = 0.0;
       if (cmp) {
-        double sim;
-        if (D.op == DK_CMP_NUMERIC) {
-          sim = numeric(D.num[q], D.numok[q] != 0, D.num[c], D.numok[c] != 0, D.min_ratio);
-          bytes += 16;
-        } else if (D.op == DK_CMP_NONE) {
-          sim = -1.0;
-        } else {
-          sim = D.width == 1 ? string_sim<uint8_t>(D, q, c, lq, lc, bucket)
-                             : string_sim<uint16_t>(D, q, c, lq, lc, bucket);
-          bytes += 8u + (uint32_t)(lq + lc) * (uint32_t)D.width;
-          if (D.op == DK_CMP_QGRAM) bytes += 8u + 8u * (uint32_t)(D.gcnt[q] + D.gcnt[c]);
-        }
         // [Duke 1.2] PropertyImpl.compare
         const double v = D.op == DK_CMP_NONE ? 0.5
                          : (sim < 0.5 ? D.low : ((D.high - 0.5) * (sim * sim)) + 0.5);
@@ -271,18 +449,14 @@ __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSo
 
   // block-ordered compaction: wave ballots -> per-wave counts in LDS -> slot-ordered
   // entries at the block's staging region; no atomics on entries
-  __shared__ uint32_t wcount[kScoreBlock / 64];
   const uint64_t em = __ballot(kind != 0);
   const uint64_t vm = __ballot(valid);
-  const uint32_t wave = threadIdx.x >> 6;
-  uint32_t wbytes = bytes;
-  for (int o = 32; o > 0; o >>= 1) wbytes += __shfl_xor(wbytes, o);
+  uint32_t sb = bytes;
+  for (int o = 32; o > 0; o >>= 1) sb += __shfl_xor(sb, o);
   if (lane_id() == 0) {
     wcount[wave] = (uint32_t)__popcll(em);
-    if (vm) {
-      atomicAdd((unsigned long long*)&out.counters[0], (unsigned long long)__popcll(vm));
-      atomicAdd((unsigned long long*)&out.counters[1], (unsigned long long)wbytes);
-    }
+    wscored[wave] = (uint32_t)__popcll(vm);
+    wbytes[wave] = sb;
   }
   __syncthreads();
   uint32_t before = 0, total = 0;
@@ -295,10 +469,47 @@ __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSo
   if (kind != 0) {
     const uint64_t e = (uint64_t)blockIdx.x * kScoreBlock + before + mask_rank(em);
     out.prob[e] = prob;
-    out.cand[e] = c | (kind << kKindShift);
+    out.cand[e] = crow | (kind << kKindShift);
     out.qidx[e] = qi;
   }
-  if (threadIdx.x == 0) out.bcnt[blockIdx.x] = total;
+  if (threadIdx.x == 0) {
+    uint32_t ns = 0, nb = 0;
+#pragma unroll
+    for (int w = 0; w < kScoreBlock / 64; ++w) {
+      ns += wscored[w];
+      nb += wbytes[w];
+    }
+    out.bcnt[blockIdx.x] = total;
+    out.bscored[blockIdx.x] = ns;
+    out.bbytes[blockIdx.x] = nb;
+  }
+}
+
+// Sum the per-block counters of a chunk into counters[0..1]: one atomic pair per block
+// of this kernel (a same-address atomic per score wave serialises at the memory side).
+__global__ __launch_bounds__(256) void k_reduce_blocks(const StageOut st, uint64_t nblocks) {
+  uint64_t a = 0, b = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nblocks;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    a += st.bscored[i];
+    b += st.bbytes[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b += __shfl_xor(b, o);
+  }
+  __shared__ uint64_t sa[4], sbb[4];
+  if (lane_id() == 0) {
+    sa[threadIdx.x >> 6] = a;
+    sbb[threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a = sa[0] + sa[1] + sa[2] + sa[3];
+    b = sbb[0] + sbb[1] + sbb[2] + sbb[3];
+    if (a) atomicAdd((unsigned long long*)&st.counters[0], (unsigned long long)a);
+    if (b) atomicAdd((unsigned long long*)&st.counters[1], (unsigned long long)b);
+  }
 }
 
 // Concatenate the per-block staged entries in block order (one block per score block).
@@ -331,6 +542,38 @@ __global__ void k_first(const uint32_t* __restrict__ qidx, uint64_t n, uint64_t 
 }
 
 // ------------------------------------------------------------------------------------
+// candidate replica: position g <- row rowof[g], units transposed
+// ------------------------------------------------------------------------------------
+template <typename CT>
+__device__ __forceinline__ void replicate_units(const ReplicaJob& J, uint64_t g, uint32_t row, int l) {
+  const CT* src = reinterpret_cast<const CT*>(J.units) + J.off[row];
+  CT* dst = reinterpret_cast<CT*>(J.runits) + g;
+  const int n = l == (int)kMissing ? 0 : l;
+  for (int j = 0; j < J.rlmax; ++j) dst[(uint64_t)j * J.stride] = j < n ? src[j] : (CT)0;
+}
+
+__global__ __launch_bounds__(256) void k_replicate(const ReplicaJob J, const uint32_t* __restrict__ rowof,
+                                                   uint64_t npos) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= npos) return;
+  const uint32_t row = rowof[g];
+  const int l = J.len[row];
+  J.rlen[g] = (uint16_t)l;
+  if (J.rlmax) {
+    if (J.width == 1) replicate_units<uint8_t>(J, g, row, l);
+    else replicate_units<uint16_t>(J, g, row, l);
+  }
+  if (J.has_num) {
+    J.rnum[g] = J.num[row];
+    J.rnumok[g] = J.numok[row];
+  }
+  if (J.has_qgram) {
+    J.rgoff[g] = J.goff[row];
+    J.rgcnt[g] = J.gcnt[row];
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // blocking: candidate counting and pair emission
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* a, uint64_t n, uint64_t v) {
@@ -351,39 +594,45 @@ __device__ __forceinline__ uint64_t upper_bound_u64(const uint64_t* a, uint64_t 
   return lo;
 }
 
-// Per query and key function: the candidate range [lo, hi) in the sorted table.  The
+// Per query and key function: the candidate range [lo, hi) in sorted table k.  The
 // query's own key is looked up by value, so a superseded or deleted query still finds
 // its block.  LINKAGE keeps only the other group's sub-range (rows are sorted by
 // (key, group, row) and groups are 1 and 2; IncrementalDataSource.java:80-84).
 __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const BlockTables T,
-                        uint2* __restrict__ ranges, uint64_t* __restrict__ counts) {
+                        uint2* __restrict__ ranges, uint64_t* __restrict__ counts,
+                        uint64_t* __restrict__ real) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq) return;
-  const uint32_t q = queries[i];
   uint64_t total = 0;
-  for (int k = 0; k < T.nkeys; ++k) {
-    const uint64_t key = T.keys[k][q];
-    const uint64_t lo = lower_bound_u64(T.skeys[k], T.n[k], key);
-    const uint64_t hi = upper_bound_u64(T.skeys[k], lo, T.n[k], key);
-    uint64_t a = lo, b = hi;
-    if (T.linkage) {
-      uint64_t s = lo, e = hi;  // first position with group >= 2
-      while (s < e) {
-        const uint64_t mid = (s + e) >> 1;
-        if (T.sgroup[k][mid] < 2) s = mid + 1; else e = mid;
+  if (i < nq) {
+    const uint32_t q = queries[i];
+    for (int k = 0; k < T.nkeys; ++k) {
+      const uint64_t key = T.keys[k][q];
+      const uint64_t lo = lower_bound_u64(T.skeys[k], T.m, key);
+      const uint64_t hi = upper_bound_u64(T.skeys[k], lo, T.m, key);
+      uint64_t a = lo, b = hi;
+      if (T.linkage) {
+        uint64_t s = lo, e = hi;  // first position with group >= 2
+        while (s < e) {
+          const uint64_t mid = (s + e) >> 1;
+          if (T.sgroup[k][mid] < 2) s = mid + 1; else e = mid;
+        }
+        if (T.group[q] < 2) a = s; else b = s;
       }
-      if (T.group[q] < 2) a = s; else b = s;
+      ranges[(uint64_t)k * nq + i] = make_uint2((uint32_t)a, (uint32_t)b);
+      total += b - a;
     }
-    ranges[(uint64_t)k * nq + i] = make_uint2((uint32_t)a, (uint32_t)b);
-    total += b - a;
+    counts[i] = (total + 63) & ~(uint64_t)63;
   }
-  counts[i] = total;
+  uint64_t w = total;
+  for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
+  if (lane_id() == 0 && w) atomicAdd((unsigned long long*)real, (unsigned long long)w);
 }
 
 // One wave per query (grid-stride): writes the query's candidate slots that fall in
-// [s0, s1).  Slot order inside a query = key function, then (group, row) order of the
-// sorted table.  Filters: isSameAs (identity) and "already a candidate under an
-// earlier key function" (Duke returns candidates as a set).
+// [s0, s1) as replica positions.  Slot order inside a query = key function, then (group,
+// row) order of the sorted table.  Filters: isSameAs (identity) and "already a candidate
+// under an earlier key function" (Duke returns candidates as a set).  Slots past the
+// query's candidates up to its next multiple of 64 are padding (kSentinel).
 __global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ queries, uint64_t q0,
                                               uint64_t q1, const uint64_t* __restrict__ qoff,
                                               const uint2* __restrict__ ranges, uint64_t nq,
@@ -399,8 +648,18 @@ __global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ queri
     if (a >= b) continue;
     const uint32_t q = queries[qi];
     const uint64_t idq = ident[q];
+    uint64_t real = 0;
+    for (int k = 0; k < T.nkeys; ++k) {
+      const uint2 r = ranges[(uint64_t)k * nq + qi];
+      real += r.y - r.x;
+    }
     for (uint64_t s = a + lane; s < b; s += 64) {
       uint64_t t = s - qa;
+      pq[s - s0] = (uint32_t)qi;
+      if (t >= real) {  // padding up to the query's last wave
+        pc[s - s0] = kSentinel;
+        continue;
+      }
       int k = 0;
       uint2 r = ranges[qi];
       for (; k < T.nkeys - 1; ++k) {
@@ -410,12 +669,11 @@ __global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ queri
         t -= len;
       }
       if (k == T.nkeys - 1) r = ranges[(uint64_t)k * nq + qi];
-      const uint32_t c = T.srows[k][r.x + t];
+      const uint64_t gpos = (uint64_t)k * T.m + r.x + t;
+      const uint32_t c = T.rowof[gpos];
       bool ok = ident[c] != idq;
-      for (int j = 0; j < k && ok; ++j)
-        ok = T.keys[j][c] != T.keys[j][q];
-      pq[s - s0] = (uint32_t)qi;
-      pc[s - s0] = ok ? (c | ((uint32_t)k << kKeyShift)) : kSentinel;
+      for (int j = 0; j < k && ok; ++j) ok = T.keys[j][c] != T.keys[j][q];
+      pc[s - s0] = ok ? (uint32_t)gpos : kSentinel;
     }
   }
 }
@@ -522,10 +780,17 @@ hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64
   return hipGetLastError();
 }
 
+hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t npos,
+                            hipStream_t s) {
+  DK_LAUNCH_GUARD(npos);
+  k_replicate<<<grid1d(npos), 256, 0, s>>>(J, rowof, npos);
+  return hipGetLastError();
+}
+
 hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint2* ranges,
-                        uint64_t* counts, hipStream_t s) {
+                        uint64_t* counts, uint64_t* real, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_count<<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts);
+  k_count<<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, real);
   return hipGetLastError();
 }
 
@@ -544,6 +809,13 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
                         uint64_t nslots, const StageOut& out, hipStream_t s) {
   DK_LAUNCH_GUARD(nslots);
   k_score<<<grid1d(nslots, kScoreBlock), kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s) {
+  DK_LAUNCH_GUARD(nblocks);
+  const unsigned g = (unsigned)std::min<uint64_t>((nblocks + 1023) / 1024, 512);
+  k_reduce_blocks<<<g, 256, 0, s>>>(st, nblocks);
   return hipGetLastError();
 }
 
