@@ -44,20 +44,29 @@ __device__ __forceinline__ double compute_bayes(double p1, double p2) {
   return (p1 * p2) / ((p1 * p2) + ((1.0 - p1) * (1.0 - p2)));
 }
 
-// A Java String's code units at a stride: 1 in the canonical arena, the replica's
-// position count in the transposed candidate replica.
+// A Java String's code units, read a 32-bit word (4 Latin-1 or 2 UTF-16 units) at a time.
+// Words of one value are `wstride` words apart: 1 in the canonical arena (strings start
+// 4-byte aligned, zero padded), the replica's position count in the candidate replica
+// ([word k][position g]: the 64 lanes of a wave read 64 consecutive words).  Units past
+// a value's length read as 0 in both layouts.
 template <typename CT>
 struct Str {
-  const CT* p;
-  uint64_t stride;
-  __device__ __forceinline__ uint32_t operator[](int j) const { return p[(uint64_t)j * stride]; }
+  static constexpr int UPW = 4 / (int)sizeof(CT);  // units per word
+  const uint32_t* w;
+  uint64_t wstride;
+  __device__ __forceinline__ uint32_t word(int k) const { return w[(uint64_t)k * wstride]; }
+  static __device__ __forceinline__ uint32_t unit(uint32_t x, int u) {
+    return sizeof(CT) == 1 ? (x >> (8 * u)) & 0xFFu : (x >> (16 * u)) & 0xFFFFu;
+  }
+  __device__ __forceinline__ uint32_t operator[](int j) const { return unit(word(j / UPW), j % UPW); }
 };
 
 template <typename CT>
 __device__ __forceinline__ bool str_equal(const Str<CT>& a, int na, const Str<CT>& b, int nb) {
   if (na != nb) return false;
-  for (int j = 0; j < na; ++j)
-    if (a[j] != b[j]) return false;
+  const int nw = (na + Str<CT>::UPW - 1) / Str<CT>::UPW;
+  for (int k = 0; k < nw; ++k)
+    if (a.word(k) != b.word(k)) return false;
   return true;
 }
 
@@ -122,32 +131,18 @@ __device__ __forceinline__ int ffs64(uint64_t m) { return (int)__builtin_ctzll(m
 // j is bit i of ~Peq[s2[j]].  Per cell: one v_bfe, one v_min3, one add, a min for the
 // cutoff.  Preconditions: 1 <= n1 <= MAXM; act lanes have n2 >= 1.
 // ------------------------------------------------------------------------------------
-template <int MAXM, typename CT>
-__device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1, const Str<CT>& s2,
-                                                    int n2, bool act) {
+template <int MAXM>
+struct LevCol {  // one lane's DP column over the query rows, kept in VGPRs
   int col[MAXM + 1];
-  const int maxdist = min(n1, n2) >> 1;
-  // first column: min(column[ix1-1], ix1-1) + cost
-  uint64_t ne = act ? ~peq_eq<CT>(peq, s2[0]) : ~0ull;
-  int prev = 1;
-#pragma unroll
-  for (int i = 1; i <= MAXM; ++i) {
-    if (i <= n1) {  // n1 is wave-uniform: a scalar branch, not a lane mask
-      const int v = min(prev, i - 1) + (int)((ne >> (i - 1)) & 1ull);
-      col[i] = v;
-      prev = v;
-    }
-  }
-  int result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
-  bool live = act && n2 > 1;
-  uint64_t ne_next = live ? ~peq_eq<CT>(peq, s2[1]) : ~0ull;
-  for (int j = 1; live; ++j) {
-    ne = ne_next;
-    if (j + 1 < n2) ne_next = ~peq_eq<CT>(peq, s2[j + 1]);
+  int n1, n2, maxdist, result;
+  bool live;
+
+  // column j >= 1 of Duke's loop with cost mask ne (bit i = s1[i] != s2[j])
+  __device__ __forceinline__ void step(uint64_t ne, int j) {
     int above = j + 1, diag = j, smallest = 2 * n1;
 #pragma unroll
     for (int i = 1; i <= MAXM; ++i) {
-      if (i <= n1) {
+      if (i <= n1) {  // n1 is wave-uniform: a scalar branch, not a lane mask
         const int left = col[i];
         const int v = imin3(above, diag, left) + (int)((ne >> (i - 1)) & 1ull);
         diag = left;
@@ -156,15 +151,54 @@ __device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1,
         smallest = min(smallest, v);
       }
     }
-    if (smallest > maxdist) {
+    if (smallest > maxdist) {        // Duke's cutoff: return the column minimum
       result = smallest;
       live = false;
-    } else if (j + 1 >= n2) {
+    } else if (j + 1 >= n2) {        // last column: return D[n1][n2]
       result = above;
       live = false;
     }
   }
-  return result;
+};
+
+template <int MAXM, typename CT>
+__device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1, const Str<CT>& s2,
+                                                    int n2, bool act) {
+  constexpr int UPW = Str<CT>::UPW;
+  LevCol<MAXM> L;
+  L.n1 = n1;
+  L.n2 = n2;
+  L.maxdist = min(n1, n2) >> 1;
+  L.result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
+  uint32_t w = act ? s2.word(0) : 0u;
+  // first column: min(column[ix1-1], ix1-1) + cost
+  const uint64_t ne0 = ~peq_eq<CT>(peq, Str<CT>::unit(w, 0));
+  int prev = 1;
+#pragma unroll
+  for (int i = 1; i <= MAXM; ++i) {
+    if (i <= n1) {
+      const int v = min(prev, i - 1) + (int)((ne0 >> (i - 1)) & 1ull);
+      L.col[i] = v;
+      prev = v;
+    }
+  }
+  L.live = act && n2 > 1;
+  // one word of s2 prefetched ahead (UPW columns of latency cover), and the Peq read of
+  // column j+1 issued before column j's DP so it lands while the column computes;
+  // (j + 1) % UPW is wave-uniform, so the word rotation is a scalar branch
+  uint32_t wn = L.live && UPW < n2 ? s2.word(1) : 0u;
+  uint64_t ne_next = ~peq_eq<CT>(peq, UPW > 1 ? Str<CT>::unit(w, 1) : wn);
+  for (int j = 1; L.live; ++j) {
+    const uint64_t ne = ne_next;
+    const int jn = j + 1;
+    if (jn % UPW == 0) {
+      w = wn;
+      wn = (jn + UPW) < n2 ? s2.word(jn / UPW + 1) : 0u;
+    }
+    ne_next = ~peq_eq<CT>(peq, Str<CT>::unit(w, jn % UPW));
+    L.step(ne, j);
+  }
+  return L.result;
 }
 
 // [Duke 1.2] comparators.Levenshtein.compare
@@ -241,14 +275,22 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
   {
     const int md = nq >> 1;
     int prev = -1;
-    for (int i = 0; rows_cand && i < nc; ++i) {
-      const uint64_t e = peq_eq<CT>(peq, cs[i]);
-      const uint64_t m = e & range_mask(max(0, i - md), min(nq, i + md));
-      if (m) {
-        const int j = ffs64(m);
-        ++c;
-        if (prev != -1 && j < prev) ++t;
-        prev = j;
+    constexpr int UPW = Str<CT>::UPW;
+    for (int k = 0; rows_cand && k * UPW < nc; ++k) {
+      const uint32_t w = cs.word(k);
+#pragma unroll
+      for (int u = 0; u < UPW; ++u) {
+        const int i = k * UPW + u;
+        if (i < nc) {
+          const uint64_t e = peq_eq<CT>(peq, Str<CT>::unit(w, u));
+          const uint64_t m = e & range_mask(max(0, i - md), min(nq, i + md));
+          if (m) {
+            const int j = ffs64(m);
+            ++c;
+            if (prev != -1 && j < prev) ++t;
+            prev = j;
+          }
+        }
       }
     }
   }
@@ -258,19 +300,25 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
     const int maxn = rows_query ? nc : 0;
     int wmax = maxn;
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
-    for (int j = 0; j < wmax; ++j) {
-      uint64_t m = 0;
-      if (j < maxn) {
-        const uint64_t r = peq_eq<CT>(peq, cs[j]);
-        m = r & range_mask(max(0, j - md + 1), min(nq, j + md + 1)) & ~found;
+    constexpr int UPW = Str<CT>::UPW;
+    for (int k = 0; k * UPW < wmax; ++k) {
+      const uint32_t w = k * UPW < maxn ? cs.word(k) : 0u;
+#pragma unroll
+      for (int u = 0; u < UPW; ++u) {
+        const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
+        uint64_t m = 0;
+        if (j < maxn) {
+          const uint64_t r = peq_eq<CT>(peq, Str<CT>::unit(w, u));
+          m = r & range_mask(max(0, j - md + 1), min(nq, j + md + 1)) & ~found;
+        }
+        found |= m;
+        if (j & 1) p0 |= m;
+        if (j & 2) p1 |= m;
+        if (j & 4) p2 |= m;
+        if (j & 8) p3 |= m;
+        if (j & 16) p4 |= m;
+        if (j & 32) p5 |= m;
       }
-      found |= m;
-      if (j & 1) p0 |= m;
-      if (j & 2) p1 |= m;
-      if (j & 4) p2 |= m;
-      if (j & 8) p3 |= m;
-      if (j & 16) p4 |= m;
-      if (j & 32) p5 |= m;
     }
     if (rows_query) {
       c = __popcll(found);
@@ -337,19 +385,19 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
                                              int lc, bool cmp) {
   const CT* base = reinterpret_cast<const CT*>(D.units);
-  const Str<CT> s1{base + D.off[q], 1};
-  const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const CT*>(D.runits) + g, rstride}
-                             : Str<CT>{base + D.off[crow], 1};
+  const Str<CT> s1{reinterpret_cast<const uint32_t*>(base + D.off[q]), 1};
+  const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + g, rstride}
+                             : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[crow]), 1};
   double sim = 0.0;
   switch (D.op) {
     case DK_CMP_LEVENSHTEIN:
     case DK_CMP_JAROWINKLER: {
       const bool table = lq <= 64 && (D.op == DK_CMP_LEVENSHTEIN || __ballot(cmp && lc > 64) == 0);
       if (table) {
-        peq_set(peq, s1.p, lq, true);
+        peq_set(peq, base + D.off[q], lq, true);
         sim = D.op == DK_CMP_LEVENSHTEIN ? levenshtein_peq(peq, s1, lq, s2, lc, cmp)
                                          : jarowinkler_peq(peq, s1, lq, s2, lc, cmp);
-        peq_set(peq, s1.p, lq, false);
+        peq_set(peq, base + D.off[q], lq, false);
       } else if (cmp) {
         sim = jarowinkler(s1, lq, s2, lc);
       }
@@ -546,10 +594,13 @@ __global__ void k_first(const uint32_t* __restrict__ qidx, uint64_t n, uint64_t 
 // ------------------------------------------------------------------------------------
 template <typename CT>
 __device__ __forceinline__ void replicate_units(const ReplicaJob& J, uint64_t g, uint32_t row, int l) {
-  const CT* src = reinterpret_cast<const CT*>(J.units) + J.off[row];
-  CT* dst = reinterpret_cast<CT*>(J.runits) + g;
+  // canonical words are zero padded past the value; words past it are written as 0
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(reinterpret_cast<const CT*>(J.units) + J.off[row]);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(J.runits) + g;
   const int n = l == (int)kMissing ? 0 : l;
-  for (int j = 0; j < J.rlmax; ++j) dst[(uint64_t)j * J.stride] = j < n ? src[j] : (CT)0;
+  const int upw = 4 / (int)sizeof(CT);
+  const int nw = (n + upw - 1) / upw, rw = J.rlmax / upw;
+  for (int k = 0; k < rw; ++k) dst[(uint64_t)k * J.stride] = k < nw ? src[k] : 0u;
 }
 
 __global__ __launch_bounds__(256) void k_replicate(const ReplicaJob J, const uint32_t* __restrict__ rowof,
