@@ -635,6 +635,9 @@ static ScoreParams make_params(const dk_ctx* c) {
   P.ident = c->ident.as<uint64_t>();
   P.rowof = c->rowof_p;
   P.rstride = c->rstride;
+  P.lev_rows = 0;
+  for (const auto& S : c->P)
+    if (S.cfg.comparator == DK_CMP_LEVENSHTEIN) P.lev_rows = std::max(P.lev_rows, S.maxlen);
   for (int i = 0; i < P.nprops; ++i) {
     const PropState& S = c->P[i];
     DevProp& D = P.props[i];

@@ -61,6 +61,8 @@ struct DevProp {
 struct ScoreParams {
   int32_t nprops;
   int32_t mode;
+  int32_t lev_rows;       // longest Levenshtein value in the index (selects the variant)
+  int32_t pad;
   double threshold;
   double maybe;
   const uint64_t* ident;

@@ -131,41 +131,47 @@ __device__ __forceinline__ int ffs64(uint64_t m) { return (int)__builtin_ctzll(m
 // j is bit i of ~Peq[s2[j]].  Per cell: one v_bfe, one v_min3, one add, a min for the
 // cutoff.  Preconditions: 1 <= n1 <= MAXM; act lanes have n2 >= 1.
 // ------------------------------------------------------------------------------------
-template <int MAXM>
+// R rows are computed unconditionally (R = n1 rounded up to the bucket); rows past n1
+// compute values that never feed rows <= n1 (the recurrence only looks up and left) and
+// are masked out of the cutoff minimum.  Only the last TAIL rows can lie past n1.
+template <int R>
 struct LevCol {  // one lane's DP column over the query rows, kept in VGPRs
-  int col[MAXM + 1];
+  static constexpr int TAIL = R <= 32 ? 4 : 8;
+  int col[R + 1];
   int n1, n2, maxdist, result;
   bool live;
 
   // column j >= 1 of Duke's loop with cost mask ne (bit i = s1[i] != s2[j])
   __device__ __forceinline__ void step(uint64_t ne, int j) {
-    int above = j + 1, diag = j, smallest = 2 * n1;
+    int above = j + 1, diag = j, smallest = 0x3FFFFFFF;
 #pragma unroll
-    for (int i = 1; i <= MAXM; ++i) {
-      if (i <= n1) {  // n1 is wave-uniform: a scalar branch, not a lane mask
-        const int left = col[i];
-        const int v = imin3(above, diag, left) + (int)((ne >> (i - 1)) & 1ull);
-        diag = left;
-        col[i] = v;
-        above = v;
-        smallest = min(smallest, v);
-      }
+    for (int i = 1; i <= R; ++i) {
+      const int left = col[i];
+      const int v = imin3(above, diag, left) + (int)((ne >> (i - 1)) & 1ull);
+      diag = left;
+      col[i] = v;
+      above = v;
+      // n1 is wave-uniform: the tail-row mask is a scalar select
+      smallest = min(smallest, (i <= R - TAIL || i <= n1) ? v : 0x3FFFFFFF);
     }
     if (smallest > maxdist) {        // Duke's cutoff: return the column minimum
       result = smallest;
       live = false;
     } else if (j + 1 >= n2) {        // last column: return D[n1][n2]
-      result = above;
+      int r = col[R - TAIL + 1];
+#pragma unroll
+      for (int i = R - TAIL + 2; i <= R; ++i) r = i == n1 ? col[i] : r;
+      result = r;
       live = false;
     }
   }
 };
 
-template <int MAXM, typename CT>
+template <int R, typename CT>
 __device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1, const Str<CT>& s2,
                                                     int n2, bool act) {
   constexpr int UPW = Str<CT>::UPW;
-  LevCol<MAXM> L;
+  LevCol<R> L;
   L.n1 = n1;
   L.n2 = n2;
   L.maxdist = min(n1, n2) >> 1;
@@ -175,12 +181,10 @@ __device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1,
   const uint64_t ne0 = ~peq_eq<CT>(peq, Str<CT>::unit(w, 0));
   int prev = 1;
 #pragma unroll
-  for (int i = 1; i <= MAXM; ++i) {
-    if (i <= n1) {
-      const int v = min(prev, i - 1) + (int)((ne0 >> (i - 1)) & 1ull);
-      L.col[i] = v;
-      prev = v;
-    }
+  for (int i = 1; i <= R; ++i) {
+    const int v = min(prev, i - 1) + (int)((ne0 >> (i - 1)) & 1ull);
+    L.col[i] = v;
+    prev = v;
   }
   L.live = act && n2 > 1;
   // one word of s2 prefetched ahead (UPW columns of latency cover), and the Peq read of
@@ -201,8 +205,10 @@ __device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1,
   return L.result;
 }
 
-// [Duke 1.2] comparators.Levenshtein.compare
-template <typename CT>
+// [Duke 1.2] comparators.Levenshtein.compare.  RMAX: the largest row bucket this kernel
+// variant instantiates (the host picks the variant from the longest Levenshtein value),
+// which bounds the VGPRs of the whole fused kernel and so its occupancy.
+template <int RMAX, typename CT>
 __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str<CT>& s1, int n1,
                                                   const Str<CT>& s2, int n2, bool act) {
   const int len = min(n1, n2);
@@ -215,10 +221,22 @@ __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str
     if (2 * len <= maxlen) run = false;
     else if (len == maxlen && str_equal(s1, n1, s2, n2)) { r = 1.0; run = false; }
   }
+  // row buckets of 4 up to 32 rows, of 8 above (n1 is wave-uniform: a scalar switch)
   int d;
-  if (n1 <= 16) d = compact_distance_peq<16>(peq, n1, s2, n2, run);
-  else if (n1 <= 32) d = compact_distance_peq<32>(peq, n1, s2, n2, run);
-  else d = compact_distance_peq<64>(peq, n1, s2, n2, run);
+  switch ((n1 + 3) >> 2) {
+    case 1: d = compact_distance_peq<4>(peq, n1, s2, n2, run); break;
+    case 2: d = compact_distance_peq<8>(peq, n1, s2, n2, run); break;
+    case 3: d = compact_distance_peq<12>(peq, n1, s2, n2, run); break;
+    case 4: d = compact_distance_peq<16>(peq, n1, s2, n2, run); break;
+    case 5: d = compact_distance_peq<20>(peq, n1, s2, n2, run); break;
+    case 6: d = compact_distance_peq<24>(peq, n1, s2, n2, run); break;
+    case 7: d = compact_distance_peq<28>(peq, n1, s2, n2, run); break;
+    case 8: d = compact_distance_peq<32>(peq, n1, s2, n2, run); break;
+    case 9: case 10: d = compact_distance_peq<(RMAX < 40 ? 4 : 40)>(peq, n1, s2, n2, run); break;
+    case 11: case 12: d = compact_distance_peq<(RMAX < 48 ? 4 : 48)>(peq, n1, s2, n2, run); break;
+    case 13: case 14: d = compact_distance_peq<(RMAX < 56 ? 4 : 56)>(peq, n1, s2, n2, run); break;
+    default: d = compact_distance_peq<(RMAX < 64 ? 4 : 64)>(peq, n1, s2, n2, run); break;
+  }
   if (run) {
     const int dist = min(d, len);
     r = 1.0 - ((double)dist / (double)len);
@@ -380,7 +398,7 @@ __device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool o
 // ------------------------------------------------------------------------------------
 // The fused scoring kernel.  One lane per slot, one query per wave.
 // ------------------------------------------------------------------------------------
-template <typename CT>
+template <int RMAX, typename CT>
 __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
                                              int lc, bool cmp) {
@@ -395,7 +413,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
       const bool table = lq <= 64 && (D.op == DK_CMP_LEVENSHTEIN || __ballot(cmp && lc > 64) == 0);
       if (table) {
         peq_set(peq, base + D.off[q], lq, true);
-        sim = D.op == DK_CMP_LEVENSHTEIN ? levenshtein_peq(peq, s1, lq, s2, lc, cmp)
+        sim = D.op == DK_CMP_LEVENSHTEIN ? levenshtein_peq<RMAX>(peq, s1, lq, s2, lc, cmp)
                                          : jarowinkler_peq(peq, s1, lq, s2, lc, cmp);
         peq_set(peq, base + D.off[q], lq, false);
       } else if (cmp) {
@@ -424,6 +442,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
   return sim;
 }
 
+template <int RMAX>
 __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSource S,
                                                uint64_t slot0, uint64_t nslots, StageOut out) {
   __shared__ uint64_t peq_all[kScoreBlock / 64][kPeqEntries];
@@ -469,8 +488,8 @@ __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSo
       if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
       if (cmp) bytes += 16;
     } else if (D.op != DK_CMP_NONE) {
-      sim = D.width == 1 ? string_sim<uint8_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp)
-                         : string_sim<uint16_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp);
+      sim = D.width == 1 ? string_sim<RMAX, uint8_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp)
+                         : string_sim<RMAX, uint16_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp);
       if (cmp) {
         bytes += 8u + (uint32_t)(lq + lc) * (uint32_t)D.width;
         if (D.op == DK_CMP_QGRAM) bytes += 8u + 8u * (uint32_t)(D.gcnt[q] + D.rgcnt[g]);
@@ -859,7 +878,13 @@ hipError_t launch_emit(const uint32_t* queries, uint64_t q0, uint64_t q1, const 
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                         uint64_t nslots, const StageOut& out, hipStream_t s) {
   DK_LAUNCH_GUARD(nslots);
-  k_score<<<grid1d(nslots, kScoreBlock), kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  const unsigned grid = grid1d(nslots, kScoreBlock);
+  // kernel variant by the longest Levenshtein query value (rows of the DP column)
+  if (P.lev_rows <= 16) k_score<16><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  else if (P.lev_rows <= 32) k_score<32><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  else if (P.lev_rows <= 40) k_score<40><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  else if (P.lev_rows <= 48) k_score<48><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  else k_score<64><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
   return hipGetLastError();
 }
 
