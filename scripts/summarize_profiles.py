@@ -1,0 +1,74 @@
+"""Turn rocprofv3 outputs into the committed profile summaries.
+
+usage: python scripts/summarize_profiles.py TRACE_DIR PMC_DIR OUT_DIR
+  TRACE_DIR: rocprofv3 --kernel-trace --stats --output-format csv -d TRACE_DIR
+  PMC_DIR:   scripts/pmc_profile.sh PMC_DIR (valu / fetch / write / stall passes)
+Writes OUT_DIR/kernel_stats.csv (copy of rocprofv3's stats), OUT_DIR/pmc_k_score.txt and
+profiles/pmc_k_score.json (read by bench.py for roofline.traffic).
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
+KiB, and on gfx950 FETCH_SIZE reads exactly half the bytes of a wide coalesced stream, so
+the read side is doubled (an upper bound for the k_score access mix, whose candidate-replica
+reads are 4-byte words coalesced across a wave).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+
+def pmc(pass_dir):
+    f = glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True)
+    agg, disp = collections.defaultdict(float), set()
+    if not f:
+        return agg, 0
+    for r in csv.DictReader(open(f[0])):
+        agg[r["Counter_Name"]] += float(r["Counter_Value"])
+        disp.add(r["Dispatch_Id"])
+    return agg, len(disp)
+
+
+def main():
+    trace, pmcdir, out = sys.argv[1:4]
+    os.makedirs(out, exist_ok=True)
+    stats = glob.glob(os.path.join(trace, "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(out, "kernel_stats.csv"))
+    res = {}
+    for name in ("valu", "fetch", "write", "stall"):
+        agg, n = pmc(os.path.join(pmcdir, name))
+        res[name] = (dict(agg), n)
+    fetch_kb, n = res["fetch"][0].get("FETCH_SIZE", 0.0), max(1, res["fetch"][1])
+    write_kb = res["write"][0].get("WRITE_SIZE", 0.0)
+    v, s = res["valu"][0], res["stall"][0]
+    per_launch = (2.0 * fetch_kb + write_kb) * 1024.0 / n
+    summary = {
+        "kernel": "k_score",
+        "launches_profiled": n,
+        "fetch_size_kib_total": fetch_kb,
+        "write_size_kib_total": write_kb,
+        "hbm_bytes_per_launch": per_launch,
+        "hbm_bytes_per_launch_uncorrected": (fetch_kb + write_kb) * 1024.0 / n,
+        "valu_insts_per_wave": v.get("SQ_INSTS_VALU", 0) / max(1.0, v.get("SQ_WAVES", 1)),
+        "valu_thread_utilization": v.get("SQ_THREAD_CYCLES_VALU", 0) /
+                                   max(1.0, v.get("SQ_ACTIVE_INST_VALU", 1) * 64),
+        "wait_any_frac": s.get("SQ_WAIT_ANY", 0) / max(1.0, s.get("SQ_WAVE_CYCLES", 1)),
+        "wait_inst_any_frac": s.get("SQ_WAIT_INST_ANY", 0) / max(1.0, s.get("SQ_WAVE_CYCLES", 1)),
+        "active_inst_any_frac": s.get("SQ_ACTIVE_INST_ANY", 0) / max(1.0, s.get("SQ_WAVE_CYCLES", 1)),
+        "lds_bank_conflict_cycles": s.get("SQ_LDS_BANK_CONFLICT", 0),
+        "counters": {k: v for d in res.values() for k, v in d[0].items()},
+    }
+    with open(os.path.join(out, "pmc_k_score.txt"), "w") as f:
+        for k, val in summary.items():
+            f.write(f"{k}: {val}\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "profiles", "pmc_k_score.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({k: summary[k] for k in list(summary)[:12]}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
