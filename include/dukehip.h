@@ -60,13 +60,16 @@ extern "C" {
 #define DK_CMP_QGRAM 3                /* comparators.QGramComparator */
 #define DK_CMP_EXACT 4                /* comparators.ExactComparator */
 #define DK_CMP_NUMERIC 5              /* comparators.NumericComparator */
-#define DK_CMP_WEIGHTED_LEVENSHTEIN 6 /* comparators.WeightedLevenshtein (reserved) */
+#define DK_CMP_WEIGHTED_LEVENSHTEIN 6 /* comparators.WeightedLevenshtein (default weights) */
+#define DK_CMP_DICE_TOKENS 7          /* comparators.DiceCoefficientComparator (Exact sub-comparator) */
+#define DK_CMP_JACCARD_TOKENS 8       /* comparators.JaccardIndexComparator (Exact sub-comparator) */
 
 #define DK_QGRAM_OVERLAP 0 /* QGramComparator.Formula */
 #define DK_QGRAM_JACCARD 1
 #define DK_QGRAM_DICE 2
 #define DK_QGRAM_BASIC 0 /* QGramComparator.Tokenizer */
 #define DK_QGRAM_POSITIONAL 1
+#define DK_QGRAM_ENDS 2
 
 #define DK_MODE_DEDUP 0    /* <Deduplication>: every other record is a candidate */
 #define DK_MODE_LINKAGE 1  /* <RecordLinkage>: candidates only from the other group */
@@ -79,7 +82,7 @@ typedef struct dk_property {
   int32_t comparator;      /* DK_CMP_* */
   int32_t qgram_q;         /* QGramComparator.setQ (default 2; 1..4) */
   int32_t qgram_formula;   /* DK_QGRAM_OVERLAP/JACCARD/DICE */
-  int32_t qgram_tokenizer; /* DK_QGRAM_BASIC/POSITIONAL (POSITIONAL: q <= 3) */
+  int32_t qgram_tokenizer; /* DK_QGRAM_BASIC/POSITIONAL/ENDS (POSITIONAL: q <= 3) */
   double low;              /* <low> */
   double high;             /* <high> */
   double min_ratio;        /* NumericComparator.setMinRatio (default 0.0) */

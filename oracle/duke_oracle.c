@@ -133,7 +133,22 @@ static int cmp_u64(const void* a, const void* b) {
   return x < y ? -1 : (x > y ? 1 : 0);
 }
 
-static int qgram_set(const uint16_t* s, int n, int q, int tokenizer, uint64_t* out) {
+/* ENDS [recalled, low confidence]: the BASIC grams plus the start gram "^" + s[0, q-1)
+ * and the end gram s[n-q+1, n) + "$" — exactly the grams of "^" + s + "$" (a Java
+ * HashSet<String>, so a marker gram may coincide with a real one). */
+static int qgram_set(const uint16_t* s0, int n0, int q, int tokenizer, uint64_t* out) {
+  const uint16_t* s = s0;
+  int n = n0;
+  uint16_t ends_buf[260];
+  uint16_t* ends = NULL;
+  if (tokenizer == DKO_QT_ENDS) {
+    ends = n0 + 2 <= 260 ? ends_buf : (uint16_t*)malloc(sizeof(uint16_t) * (size_t)(n0 + 2));
+    ends[0] = '^';
+    memcpy(ends + 1, s0, sizeof(uint16_t) * (size_t)n0);
+    ends[n0 + 1] = '$';
+    s = ends;
+    n = n0 + 2;
+  }
   int m = 0;
   for (int ix = 0; ix < n - q + 1; ix++) {
     uint64_t g = 0;
@@ -141,6 +156,7 @@ static int qgram_set(const uint16_t* s, int n, int q, int tokenizer, uint64_t* o
     if (tokenizer == DKO_QT_POSITIONAL) g |= (uint64_t)ix << 48;
     out[m++] = g;
   }
+  if (ends && ends != ends_buf) free(ends);
   qsort(out, (size_t)m, sizeof(uint64_t), cmp_u64);
   int u = 0;
   for (int i = 0; i < m; i++)
@@ -152,9 +168,9 @@ static int qgram_set(const uint16_t* s, int n, int q, int tokenizer, uint64_t* o
 double dko_qgram(const uint16_t* s1, int n1, const uint16_t* s2, int n2,
                  int q, int formula, int tokenizer) {
   if (u16eq(s1, n1, s2, n2)) return 1.0;
-  uint64_t st1[260], st2[260];
-  uint64_t* g1 = n1 < 260 ? st1 : (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n1 + 1));
-  uint64_t* g2 = n2 < 260 ? st2 : (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n2 + 1));
+  uint64_t st1[264], st2[264];
+  uint64_t* g1 = n1 < 260 ? st1 : (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n1 + 3));
+  uint64_t* g2 = n2 < 260 ? st2 : (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n2 + 3));
   int m1 = qgram_set(s1, n1, q, tokenizer, g1);
   int m2 = qgram_set(s2, n2, q, tokenizer, g2);
   double r;
@@ -318,6 +334,52 @@ double dko_weighted_levenshtein(const uint16_t* s1, int n1, const uint16_t* s2, 
   return 1.0 - (dist / maxlen);
 }
 
+/* [Duke 1.2, recalled] utils.StringUtils.split: the maximal runs of non-' ' units, as
+ * (start, length) pairs; returns the token count. */
+static int split_tokens(const uint16_t* s, int n, int* start, int* len) {
+  int t = 0, i = 0;
+  while (i < n) {
+    while (i < n && s[i] == ' ') i++;
+    if (i >= n) break;
+    int a = i;
+    while (i < n && s[i] != ' ') i++;
+    start[t] = a;
+    len[t] = i - a;
+    t++;
+  }
+  return t;
+}
+
+/* [Duke 1.2, recalled, low confidence] comparators.DiceCoefficientComparator /
+ * JaccardIndexComparator with the default ExactComparator sub-comparator: equal -> 1.0;
+ * t1 = the token list with fewer tokens (s1 on a tie); for each t1 token the highest
+ * sub-comparator score against t2 (Math.max from 0.0), summed; Dice = (sum * 2) /
+ * (|t1| + |t2|); Jaccard = sum / union with union = |t1| + |t2| reduced by each highest. */
+double dko_token_similarity(const uint16_t* s1, int n1, const uint16_t* s2, int n2, int jaccard) {
+  if (u16eq(s1, n1, s2, n2)) return 1.0;
+  int* b = (int*)malloc(sizeof(int) * (size_t)(2 * (n1 + n2) + 4));
+  int *st1 = b, *ln1 = b + n1 + 1, *st2 = b + 2 * n1 + 2, *ln2 = st2 + n2 + 1;
+  int m1 = split_tokens(s1, n1, st1, ln1);
+  int m2 = split_tokens(s2, n2, st2, ln2);
+  if (m1 > m2) {
+    const uint16_t* ts = s1; s1 = s2; s2 = ts;
+    int* tp = st1; st1 = st2; st2 = tp;
+    tp = ln1; ln1 = ln2; ln2 = tp;
+    int tm = m1; m1 = m2; m2 = tm;
+  }
+  double sum = 0.0, uni = (double)(m1 + m2);
+  for (int i = 0; i < m1; i++) {
+    double highest = 0.0;
+    for (int j = 0; j < m2; j++)
+      highest = dko_java_max(highest, dko_exact(s1 + st1[i], ln1[i], s2 + st2[j], ln2[j]));
+    sum += highest;
+    uni -= highest;
+  }
+  free(b);
+  if (jaccard) return sum / uni;
+  return (sum * 2) / (double)(m1 + m2);
+}
+
 /* java.lang.Math.max(double, double): NaN if either is NaN; +0.0 beats -0.0. */
 double dko_java_max(double a, double b) {
   if (a != a) return a;
@@ -343,6 +405,8 @@ double dko_property_compare(const dko_prop* p, const uint16_t* s1, int n1,
     case DKO_CMP_EXACT: sim = dko_exact(s1, n1, s2, n2); break;
     case DKO_CMP_NUMERIC: sim = dko_numeric(s1, n1, s2, n2, p->min_ratio); break;
     case DKO_CMP_WEIGHTED_LEVENSHTEIN: sim = dko_weighted_levenshtein(s1, n1, s2, n2); break;
+    case DKO_CMP_DICE_TOKENS: sim = dko_token_similarity(s1, n1, s2, n2, 0); break;
+    case DKO_CMP_JACCARD_TOKENS: sim = dko_token_similarity(s1, n1, s2, n2, 1); break;
     default: return 0.5;
   }
   if (sim < 0.5) return p->low;

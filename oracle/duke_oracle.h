@@ -31,10 +31,12 @@ enum {
   DKO_CMP_QGRAM = 3,
   DKO_CMP_EXACT = 4,
   DKO_CMP_NUMERIC = 5,
-  DKO_CMP_WEIGHTED_LEVENSHTEIN = 6
+  DKO_CMP_WEIGHTED_LEVENSHTEIN = 6,
+  DKO_CMP_DICE_TOKENS = 7,   /* DiceCoefficientComparator (ExactComparator sub-comparator) */
+  DKO_CMP_JACCARD_TOKENS = 8 /* JaccardIndexComparator (ExactComparator sub-comparator) */
 };
 enum { DKO_QF_OVERLAP = 0, DKO_QF_JACCARD = 1, DKO_QF_DICE = 2 };
-enum { DKO_QT_BASIC = 0, DKO_QT_POSITIONAL = 1 };
+enum { DKO_QT_BASIC = 0, DKO_QT_POSITIONAL = 1, DKO_QT_ENDS = 2 };
 enum { DKO_MODE_DEDUP = 0, DKO_MODE_LINKAGE = 1, DKO_MODE_ALLPAIRS = 2 };
 enum { DKO_KIND_MATCH = 1, DKO_KIND_MAYBE = 2 };
 
@@ -49,6 +51,7 @@ double dko_exact(const uint16_t* s1, int n1, const uint16_t* s2, int n2);
 int    dko_parse_java_double(const uint16_t* s, int n, double* out);
 double dko_numeric(const uint16_t* s1, int n1, const uint16_t* s2, int n2, double min_ratio);
 double dko_weighted_levenshtein(const uint16_t* s1, int n1, const uint16_t* s2, int n2);
+double dko_token_similarity(const uint16_t* s1, int n1, const uint16_t* s2, int n2, int jaccard);
 
 /* ---- probability model ---- */
 double dko_java_max(double a, double b);                 /* java.lang.Math.max */

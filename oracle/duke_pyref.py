@@ -17,8 +17,10 @@ import math
 import re
 
 LEVENSHTEIN, JAROWINKLER, QGRAM, EXACT, NUMERIC, WEIGHTED_LEVENSHTEIN = 1, 2, 3, 4, 5, 6
+DICE_TOKENS, JACCARD_TOKENS = 7, 8
 OVERLAP, JACCARD, DICE = 0, 1, 2
-BASIC, POSITIONAL = 0, 1
+BASIC, POSITIONAL, ENDS = 0, 1, 2
+_CARET, _DOLLAR = ord("^"), ord("$")
 
 
 def units(s: str) -> tuple:
@@ -95,6 +97,12 @@ def jarowinkler(s1, s2) -> float:
 
 
 def qgrams(s, q, tokenizer=BASIC) -> set:
+    """QGramComparator.Tokenizer: BASIC substrings; POSITIONAL substring + index;
+    ENDS [recalled, low confidence] BASIC plus the start gram "^" + s[0:q-1] and the end
+    gram s[n-q+1:] + "$" — i.e. the q-grams of "^" + s + "$" (HashSet<String>, so marker
+    grams may coincide with real ones)."""
+    if tokenizer == ENDS:
+        s = (_CARET,) + tuple(s) + (_DOLLAR,)
     out = set()
     for ix in range(0, len(s) - q + 1):
         g = tuple(s[ix:ix + q])
@@ -119,6 +127,108 @@ def qgram(s1, s2, q=2, formula=OVERLAP, tokenizer=BASIC) -> float:
 
 def exact(s1, s2) -> float:
     return 1.0 if tuple(s1) == tuple(s2) else 0.0
+
+
+def _wl_weight(ch):
+    """[Duke 1.2, recalled] WeightedLevenshtein.DefaultWeightEstimator: letters 1.0,
+    digits 2.0, punctuation / space 0.1, anything else 1.0."""
+    if ord("a") <= ch <= ord("z") or ord("A") <= ch <= ord("Z"):
+        return 1.0
+    if ord("0") <= ch <= ord("9"):
+        return 2.0
+    if chr(ch) in " '.-/\\,\"":
+        return 0.1
+    return 1.0
+
+
+def weighted_distance(s1, s2):
+    """[Duke 1.2, recalled] WeightedLevenshtein.distance, literally: one flat array
+    addressed ix1 + s1len * ix2 (stride s1len, not s1len + 1), column init then row init,
+    s1-major loop nest."""
+    n1, n2 = len(s1), len(s2)
+    if n1 == 0:
+        return sum_weights(s2)
+    if n2 == 0:
+        return sum_weights(s1)
+    m = [0.0] * ((n1 + 1) * (n2 + 1))
+    for col in range(n2 + 1):
+        m[col * n1] = float(col)
+    for row in range(n1 + 1):
+        m[row] = float(row)
+    for ix1 in range(n1):
+        ch1 = s1[ix1]
+        for ix2 in range(n2):
+            ch2 = s2[ix2]
+            cost = 0.0 if ch1 == ch2 else max(_wl_weight(ch1), _wl_weight(ch2))
+            left = m[ix1 + (ix2 + 1) * n1] + _wl_weight(ch1)
+            above = m[ix1 + 1 + ix2 * n1] + _wl_weight(ch2)
+            aboveleft = m[ix1 + ix2 * n1] + cost
+            m[ix1 + 1 + (ix2 + 1) * n1] = min(left, min(above, aboveleft))
+    return m[n1 + n2 * n1]
+
+
+def sum_weights(s):
+    e = 0.0
+    for ch in s:
+        e += _wl_weight(ch)
+    return e
+
+
+def weighted_levenshtein(s1, s2) -> float:
+    """[Duke 1.2, recalled] WeightedLevenshtein.compare: 1 - dist / maxlen, 0 if dist >
+    maxlen."""
+    if tuple(s1) == tuple(s2):
+        return 1.0
+    dist = weighted_distance(s1, s2)
+    maxlen = float(max(len(s1), len(s2)))
+    if dist > maxlen:
+        return 0.0
+    return 1.0 - (dist / maxlen)
+
+
+def split_tokens(s):
+    """[Duke 1.2, recalled] utils.StringUtils.split: maximal runs of non-' ' units."""
+    out, cur = [], []
+    for ch in s:
+        if ch == 0x20:
+            if cur:
+                out.append(tuple(cur))
+            cur = []
+        else:
+            cur.append(ch)
+    if cur:
+        out.append(tuple(cur))
+    return out
+
+
+def token_set_similarity(s1, s2, jaccard):
+    """[Duke 1.2, recalled, low confidence] DiceCoefficientComparator /
+    JaccardIndexComparator with the default ExactComparator sub-comparator: t1 = the
+    token list with fewer tokens (s1 on a tie); per t1 token the best sub-comparator score
+    against t2; Dice = 2*sum / (|t1|+|t2|), Jaccard = sum / (|t1|+|t2| - sum) with the
+    union reduced token by token."""
+    if tuple(s1) == tuple(s2):
+        return 1.0
+    t1, t2 = split_tokens(s1), split_tokens(s2)
+    if len(t1) > len(t2):
+        t1, t2 = t2, t1
+    total = 0.0
+    union = float(len(t1) + len(t2))
+    for a in t1:
+        highest = 0.0
+        for b in t2:
+            highest = max(highest, exact(a, b))
+        total += highest
+        union -= highest
+    if jaccard:
+        return _div(total, union)
+    return _div(total * 2, float(len(t1) + len(t2)))
+
+
+def _div(num, den):
+    if den == 0.0:
+        return math.nan if num == 0.0 else math.copysign(math.inf, num)
+    return num / den
 
 
 _DEC = re.compile(r"^[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?[fFdD]?$")
@@ -205,6 +315,10 @@ def property_compare(prop, v1, v2):
         sim = exact(v1, v2)
     elif c == NUMERIC:
         sim = numeric(v1, v2, prop.get("min_ratio", 0.0))
+    elif c == WEIGHTED_LEVENSHTEIN:
+        sim = weighted_levenshtein(v1, v2)
+    elif c in (DICE_TOKENS, JACCARD_TOKENS):
+        sim = token_set_similarity(v1, v2, c == JACCARD_TOKENS)
     else:
         return 0.5
     if sim < 0.5:

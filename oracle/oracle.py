@@ -65,6 +65,8 @@ def lib():
             f.argtypes = [u16p, C.c_int, u16p, C.c_int]
         L.dko_compact_distance.restype = C.c_int
         L.dko_compact_distance.argtypes = [u16p, C.c_int, u16p, C.c_int]
+        L.dko_token_similarity.restype = C.c_double
+        L.dko_token_similarity.argtypes = [u16p, C.c_int, u16p, C.c_int, C.c_int]
         L.dko_qgram.restype = C.c_double
         L.dko_qgram.argtypes = [u16p, C.c_int, u16p, C.c_int, C.c_int, C.c_int, C.c_int]
         L.dko_numeric.restype = C.c_double
@@ -132,6 +134,10 @@ def numeric(s1, s2, min_ratio=0.0):
 
 def weighted_levenshtein(s1, s2):
     return _call2("dko_weighted_levenshtein", s1, s2)
+
+
+def token_similarity(s1, s2, jaccard):
+    return _call2("dko_token_similarity", s1, s2, 1 if jaccard else 0)
 
 
 def parse_java_double(s):

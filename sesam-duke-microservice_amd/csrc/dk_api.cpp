@@ -171,9 +171,22 @@ static bool java_parse_double(const uint16_t* u, size_t n, double* out) {
 }
 
 // q-gram set of one value: sorted unique 64-bit codes, 16 bits per code unit
-// (QGramComparator's HashSet<String> of substrings; POSITIONAL adds the index).
-static void qgram_codes(const uint16_t* u, int n, int q, int tokenizer, std::vector<uint64_t>& g) {
+// (QGramComparator's HashSet<String> of substrings; POSITIONAL adds the index; ENDS
+// [recalled] adds the start gram "^" + s[0, q-1) and the end gram s[n-q+1, n) + "$",
+// i.e. it takes the grams of "^" + s + "$").
+static void qgram_codes(const uint16_t* u0, int n0, int q, int tokenizer, std::vector<uint64_t>& g) {
   g.clear();
+  std::vector<uint16_t> ends;
+  const uint16_t* u = u0;
+  int n = n0;
+  if (tokenizer == DK_QGRAM_ENDS) {
+    ends.resize(n0 + 2);
+    ends[0] = '^';
+    std::copy(u0, u0 + n0, ends.begin() + 1);
+    ends[n0 + 1] = '$';
+    u = ends.data();
+    n = n0 + 2;
+  }
   for (int ix = 0; ix + q <= n; ++ix) {
     uint64_t c = 0;
     for (int k = 0; k < q; ++k) c = (c << 16) | u[ix + k];
@@ -184,11 +197,32 @@ static void qgram_codes(const uint16_t* u, int n, int q, int tokenizer, std::vec
   g.erase(std::unique(g.begin(), g.end()), g.end());
 }
 
+// [Duke 1.2, recalled] utils.StringUtils.split — the maximal runs of non-' ' units — as
+// exact token ids (interned per property across batches), sorted with duplicates kept:
+// the token comparators count, per token of the shorter list, membership in the other.
+static void token_codes(const uint16_t* u, int n, std::unordered_map<std::u16string, uint64_t>& tab,
+                        std::vector<uint64_t>& g) {
+  g.clear();
+  int i = 0;
+  while (i < n) {
+    while (i < n && u[i] == ' ') ++i;
+    if (i >= n) break;
+    const int a = i;
+    while (i < n && u[i] != ' ') ++i;
+    std::u16string t(reinterpret_cast<const char16_t*>(u + a), (size_t)(i - a));
+    auto it = tab.find(t);
+    if (it == tab.end()) it = tab.emplace(std::move(t), (uint64_t)tab.size()).first;
+    g.push_back(it->second);
+  }
+  std::sort(g.begin(), g.end());
+}
+
 // ----------------------------------------------------------------------------------------
 // context
 // ----------------------------------------------------------------------------------------
 struct PropState {
   dk_property cfg{};
+  std::unordered_map<std::u16string, uint64_t> tokens;  // token comparators: token -> id
   int width = 0;           // arena width; 0 until the first batch
   uint64_t units_used = 0; // code units
   uint64_t grams_used = 0;
@@ -275,7 +309,7 @@ static hipError_t grow_rows(dk_ctx* c, uint64_t need) {
       GROW(p.num, double);
       GROW(p.numok, uint8_t);
     }
-    if (p.cfg.comparator == DK_CMP_QGRAM) {
+    if (uses_codes(p.cfg.comparator)) {
       GROW(p.goff, uint32_t);
       GROW(p.gcnt, uint16_t);
     }
@@ -302,6 +336,9 @@ static int validate_schema(const dk_schema* s) {
       case DK_CMP_JAROWINKLER:
       case DK_CMP_EXACT:
       case DK_CMP_NUMERIC:
+      case DK_CMP_WEIGHTED_LEVENSHTEIN:
+      case DK_CMP_DICE_TOKENS:
+      case DK_CMP_JACCARD_TOKENS:
         break;
       case DK_CMP_QGRAM:
         if (p.qgram_q < 1 || p.qgram_q > 4)
@@ -309,7 +346,8 @@ static int validate_schema(const dk_schema* s) {
                       p.qgram_q);
         if (p.qgram_tokenizer == DK_QGRAM_POSITIONAL && p.qgram_q > 3)
           return fail(DK_E_UNSUPPORTED, "property %d: POSITIONAL tokenizer needs q <= 3", i);
-        if (p.qgram_tokenizer != DK_QGRAM_BASIC && p.qgram_tokenizer != DK_QGRAM_POSITIONAL)
+        if (p.qgram_tokenizer != DK_QGRAM_BASIC && p.qgram_tokenizer != DK_QGRAM_POSITIONAL &&
+            p.qgram_tokenizer != DK_QGRAM_ENDS)
           return fail(DK_E_UNSUPPORTED, "property %d: q-gram tokenizer %d", i, p.qgram_tokenizer);
         if (p.qgram_formula < DK_QGRAM_OVERLAP || p.qgram_formula > DK_QGRAM_DICE)
           return fail(DK_E_UNSUPPORTED, "property %d: q-gram formula %d", i, p.qgram_formula);
@@ -426,7 +464,9 @@ static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, 
   std::vector<uint16_t> len(n);
   std::vector<uint8_t> bytes;
   uint64_t cur = P.units_used;
-  const bool is_lev = P.cfg.comparator == DK_CMP_LEVENSHTEIN;
+  // values on the DP comparators are bounded by the long-value DP (query rows <= 256)
+  const bool is_dp = P.cfg.comparator == DK_CMP_LEVENSHTEIN ||
+                     P.cfg.comparator == DK_CMP_WEIGHTED_LEVENSHTEIN;
   std::vector<uint16_t> u16;
   std::vector<double> num;
   std::vector<uint8_t> numok;
@@ -434,7 +474,8 @@ static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, 
   std::vector<uint16_t> gcnt;
   std::vector<uint64_t> grams, g;
   const bool is_num = P.cfg.comparator == DK_CMP_NUMERIC;
-  const bool is_qg = P.cfg.comparator == DK_CMP_QGRAM;
+  const bool is_qg = uses_codes(P.cfg.comparator);
+  const bool is_tok = P.cfg.comparator != DK_CMP_QGRAM;
   if (is_num) { num.assign(n, 0.0); numok.assign(n, 0); }
   if (is_qg) { goff.assign(n, 0); gcnt.assign(n, 0); }
   for (uint64_t i = 0; i < n; ++i) {
@@ -446,10 +487,10 @@ static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, 
     if (present && L >= kMissing)
       return fail(DK_E_UNSUPPORTED, "property %d: value of %llu units (max %u)", pidx,
                   (unsigned long long)L, (unsigned)kMissing - 1);
-    if (present && is_lev && L > (uint64_t)kMaxUnits)
+    if (present && is_dp && L > (uint64_t)kMaxLongUnits)
       return fail(DK_E_UNSUPPORTED,
-                  "property %d: Levenshtein value of %llu units (GPU limit %d)", pidx,
-                  (unsigned long long)L, kMaxUnits);
+                  "property %d: (Weighted)Levenshtein value of %llu units (GPU limit %d)", pidx,
+                  (unsigned long long)L, kMaxLongUnits);
     off[i] = (uint32_t)cur;
     len[i] = present ? (uint16_t)L : kMissing;
     if (!present) continue;
@@ -469,9 +510,10 @@ static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, 
       num[i] = v;
     }
     if (is_qg) {
-      qgram_codes(u16.data(), (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, g);
+      if (is_tok) token_codes(u16.data(), (int)L, P.tokens, g);
+      else qgram_codes(u16.data(), (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, g);
       if (g.size() >= kMissing)
-        return fail(DK_E_UNSUPPORTED, "property %d: %zu q-grams", pidx, g.size());
+        return fail(DK_E_UNSUPPORTED, "property %d: %zu q-grams / tokens", pidx, g.size());
       goff[i] = (uint32_t)(P.grams_used + grams.size());
       gcnt[i] = (uint16_t)g.size();
       grams.insert(grams.end(), g.begin(), g.end());
@@ -636,8 +678,15 @@ static ScoreParams make_params(const dk_ctx* c) {
   P.rowof = c->rowof_p;
   P.rstride = c->rstride;
   P.lev_rows = 0;
-  for (const auto& S : c->P)
-    if (S.cfg.comparator == DK_CMP_LEVENSHTEIN) P.lev_rows = std::max(P.lev_rows, S.maxlen);
+  P.long_rows = 0;
+  for (const auto& S : c->P) {
+    if (S.cfg.comparator == DK_CMP_LEVENSHTEIN) {
+      P.lev_rows = std::max(P.lev_rows, std::min(S.maxlen, kMaxUnits));
+      if (S.maxlen > kMaxUnits) P.long_rows = std::max(P.long_rows, S.maxlen);
+    }
+    if (S.cfg.comparator == DK_CMP_WEIGHTED_LEVENSHTEIN)
+      P.long_rows = std::max(P.long_rows, std::max(S.maxlen, 1));
+  }
   for (int i = 0; i < P.nprops; ++i) {
     const PropState& S = c->P[i];
     DevProp& D = P.props[i];
@@ -677,12 +726,13 @@ static int build_replica(dk_ctx* c, const uint32_t* rowof, uint64_t npos) {
   for (auto& S : c->P) {
     const int op = S.cfg.comparator;
     const bool strcmp_ = op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER ||
-                         op == DK_CMP_EXACT || op == DK_CMP_QGRAM;
+                         op == DK_CMP_EXACT || uses_codes(op) ||
+                         op == DK_CMP_WEIGHTED_LEVENSHTEIN;
     const int W = S.width ? S.width : 1;
     S.rlmax = strcmp_ && S.maxlen <= kMaxReplicaUnits ? ((std::max(S.maxlen, 1) + 3) & ~3) : 0;
     HIPCHK(S.rlen.reserve(npos * 2 + 8, 0, s));
     if (S.rlmax) HIPCHK(S.runits.reserve(npos * (uint64_t)S.rlmax * W + 64, 0, s));
-    const bool num = op == DK_CMP_NUMERIC, qg = op == DK_CMP_QGRAM;
+    const bool num = op == DK_CMP_NUMERIC, qg = uses_codes(op);
     if (num) {
       HIPCHK(S.rnum.reserve(npos * 8 + 8, 0, s));
       HIPCHK(S.rnumok.reserve(npos + 8, 0, s));

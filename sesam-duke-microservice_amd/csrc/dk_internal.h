@@ -12,9 +12,17 @@ namespace dk {
 constexpr int kMaxProps = 16;
 constexpr int kMaxKeys = 8;
 constexpr uint16_t kMissing = 0xFFFF;  // length sentinel: record has no value
-constexpr int kMaxUnits = 64;          // Levenshtein value limit of the lane-per-pair kernel
+constexpr int kMaxUnits = 64;          // Levenshtein query limit of the lane-per-pair DP
+constexpr int kMaxLongUnits = 256;     // WeightedLevenshtein / long Levenshtein value limit
 constexpr int kMaxReplicaUnits = 64;   // longer columns are read in place (canonical arena)
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // filtered candidate slot
+
+// comparators whose values carry a precomputed sorted code list (goff/gcnt/grams):
+// QGram sets (sorted unique packed grams) and the token comparators (sorted token ids,
+// duplicates kept)
+__host__ __device__ constexpr bool uses_codes(int op) {
+  return op == DK_CMP_QGRAM || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS;
+}
 
 constexpr uint8_t kAlive = 1;    // not superseded by a later upsert of the same ID
 constexpr uint8_t kDeleted = 2;  // dukeDeleted == "true" (IncrementalLuceneDatabase.java:478)
@@ -24,7 +32,8 @@ constexpr uint8_t kDeleted = 2;  // dukeDeleted == "true" (IncrementalLuceneData
 //  canonical index (row-indexed, grows with dk_upsert):
 //    per property: off[row] (first code unit, 4-byte aligned), len[row] (kMissing = no
 //    value), units arena (u8 or u16, zero padded), num/numok (NUMERIC), goff/gcnt/grams
-//    (QGRAM, sorted unique packed grams); per row: ident, flags, group; per key function
+//    (QGRAM: sorted unique packed grams; DICE/JACCARD_TOKENS: sorted token ids with
+//    duplicates); per row: ident, flags, group; per key function
 //    keys[k][row].
 //  candidate replica (rebuilt by every dk_match after the blocking sort): the K key
 //    functions' sorted candidate lists concatenated — position g = k * M + i holds row
@@ -62,7 +71,7 @@ struct ScoreParams {
   int32_t nprops;
   int32_t mode;
   int32_t lev_rows;       // longest Levenshtein value in the index (selects the variant)
-  int32_t pad;
+  int32_t long_rows;      // longest value on the long-value DP (0 = none; selects the variant)
   double threshold;
   double maybe;
   const uint64_t* ident;

@@ -12,6 +12,7 @@
 #include <cstring>
 
 #include <algorithm>
+#include <type_traits>
 #include <rocprim/rocprim.hpp>
 
 #include "dk_internal.h"
@@ -244,6 +245,196 @@ __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str
   return r;
 }
 
+// ------------------------------------------------------------------------------------
+// Long-value DP: WeightedLevenshtein (any length) and Levenshtein with a query value over
+// 64 units, both up to kMaxLongUnits.  One candidate per 16-lane DPP row (4 pairs per
+// wave, all against the wave's query); lane k of a row owns query rows
+// i in (k*R, k*R + R] and, at step t, computes DP column j = t - k + 1 of them
+// (anti-diagonal / systolic schedule).  Row k*R of column j arrives from lane k-1 by DPP
+// row_shr:1; lane 0 takes the matrix's top boundary instead.  Every cell is a pure
+// function of its three neighbours, so this order yields the cells of the Java loop nest
+// bit for bit.
+//
+// Both comparators reduce to a full (n1+1) x (n2+1) matrix D with D(i,0) = i:
+//  * Levenshtein.compactDistance: D(0,j) = j, D(i,j) = min(D(i-1,j), D(i-1,j-1),
+//    D(i,j-1)) + cost — Duke's column loop with its virtual first row (ix2+1) and first
+//    column min(column[ix1-1], ix1-1) + cost, re-indexed by one column.  The early-exit
+//    cutoff is not replayed: when it fires (column minimum m > min(n1,n2)/2) the full
+//    matrix's D(n1,n2) >= min(m, j) > maxdist as well, so the similarity is < 0.5 either
+//    way and PropertyImpl maps both to `low`.
+//  * WeightedLevenshtein.distance over the flat array of stride s1len: cell (s1len, c)
+//    aliases (0, c+1), which leaves D(0,1) = n1 (the row init overwrites it) and, for
+//    n1 == 1, makes row 0 of column j read the row-1 value of column j-1.  Cell:
+//    min(D(i-1,j) + w(s1[i-1]), D(i,j-1) + w(s2[j-1]), D(i-1,j-1) + cost).
+// ------------------------------------------------------------------------------------
+constexpr int kLongRowLanes = 16;  // lanes per candidate (one DPP row)
+
+// [Duke 1.2] comparators.WeightedLevenshtein.DefaultWeightEstimator: letters 1.0,
+// digits 2.0, punctuation 0.1, anything else 1.0
+__device__ __forceinline__ double wl_weight(uint32_t ch) {
+  if ((ch | 0x20u) - 'a' < 26u) return 1.0;
+  if (ch - '0' < 10u) return 2.0;
+  // ' ' '"' '\'' ',' '-' '.' '/' below 64, and '\\'
+  constexpr uint64_t kPunct = (1ull << ' ') | (1ull << '"') | (1ull << '\'') | (1ull << ',') |
+                              (1ull << '-') | (1ull << '.') | (1ull << '/');
+  if ((ch < 64u && ((kPunct >> ch) & 1ull)) || ch == '\\') return 0.1;
+  return 1.0;
+}
+
+__device__ __forceinline__ int dpp_row_shr1(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, 0x111, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ double dpp_row_shr1(double old, double v) {
+  const uint64_t o = (uint64_t)__double_as_longlong(old), x = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)o, (int)(uint32_t)x, 0x111, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(o >> 32), (int)(uint32_t)(x >> 32),
+                                                            0x111, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// Per-wave LDS of the long-value section (inside the wave's Peq slice, zeroed on exit):
+// u16 s2 units [4 rows][kMaxLongUnits], f64 results [64], u32 lane list [64].
+constexpr int kLongS2Words = 4 * kMaxLongUnits * 2 / 8;  // u64 words of the s2 staging
+constexpr int kLongLdsWords = kLongS2Words + 64 + 32;
+static_assert(kLongLdsWords <= kPeqEntries, "long-value LDS must fit the Peq slice");
+
+template <int R, bool WL, typename CT>
+__device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint64_t* lds, const CT* s1p,
+                                        int n1, uint32_t g, uint32_t crow, int lc, int nneed) {
+  using T = typename std::conditional<WL, double, int>::type;
+  constexpr int UPW = 4 / (int)sizeof(CT);
+  uint16_t* s2buf = reinterpret_cast<uint16_t*>(lds);
+  double* res = reinterpret_cast<double*>(lds + kLongS2Words);
+  const uint32_t* list = reinterpret_cast<const uint32_t*>(lds + kLongS2Words + 64);
+  const int lane = (int)lane_id();
+  const int grp = lane >> 4, k = lane & 15;
+  const int kstar = (n1 - 1) / R, rstar = n1 - kstar * R;
+  uint16_t* row_s2 = s2buf + grp * kMaxLongUnits;
+  // this lane's query rows
+  uint32_t c1[R];
+  double w1[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = k * R + r;
+    c1[r] = i < n1 ? (uint32_t)s1p[i] : 0xFFFFFFFFu;  // rows past n1 never match
+    w1[r] = WL ? wl_weight(c1[r]) : 0.0;
+  }
+  const CT* base = reinterpret_cast<const CT*>(D.units);
+  for (int r0 = 0; r0 < nneed; r0 += 4) {
+    const int idx = r0 + grp;
+    const bool has = idx < nneed;
+    const int src = has ? (int)list[idx] : 0;
+    // cross-lane reads with every lane active (a lane of a row without a pair may still
+    // be the source another row reads from)
+    const uint32_t gg = (uint32_t)__shfl((int)g, src);
+    const uint32_t cr = (uint32_t)__shfl((int)crow, src);
+    const int lsrc = __shfl(lc, src);
+    const int n2 = has ? lsrc : 0;
+    // stage the row's candidate value in LDS as u16 units
+    const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + gg, rstride}
+                               : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[cr]), 1};
+    wave_lds_sync();  // previous round's reads of s2buf are done
+    const int nw = (n2 + UPW - 1) / UPW;
+    for (int w = k; w < nw; w += kLongRowLanes) {
+      const uint32_t x = s2.word(w);
+#pragma unroll
+      for (int u = 0; u < UPW; ++u) row_s2[w * UPW + u] = (uint16_t)Str<CT>::unit(x, u);
+    }
+    wave_lds_sync();
+    int tmax = n2 > 0 ? n2 + kstar : 0;
+    for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o));
+    T col[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) col[r] = (T)(k * R + r + 1);  // D(i, 0) = i
+    T prev = (T)(k * R);                                      // D(k*R, j-1)
+    T bot = col[R - 1];
+    uint32_t ch_next = row_s2[0];
+    for (int t = 0; t < tmax; ++t) {
+      const int j = t - k + 1;
+      const uint32_t ch2 = ch_next;
+      ch_next = row_s2[min(max(j, 0), kMaxLongUnits - 1)];  // column j+1's unit, one step ahead
+      // lane 0's row above: the matrix's top boundary D(0, j)
+      T top;
+      if (WL) top = n1 == 1 ? col[0] : (T)(j == 1 ? n1 : j);
+      else top = (T)j;
+      const T recv = dpp_row_shr1(top, bot);  // D(k*R, j)
+      if (j >= 1 && j <= n2) {
+        T up = recv, dg = prev;
+        if (WL) {
+          const double w2 = wl_weight(ch2);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const double old = col[r];
+            const double cost = c1[r] == ch2 ? 0.0 : fmax(w1[r], w2);
+            // Math.min(left, Math.min(above, aboveleft)) on non-negative values
+            const double v = fmin((double)up + w1[r], fmin(old + w2, (double)dg + cost));
+            col[r] = (T)v;
+            dg = (T)old;
+            up = (T)v;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int old = (int)col[r];
+            const int v = imin3((int)up, (int)dg, old) + (c1[r] == ch2 ? 0 : 1);
+            col[r] = (T)v;
+            dg = (T)old;
+            up = (T)v;
+          }
+        }
+        prev = recv;
+        bot = col[R - 1];
+      }
+    }
+    if (has && k == kstar) {
+      T v = col[0];
+#pragma unroll
+      for (int r = 1; r < R; ++r) v = r + 1 == rstar ? col[r] : v;
+      double sim;
+      if (WL) {
+        // [Duke 1.2] WeightedLevenshtein.compare
+        const double maxlen = (double)max(n1, n2);
+        const double dist = (double)v;
+        sim = dist > maxlen ? 0.0 : 1.0 - (dist / maxlen);
+      } else {
+        // [Duke 1.2] Levenshtein.compare: 1 - min(dist, len) / len
+        const int len = min(n1, n2);
+        sim = 1.0 - ((double)min((int)v, len) / (double)len);
+      }
+      res[src] = sim;
+    }
+  }
+}
+
+// Similarity of every lane with `need` set (the others keep `sim`) through long_dp.
+// Wave-uniform call: all 64 lanes enter.
+template <int LR, bool WL, typename CT>
+__device__ __forceinline__ double long_sims(const DevProp& D, uint64_t rstride, uint64_t* lds, uint32_t q,
+                                            int n1, uint32_t g, uint32_t crow, int lc, bool need,
+                                            double sim) {
+  const uint64_t nm = __ballot(need);
+  if (nm == 0) return sim;
+  const int nneed = __popcll(nm);
+  uint32_t* list = reinterpret_cast<uint32_t*>(lds + kLongS2Words + 64);
+  double* res = reinterpret_cast<double*>(lds + kLongS2Words);
+  if (need) list[mask_rank(nm)] = lane_id();
+  wave_lds_sync();
+  const CT* s1p = reinterpret_cast<const CT*>(D.units) + D.off[q];
+  // rows per lane: n1 is wave-uniform, so this is a scalar switch
+  if (n1 <= 16) long_dp<1, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 32) long_dp<2, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 64 || LR <= 4) long_dp<4, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 128 || LR <= 8) long_dp<(LR < 8 ? 4 : 8), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else long_dp<(LR < 16 ? 4 : 16), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  wave_lds_sync();
+  if (need) sim = res[lane_id()];
+  wave_lds_sync();
+  for (int e = (int)lane_id(); e < kLongLdsWords; e += 64) lds[e] = 0;  // Peq slice stays zero
+  wave_lds_sync();
+  return sim;
+}
+
 // [Duke 1.2] comparators.JaroWinkler.similarity — per-lane form for values over 64 units
 template <typename CT>
 __device__ __forceinline__ double jarowinkler(Str<CT> s1, int n1, Str<CT> s2, int n2) {
@@ -373,6 +564,21 @@ __device__ __forceinline__ double qgram_formula(int common, int m1, int m2, int 
   return (double)common / fmin((double)m1, (double)m2);
 }
 
+// [Duke 1.2, recalled] DiceCoefficientComparator / JaccardIndexComparator with the
+// ExactComparator sub-comparator: the tokens of the shorter list (s1 on a tie) that occur
+// in the other, counted with multiplicity (sorted token ids, duplicates kept)
+__device__ __forceinline__ int count_members(const uint64_t* __restrict__ g1, int m1,
+                                             const uint64_t* __restrict__ g2, int m2) {
+  int i = 0, j = 0, hit = 0;
+  while (i < m1 && j < m2) {
+    const uint64_t x = g1[i], y = g2[j];
+    hit += (x == y);
+    i += (x <= y);
+    j += (y < x);
+  }
+  return hit;
+}
+
 __device__ __forceinline__ int intersect_sorted(const uint64_t* __restrict__ g1, int m1,
                                                 const uint64_t* __restrict__ g2, int m2) {
   int i = 0, j = 0, common = 0;
@@ -398,7 +604,7 @@ __device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool o
 // ------------------------------------------------------------------------------------
 // The fused scoring kernel.  One lane per slot, one query per wave.
 // ------------------------------------------------------------------------------------
-template <int RMAX, typename CT>
+template <int RMAX, int LR, typename CT>
 __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
                                              int lc, bool cmp) {
@@ -408,7 +614,26 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
                              : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[crow]), 1};
   double sim = 0.0;
   switch (D.op) {
+    case DK_CMP_WEIGHTED_LEVENSHTEIN:
+      if (LR > 0) {  // the host only schedules WeightedLevenshtein on LR > 0 variants
+        const bool same = cmp && str_equal(s1, lq, s2, lc);
+        sim = same ? 1.0 : 0.0;
+        sim = long_sims<LR, true, CT>(D, rstride, peq, q, lq, g, crow, lc, cmp && !same, sim);
+      }
+      break;
     case DK_CMP_LEVENSHTEIN:
+      if (LR > 0 && lq > kMaxUnits) {  // query over 64 units: long-value DP
+        bool need = false;
+        if (cmp) {
+          const int len = min(lq, lc), maxlen = max(lq, lc);
+          if (2 * len <= maxlen) sim = 0.0;
+          else if (len == maxlen && str_equal(s1, lq, s2, lc)) sim = 1.0;
+          else need = true;
+        }
+        sim = long_sims<LR, false, CT>(D, rstride, peq, q, lq, g, crow, lc, need, sim);
+        break;
+      }
+      [[fallthrough]];
     case DK_CMP_JAROWINKLER: {
       const bool table = lq <= 64 && (D.op == DK_CMP_LEVENSHTEIN || __ballot(cmp && lc > 64) == 0);
       if (table) {
@@ -436,13 +661,33 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
         }
       }
       break;
+    case DK_CMP_DICE_TOKENS:
+    case DK_CMP_JACCARD_TOKENS:
+      if (cmp) {
+        if (str_equal(s1, lq, s2, lc)) {
+          sim = 1.0;
+        } else {
+          int m1 = D.gcnt[q], m2 = D.rgcnt[g];
+          const uint64_t* t1 = D.grams + D.goff[q];
+          const uint64_t* t2 = D.grams + D.rgoff[g];
+          if (m1 > m2) {
+            const uint64_t* tt = t1; t1 = t2; t2 = tt;
+            const int tm = m1; m1 = m2; m2 = tm;
+          }
+          const int hit = count_members(t1, m1, t2, m2);
+          // exact small integers in doubles: sum = hit, union = m1 + m2 - hit
+          sim = D.op == DK_CMP_JACCARD_TOKENS ? (double)hit / (double)(m1 + m2 - hit)
+                                              : ((double)hit * 2) / (double)(m1 + m2);
+        }
+      }
+      break;
     default:
       break;
   }
   return sim;
 }
 
-template <int RMAX>
+template <int RMAX, int LR>
 __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSource S,
                                                uint64_t slot0, uint64_t nslots, StageOut out) {
   __shared__ uint64_t peq_all[kScoreBlock / 64][kPeqEntries];
@@ -488,11 +733,11 @@ __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSo
       if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
       if (cmp) bytes += 16;
     } else if (D.op != DK_CMP_NONE) {
-      sim = D.width == 1 ? string_sim<RMAX, uint8_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp)
-                         : string_sim<RMAX, uint16_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp);
+      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp)
+                         : string_sim<RMAX, LR, uint16_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp);
       if (cmp) {
         bytes += 8u + (uint32_t)(lq + lc) * (uint32_t)D.width;
-        if (D.op == DK_CMP_QGRAM) bytes += 8u + 8u * (uint32_t)(D.gcnt[q] + D.rgcnt[g]);
+        if (uses_codes(D.op)) bytes += 8u + 8u * (uint32_t)(D.gcnt[q] + D.rgcnt[g]);
       }
     }
     if (present) {
@@ -879,12 +1124,21 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
                         uint64_t nslots, const StageOut& out, hipStream_t s) {
   DK_LAUNCH_GUARD(nslots);
   const unsigned grid = grid1d(nslots, kScoreBlock);
-  // kernel variant by the longest Levenshtein query value (rows of the DP column)
-  if (P.lev_rows <= 16) k_score<16><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
-  else if (P.lev_rows <= 32) k_score<32><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
-  else if (P.lev_rows <= 40) k_score<40><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
-  else if (P.lev_rows <= 48) k_score<48><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
-  else k_score<64><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  // kernel variant by the longest Levenshtein query value (rows of the lane-per-pair DP
+  // column) and the longest value of the long-value DP (WeightedLevenshtein, or a
+  // Levenshtein value over 64 units): both bound the VGPRs of the fused kernel
+#define DK_SCORE(RM, L) k_score<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
+  if (P.long_rows > 0) {
+    const bool lev64 = P.lev_rows > 16;
+    if (P.long_rows <= 64) { if (lev64) DK_SCORE(64, 4); else DK_SCORE(16, 4); }
+    else if (P.long_rows <= 128) { if (lev64) DK_SCORE(64, 8); else DK_SCORE(16, 8); }
+    else { if (lev64) DK_SCORE(64, 16); else DK_SCORE(16, 16); }
+  } else if (P.lev_rows <= 16) DK_SCORE(16, 0);
+  else if (P.lev_rows <= 32) DK_SCORE(32, 0);
+  else if (P.lev_rows <= 40) DK_SCORE(40, 0);
+  else if (P.lev_rows <= 48) DK_SCORE(48, 0);
+  else DK_SCORE(64, 0);
+#undef DK_SCORE
   return hipGetLastError();
 }
 

@@ -21,9 +21,13 @@ COMPARATOR_CLASSES = {
     DUKE_CMP + "QGramComparator": A.CMP_QGRAM,
     DUKE_CMP + "ExactComparator": A.CMP_EXACT,
     DUKE_CMP + "NumericComparator": A.CMP_NUMERIC,
+    DUKE_CMP + "WeightedLevenshtein": A.CMP_WEIGHTED_LEVENSHTEIN,
+    DUKE_CMP + "DiceCoefficientComparator": A.CMP_DICE_TOKENS,
+    DUKE_CMP + "JaccardIndexComparator": A.CMP_JACCARD_TOKENS,
 }
+EXACT_CLASS = DUKE_CMP + "ExactComparator"
 FORMULAS = {"OVERLAP": A.QGRAM_OVERLAP, "JACCARD": A.QGRAM_JACCARD, "DICE": A.QGRAM_DICE}
-TOKENIZERS = {"BASIC": A.QGRAM_BASIC, "POSITIONAL": A.QGRAM_POSITIONAL}
+TOKENIZERS = {"BASIC": A.QGRAM_BASIC, "POSITIONAL": A.QGRAM_POSITIONAL, "ENDS": A.QGRAM_ENDS}
 
 ID_PROPERTY = "ID"
 GROUP_NO_PROPERTY_NAME = "dukeGroupNo"               # IncrementalLuceneDatabase.java:449
@@ -57,6 +61,11 @@ class Comparator:
                 p.qgram_formula = FORMULAS[value.strip().upper()]
             elif op == A.CMP_QGRAM and key == "tokenizer":
                 p.qgram_tokenizer = TOKENIZERS[value.strip().upper()]
+            elif op in (A.CMP_DICE_TOKENS, A.CMP_JACCARD_TOKENS) and key == "comparator":
+                # the token sub-comparator: only the default ExactComparator has a kernel
+                sub = value.klass if isinstance(value, Comparator) else str(value).strip()
+                if sub != EXACT_CLASS:
+                    raise UnsupportedComparator(f"{self.klass}: sub-comparator {sub} has no GPU kernel")
             else:
                 raise UnsupportedComparator(f"{self.klass}: parameter {name!r}")
         return p
@@ -178,6 +187,12 @@ def parse_duke_config(xml, linkage=None) -> DukeConfig:
     for ob in root.findall("object"):
         objects[ob.get("name")] = Comparator(
             ob.get("class"), {pa.get("name"): pa.get("value") for pa in ob.findall("param")})
+    # ConfigLoader resolves a <param> value that names another <object> to that object
+    # (e.g. the sub-comparator of DiceCoefficientComparator / JaccardIndexComparator)
+    for ob in objects.values():
+        for k, v in list(ob.params.items()):
+            if isinstance(v, str) and v in objects:
+                ob.params[k] = objects[v]
     schema = root.find("schema")
     threshold = float(_text(schema, "threshold"))
     maybe = float(_text(schema, "maybe-threshold", "0.0"))

@@ -31,9 +31,12 @@ def string_cases(seed, n):
     fixed = [("", ""), ("a", "b"), ("a", "a"), ("ab", "ba"), ("aab", "ab"), ("kitten", "sitting"),
              ("MARTHA", "MARHTA"), ("DWAYNE", "DUANE"), ("DIXON", "DICKSONX"), ("abc", ""),
              ("Norway", "Norwegian"), ("Oslo", "Olso"), ("ł\U0001F600a", "ła\U0001F600"),
-             ("x" * 64, "x" * 63 + "y"), ("abcdefgh", "badcfehg")]
+             ("x" * 64, "x" * 63 + "y"), ("abcdefgh", "badcfehg"), ("a", "ab"), ("ab", "a"),
+             ("a b c", "b c d e"), (" a  b ", "b a"), (" ", "  "), ("a a b", "a b"),
+             ("12 main st.", "12 main street"), ("o'neil-smith", "oneil smith"), ("a\\b", "a/b"),
+             ('"q"', "q")]
     out = list(fixed)
-    alphas = ["ab", "abcd", "abcdefghijklmnopqrstuvwxyz", "ałé\U0001F600"]
+    alphas = ["ab", "abcd", "abcdefghijklmnopqrstuvwxyz", "ałé\U0001F600", "ab 1.-", "a b  "]
     for i in range(n):
         a = alphas[i % len(alphas)]
         out.append((rnd_str(rng, a, 0, 14), rnd_str(rng, a, 0, 14)))
@@ -55,7 +58,32 @@ def main():
                 for form in (0, 1, 2):
                     rec[f"qgram_q{q}_f{form}"] = fl(R.qgram(u1, u2, q, form))
             rec["qgram_q2_f1_positional"] = fl(R.qgram(u1, u2, 2, 1, R.POSITIONAL))
+            rec["qgram_q2_f1_ends"] = fl(R.qgram(u1, u2, 2, 1, R.ENDS))
+            rec["qgram_q3_f2_ends"] = fl(R.qgram(u1, u2, 3, 2, R.ENDS))
+            rec["weighted_levenshtein"] = fl(R.weighted_levenshtein(u1, u2))
+            rec["dice_tokens"] = fl(R.token_set_similarity(u1, u2, False))
+            rec["jaccard_tokens"] = fl(R.token_set_similarity(u1, u2, True))
             f.write(json.dumps(rec) + "\n")
+    # long values for the long-value DP (WeightedLevenshtein, Levenshtein over 64 units)
+    rng = random.Random(5)
+    words = ["oslo", "bergen", "street", "42", "no.", "gate", "vei", "a/s", "-", "o'neil", "x"]
+    with open(os.path.join(OUT, "long_values.jsonl"), "w") as f:
+        for i in range(60):
+            a = " ".join(rng.choice(words) for _ in range(rng.randint(1, 50)))[:256]
+            b = list(a)
+            for _ in range(rng.randint(0, 12)):
+                if b and rng.random() < 0.5:
+                    del b[rng.randrange(len(b))]
+                else:
+                    b.insert(rng.randrange(len(b) + 1), rng.choice("abc 1.-"))
+            b = "".join(b)[:256] or "z"
+            if i % 7 == 0:
+                b = a[: max(1, len(a) // 2)]
+            u1, u2 = R.units(a), R.units(b)
+            f.write(json.dumps({"s1": list(u1), "s2": list(u2),
+                                "compact_distance": R.compact_distance(u1, u2),
+                                "levenshtein": fl(R.levenshtein(u1, u2)),
+                                "weighted_levenshtein": fl(R.weighted_levenshtein(u1, u2))}) + "\n")
     nums = ["1", "2", "0", "-0", "0.0", "-3", "-4.5", "1e3", "1000", "abc", " 7 ", "7f", "NaN",
             "Infinity", "-Infinity", "0x1p3", "0x.8p1", "8", "1e", "", "1.", ".5", "0.5d",
             "3.3", "3.30", "+2", "1.e5", "1_0", "inf", "0x1", "1e-400", "1e400", "\t5\n"]

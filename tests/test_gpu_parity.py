@@ -17,6 +17,7 @@ from dukehip import synth
 pytestmark = pytest.mark.gpu
 
 LEV, JW, QG, EX, NUM = A.CMP_LEVENSHTEIN, A.CMP_JAROWINKLER, A.CMP_QGRAM, A.CMP_EXACT, A.CMP_NUMERIC
+WL, DICE_T, JACC_T = A.CMP_WEIGHTED_LEVENSHTEIN, A.CMP_DICE_TOKENS, A.CMP_JACCARD_TOKENS
 MODES = {"dedup": A.MODE_DEDUP, "linkage": A.MODE_LINKAGE, "allpairs": A.MODE_ALLPAIRS}
 
 
@@ -249,8 +250,109 @@ def test_processor_replay_order():
     db.close()
 
 
-def test_unsupported_levenshtein_length():
-    eng = dh.GpuEngine(schema_of([{"comparator": LEV, "low": 0.1, "high": 0.9}], 0.9, 0.0, "dedup", 1))
+def mutate(rng, s, k, alpha):
+    b = list(s)
+    for _ in range(k):
+        r = rng.random()
+        if b and r < 0.35:
+            del b[rng.randrange(len(b))]
+        elif b and r < 0.7:
+            b[rng.randrange(len(b))] = rng.choice(alpha)
+        else:
+            b.insert(rng.randrange(len(b) + 1), rng.choice(alpha))
+    return "".join(b)
+
+
+def families(rng, nbase, per, alpha, lo, hi, edits, cap):
+    """Base strings plus edited copies, so that many pairs are similar enough to reach
+    the DP (and the >= 0.5 similarity branch of PropertyImpl)."""
+    out = []
+    for _ in range(nbase):
+        base = "".join(rng.choice(alpha) for _ in range(rng.randint(lo, hi)))
+        out.append(base[:cap])
+        for _ in range(per):
+            out.append((mutate(rng, base, rng.randint(0, edits), alpha) or "z")[:cap])
+    return out
+
+
+WL_ALPHA = "abcdef 01.-/'" + '"\\,'
+
+
+@pytest.mark.parametrize("lo,hi", [(1, 3), (1, 16), (10, 40), (30, 64), (60, 130), (120, 256)])
+def test_weighted_levenshtein_allpairs(lo, hi):
+    rng = random.Random(lo * 1000 + hi)
+    vals = families(rng, 20, 5, WL_ALPHA, lo, hi, max(2, hi // 8), 256)
+    res, ref = allpairs_single({"comparator": WL, "low": 0.1, "high": 0.9}, vals)
+    assert_same(res, ref)
+
+
+def test_weighted_levenshtein_quirks_and_utf16():
+    vals = ["a", "b", "ab", "ba", "a.", "1", "12", "x" * 256, "x" * 255 + "y", "é", "\U0001F600a",
+            "a\U0001F600", "o'neil-smith", "oneil smith", "a b", "ab ", " ", "\\", "/"]
+    res, ref = allpairs_single({"comparator": WL, "low": 0.0, "high": 1.0}, vals)
+    assert_same(res, ref)
+
+
+@pytest.mark.parametrize("lo,hi", [(60, 100), (65, 128), (120, 256)])
+def test_levenshtein_long_allpairs(lo, hi):
+    """Query values over 64 units take the long-value DP (no cutoff replay)."""
+    rng = random.Random(hi)
+    vals = families(rng, 16, 6, "abcd", lo, hi, hi // 6, 256)
+    res, ref = allpairs_single({"comparator": LEV, "low": 0.1, "high": 0.9}, vals)
+    assert_same(res, ref)
+
+
+def test_long_and_short_properties_fused():
+    """WeightedLevenshtein + long Levenshtein + JaroWinkler + QGram in one kernel, with
+    missing values, under blocking."""
+    rng = random.Random(77)
+    n = 600
+    text = families(rng, 60, 9, WL_ALPHA, 20, 200, 12, 256)[:n]
+    lev = families(rng, 60, 9, "abc", 50, 120, 10, 256)[:n]
+    name = families(rng, 60, 9, "abcdefg", 3, 12, 2, 64)[:n]
+    for col in (text, lev):
+        for i in range(0, n, 17):
+            col[i] = None
+    keys = [[("k%d" % (i % 40)) for i in range(n)]]
+    props = [{"comparator": WL, "low": 0.2, "high": 0.9},
+             {"comparator": LEV, "low": 0.1, "high": 0.8},
+             {"comparator": JW, "low": 0.3, "high": 0.7},
+             {"comparator": QG, "low": 0.4, "high": 0.6, "q": 3, "formula": 1}]
+    res, ref = run_both(props, [text, lev, name, text], keys, threshold=0.6, maybe=0.3)
+    assert res.n > 0
+    assert_same(res, ref)
+
+
+@pytest.mark.parametrize("cmp", [DICE_T, JACC_T])
+def test_token_comparators_allpairs(cmp):
+    rng = random.Random(cmp)
+    words = ["oslo", "bergen", "a", "b", "gate", "vei", "ø", "\U0001F600"]
+    vals = []
+    for _ in range(140):
+        k = rng.randint(0, 6)
+        sep = [" ", "  ", " "][rng.randint(0, 2)]
+        v = sep.join(rng.choice(words) for _ in range(k))
+        if rng.random() < 0.2:
+            v = " " + v + " "
+        vals.append(v if v else " ")
+    vals += ["a a b", "a b", "b a", " ", "  "]
+    res, ref = allpairs_single({"comparator": cmp, "low": 0.1, "high": 0.9}, vals)
+    assert_same(res, ref)
+
+
+@pytest.mark.parametrize("q,formula", [(1, 0), (2, 1), (3, 2), (4, 0)])
+def test_qgram_ends_allpairs(q, formula):
+    rng = random.Random(q * 7 + formula)
+    vals = [v for v in rand_strings(rng, 120, "ab^$", 1, 10) if v]
+    res, ref = allpairs_single({"comparator": QG, "low": 0.2, "high": 0.8, "q": q,
+                                "formula": formula, "tokenizer": A.QGRAM_ENDS}, vals)
+    assert_same(res, ref)
+
+
+@pytest.mark.parametrize("cmp", [LEV, WL])
+def test_unsupported_value_length(cmp):
+    eng = dh.GpuEngine(schema_of([{"comparator": cmp, "low": 0.1, "high": 0.9}], 0.9, 0.0, "dedup", 1))
+    eng.upsert(1, [0], [dh.Column.from_strings(["x" * 256])], key_columns=[dh.Column.from_strings(["k"])])
     with pytest.raises(dh.DukeHipError):
-        eng.upsert(1, [0], [dh.Column.from_strings(["x" * 65])], key_columns=[dh.Column.from_strings(["k"])])
+        eng.upsert(1, [1], [dh.Column.from_strings(["x" * 257])], key_columns=[dh.Column.from_strings(["k"])])
     eng.close()
