@@ -16,7 +16,10 @@ keys = [synth.column(k) for k in synth.keys_config2(p)]
 spec = {"NAME": (A.CMP_JAROWINKLER, 0.1, 0.95, "name"), "ADDRESS": (A.CMP_LEVENSHTEIN, 0.2, 0.8, "address"),
         "DOB": (A.CMP_LEVENSHTEIN, 0.1, 0.85, "dob")}
 cols = {k: synth.column(p[v[3]]) for k, v in spec.items()}
-for names in (["DOB", "ADDRESS", "NAME"], ["DOB"], ["ADDRESS"], ["NAME"], []):
+SETS = (["DOB", "ADDRESS", "NAME"], ["DOB"], ["ADDRESS"], ["NAME"], [])
+if os.environ.get("PROPS") is not None:   # e.g. PROPS=ADDRESS (one schema, for PMC passes)
+    SETS = ([x for x in os.environ["PROPS"].split(",") if x],)
+for names in SETS:
     arr = (A.dk_property * max(1, len(names)))()
     for i, k in enumerate(names):
         c, lo, hi, _ = spec[k]

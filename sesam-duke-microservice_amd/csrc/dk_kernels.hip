@@ -55,7 +55,11 @@ struct Str {
   static constexpr int UPW = 4 / (int)sizeof(CT);  // units per word
   const uint32_t* w;
   uint64_t wstride;
+  int kmax;  // last word that may be read speculatively (replica: its row count - 1)
   __device__ __forceinline__ uint32_t word(int k) const { return w[(uint64_t)k * wstride]; }
+  // a word read without a per-lane branch (the caller masks words past the value): the
+  // canonical arena keeps >= 512 zero bytes after the last value, the replica is clamped
+  __device__ __forceinline__ uint32_t word_any(int k) const { return w[(uint64_t)min(k, kmax) * wstride]; }
   static __device__ __forceinline__ uint32_t unit(uint32_t x, int u) {
     return sizeof(CT) == 1 ? (x >> (8 * u)) & 0xFFu : (x >> (16 * u)) & 0xFFFFu;
   }
@@ -332,8 +336,9 @@ __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint
     const int lsrc = __shfl(lc, src);
     const int n2 = has ? lsrc : 0;
     // stage the row's candidate value in LDS as u16 units
-    const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + gg, rstride}
-                               : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[cr]), 1};
+    const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + gg, rstride,
+                                         D.rlmax / Str<CT>::UPW - 1}
+                               : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[cr]), 1, 1 << 30};
     wave_lds_sync();  // previous round's reads of s2buf are done
     const int nw = (n2 + UPW - 1) / UPW;
     for (int w = k; w < nw; w += kLongRowLanes) {
@@ -609,9 +614,10 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
                                              int lc, bool cmp) {
   const CT* base = reinterpret_cast<const CT*>(D.units);
-  const Str<CT> s1{reinterpret_cast<const uint32_t*>(base + D.off[q]), 1};
-  const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + g, rstride}
-                             : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[crow]), 1};
+  const Str<CT> s1{reinterpret_cast<const uint32_t*>(base + D.off[q]), 1, 1 << 30};
+  const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + g, rstride,
+                                       D.rlmax / Str<CT>::UPW - 1}
+                             : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[crow]), 1, 1 << 30};
   double sim = 0.0;
   switch (D.op) {
     case DK_CMP_WEIGHTED_LEVENSHTEIN:
@@ -688,8 +694,8 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
 }
 
 template <int RMAX, int LR>
-__global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSource S,
-                                               uint64_t slot0, uint64_t nslots, StageOut out) {
+__device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
+                                           uint64_t nslots, const StageOut& out) {
   __shared__ uint64_t peq_all[kScoreBlock / 64][kPeqEntries];
   __shared__ uint32_t wcount[kScoreBlock / 64], wscored[kScoreBlock / 64], wbytes[kScoreBlock / 64];
   const uint32_t wave = threadIdx.x >> 6;
@@ -795,6 +801,21 @@ __global__ __launch_bounds__(256) void k_score(const ScoreParams P, const PairSo
     out.bscored[blockIdx.x] = ns;
     out.bbytes[blockIdx.x] = nb;
   }
+}
+
+// The fused scoring kernel.  Short-value variants pin the occupancy (the DP is
+// latency-bound: 5 waves/SIMD up to 40 rows, 4 above); the long-value variants (LR > 0)
+// carry the systolic DP's f64 rows and take what the register allocator needs.
+template <int RMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? 5 : 4, 8)))
+void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
+  score_body<RMAX, 0>(P, S, slot0, nslots, out);
+}
+
+template <int RMAX, int LR>
+__global__ __launch_bounds__(256) void k_score_long(const ScoreParams P, const PairSource S,
+                                                    uint64_t slot0, uint64_t nslots, StageOut out) {
+  score_body<RMAX, LR>(P, S, slot0, nslots, out);
 }
 
 // Sum the per-block counters of a chunk into counters[0..1]: one atomic pair per block
@@ -1127,18 +1148,20 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
   // kernel variant by the longest Levenshtein query value (rows of the lane-per-pair DP
   // column) and the longest value of the long-value DP (WeightedLevenshtein, or a
   // Levenshtein value over 64 units): both bound the VGPRs of the fused kernel
-#define DK_SCORE(RM, L) k_score<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
+#define DK_SHORT(RM) k_score<RM><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
+#define DK_LONG(RM, L) k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
   if (P.long_rows > 0) {
     const bool lev64 = P.lev_rows > 16;
-    if (P.long_rows <= 64) { if (lev64) DK_SCORE(64, 4); else DK_SCORE(16, 4); }
-    else if (P.long_rows <= 128) { if (lev64) DK_SCORE(64, 8); else DK_SCORE(16, 8); }
-    else { if (lev64) DK_SCORE(64, 16); else DK_SCORE(16, 16); }
-  } else if (P.lev_rows <= 16) DK_SCORE(16, 0);
-  else if (P.lev_rows <= 32) DK_SCORE(32, 0);
-  else if (P.lev_rows <= 40) DK_SCORE(40, 0);
-  else if (P.lev_rows <= 48) DK_SCORE(48, 0);
-  else DK_SCORE(64, 0);
-#undef DK_SCORE
+    if (P.long_rows <= 64) { if (lev64) DK_LONG(64, 4); else DK_LONG(16, 4); }
+    else if (P.long_rows <= 128) { if (lev64) DK_LONG(64, 8); else DK_LONG(16, 8); }
+    else { if (lev64) DK_LONG(64, 16); else DK_LONG(16, 16); }
+  } else if (P.lev_rows <= 16) DK_SHORT(16);
+  else if (P.lev_rows <= 32) DK_SHORT(32);
+  else if (P.lev_rows <= 40) DK_SHORT(40);
+  else if (P.lev_rows <= 48) DK_SHORT(48);
+  else DK_SHORT(64);
+#undef DK_SHORT
+#undef DK_LONG
   return hipGetLastError();
 }
 
