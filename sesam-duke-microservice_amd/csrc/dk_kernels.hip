@@ -66,6 +66,23 @@ struct Str {
   __device__ __forceinline__ uint32_t operator[](int j) const { return unit(word(j / UPW), j % UPW); }
 };
 
+// Length of the common prefix of a and b, at most `last` (<= 4 and <= both lengths), from
+// their first words by XOR and trailing-zero count (units past a value read as 0 in both
+// layouts, and `last` cuts at the shorter value) — no per-unit loop of dependent loads.
+template <typename CT>
+__device__ __forceinline__ int common_prefix4(const Str<CT>& a, const Str<CT>& b, int last) {
+  constexpr int UB = 8 * (int)sizeof(CT);
+  int p;
+  const uint32_t x0 = a.word(0) ^ b.word(0);
+  if (sizeof(CT) == 1) {
+    p = x0 ? (int)(__builtin_ctz(x0) / UB) : 4;
+  } else {
+    const uint32_t x1 = a.word_any(1) ^ b.word_any(1);
+    p = x0 ? (int)(__builtin_ctz(x0) / UB) : (x1 ? 2 + (int)(__builtin_ctz(x1) / UB) : 4);
+  }
+  return min(p, last);
+}
+
 template <typename CT>
 __device__ __forceinline__ bool str_equal(const Str<CT>& a, int na, const Str<CT>& b, int nb) {
   if (na != nb) return false;
@@ -195,14 +212,17 @@ __device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1,
   // one word of s2 prefetched ahead (UPW columns of latency cover), and the Peq read of
   // column j+1 issued before column j's DP so it lands while the column computes;
   // (j + 1) % UPW is wave-uniform, so the word rotation is a scalar branch
-  uint32_t wn = L.live && UPW < n2 ? s2.word(1) : 0u;
+  // Words past the value are read speculatively (word_any) and only ever feed columns no
+  // live lane computes: a load under a per-lane condition would be waited for at once
+  // (hipcc branches around it and waits vmcnt(0) at the join).
+  uint32_t wn = s2.word_any(1);
   uint64_t ne_next = ~peq_eq<CT>(peq, UPW > 1 ? Str<CT>::unit(w, 1) : wn);
   for (int j = 1; L.live; ++j) {
     const uint64_t ne = ne_next;
     const int jn = j + 1;
     if (jn % UPW == 0) {
       w = wn;
-      wn = (jn + UPW) < n2 ? s2.word(jn / UPW + 1) : 0u;
+      wn = s2.word_any(jn / UPW + 1);
     }
     ne_next = ~peq_eq<CT>(peq, Str<CT>::unit(w, jn % UPW));
     L.step(ne, j);
@@ -464,9 +484,7 @@ __device__ __forceinline__ double jarowinkler(Str<CT> s1, int n1, Str<CT> s2, in
   }
   if (c == 0) return 0.0;
   double score = ((c / (double)n1) + (c / (double)n2) + ((c - t) / (double)c)) / 3.0;
-  int p = 0;
-  const int last = min(4, n1);
-  while (p < last && s1[p] == s2[p]) ++p;
+  const int p = common_prefix4(s1, s2, min(4, n1));
   score += ((p * (1 - score)) / 10);
   return score;
 }
@@ -516,7 +534,7 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
     for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
     constexpr int UPW = Str<CT>::UPW;
     for (int k = 0; k * UPW < wmax; ++k) {
-      const uint32_t w = k * UPW < maxn ? cs.word(k) : 0u;
+      const uint32_t w = cs.word_any(k);  // units past maxn are never used (j < maxn)
 #pragma unroll
       for (int u = 0; u < UPW; ++u) {
         const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
@@ -555,9 +573,7 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
   const Str<CT>& s2 = rows_cand ? qs : cs;
   const int n1 = rows_cand ? nc : nq, n2 = rows_cand ? nq : nc;
   double score = ((c / (double)n1) + (c / (double)n2) + ((c - t) / (double)c)) / 3.0;
-  int p = 0;
-  const int last = min(4, n1);
-  while (p < last && s1[p] == s2[p]) ++p;
+  const int p = common_prefix4(s1, s2, min(4, n1));
   score += ((p * (1 - score)) / 10);
   return score;
 }

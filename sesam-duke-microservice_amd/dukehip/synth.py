@@ -122,6 +122,100 @@ def persons(n_orig, n_dup, seed=SEED, utf16_frac=0.0, shuffle=True):
     return out
 
 
+def linkage_persons(n_group1, dup_frac=0.3, seed=SEED + 2):
+    """BASELINE config 3: group 1 = n_group1 persons; group 2 = n_group1 persons of which
+    dup_frac are perturbed copies of group-1 records, the rest new.  Adds BIRTHYEAR
+    (dob[0:4]) and ZIP (4 digits fixed per city) for the Numeric comparators.  Returns
+    the persons dict (group-1 rows first) and the group array (1 / 2)."""
+    n_dup = int(n_group1 * dup_frac)
+    n_new = n_group1 - n_dup
+    p = persons(n_group1 + n_new, 0, seed=seed, shuffle=False)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    src = rng.integers(0, n_group1, n_dup)
+    fields = ("given", "surname", "address", "dob")
+    out = {k: list(p[k][:n_group1]) for k in fields}
+    extra = {k: list(p[k][n_group1:]) for k in fields}
+    dup = {k: [] for k in fields}
+    for j in range(n_dup):
+        i = int(src[j])
+        g, su, a, d = out["given"][i], out["surname"][i], out["address"][i], out["dob"][i]
+        if rng.random() < 0.3:
+            g = _corrupt(rng, g)
+        if rng.random() < 0.3:
+            su = _corrupt(rng, su)
+        if rng.random() < 0.3:
+            a = _corrupt(rng, a)
+        if rng.random() < 0.1:
+            d = f"{d[:4]}-{d[8:10]}-{d[5:7]}"
+        for k, v in zip(fields, (g, su, a, d)):
+            dup[k].append(v)
+    for k in fields:
+        out[k] = out[k] + dup[k] + extra[k]
+    n = len(out["given"])
+    out["name"] = [f"{g} {s}" for g, s in zip(out["given"], out["surname"])]
+    out["birthyear"] = [d[:4] for d in out["dob"]]
+    out["zip"] = [str(1000 + hash_str(a.rsplit(" ", 1)[-1]) % 9000) for a in out["address"]]
+    group = np.concatenate([np.ones(n_group1, np.uint8), np.full(n - n_group1, 2, np.uint8)])
+    return out, group
+
+
+def hash_str(s):
+    """Deterministic string hash (FNV-1a 32), stable across processes."""
+    h = 0x811C9DC5
+    for ch in s.encode("utf-8"):
+        h = ((h ^ ch) * 0x01000193) & 0xFFFFFFFF
+    return h
+
+
+def short_strings(n, lo=4, hi=16, seed=SEED + 3):
+    """BASELINE config 4: n strings over a-z with lengths U[lo, hi]."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lens = rng.integers(lo, hi + 1, n)
+    chars = rng.integers(ord("a"), ord("z") + 1, int(lens.sum()), dtype=np.uint8).tobytes()
+    out, o = [], 0
+    for L in lens:
+        out.append(chars[o:o + int(L)].decode("latin-1"))
+        o += int(L)
+    return out
+
+
+def long_texts(n_group1, dup_frac=0.3, lo=64, hi=256, vocab=50000, seed=SEED + 4):
+    """BASELINE config 5: TEXT values of lo..hi characters (lognormal length, clipped) from
+    a `vocab`-word list (Zipf s=1.05); group 2 holds dup_frac copies of group-1 texts with
+    1-8 character edits, and new texts for the rest.  Returns (texts, group)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    words = _vocab(rng, vocab, 1, 4, cap=False)
+    n_dup = int(n_group1 * dup_frac)
+    total = 2 * n_group1 - n_dup
+    target = np.clip(rng.lognormal(np.log(120.0), 0.35, total), lo, hi).astype(np.int64)
+    w = _zipf_choice(rng, len(words), 1.05, int(target.sum() // 3 + 64 * total))
+    texts, k = [], 0
+    for t in target:
+        parts, L = [], -1
+        while L < t:
+            wd = words[int(w[k])]
+            k += 1
+            parts.append(wd)
+            L += len(wd) + 1
+        texts.append(" ".join(parts)[:hi])
+    g1 = texts[:n_group1]
+    src = rng.integers(0, n_group1, n_dup)
+    dups = []
+    for j in range(n_dup):
+        s = g1[int(src[j])]
+        for _ in range(int(rng.integers(1, 9))):
+            s = _corrupt(rng, s)
+        dups.append(s[:hi])
+    out = g1 + dups + texts[n_group1:]
+    group = np.concatenate([np.ones(n_group1, np.uint8), np.full(len(out) - n_group1, 2, np.uint8)])
+    return out, group
+
+
+def keys_first_two_tokens(texts):
+    """BASELINE config 5 key: the first two tokens."""
+    return [[" ".join(t.split(" ")[:2]) for t in texts]]
+
+
 def keys_config2(p):
     """K1 = surname[0:3] + dob[0:4]; K2 = given[0:2] + dob[5:10]."""
     k1 = [s[:3] + d[:4] for s, d in zip(p["surname"], p["dob"])]
