@@ -1,11 +1,21 @@
-"""Benchmark: candidate pairs scored/sec on BASELINE.json configs[1] — 1M synthetic person
-records deduplicated with two key functions, NAME JaroWinkler + ADDRESS/DOB Levenshtein.
+"""Benchmark: candidate pairs scored/sec on BASELINE.json's configurations.
+
+Default (the driver's line): configs[1] — 1M synthetic person records deduplicated with two
+key functions, NAME JaroWinkler + ADDRESS/DOB Levenshtein.  `--workload` selects the other
+GPU configurations for measurement runs (not the headline line):
+  linkage   configs[2]: person linkage, QGram DICE/JACCARD names/addresses + Numeric
+            BIRTHYEAR/ZIP (min-ratio 0.9), cross-group key blocking (default 1M x 1M; the
+            published shape is 10M x 10M over 8 GPUs: --records 10000000)
+  allpairs  configs[3]: 200k x 200k unblocked (Duke InMemoryDatabase), one <=16-char a-z
+            field, --comparator lev|jw
+  longtext  configs[4]: text linkage, 64-256 chars, WeightedLevenshtein + QGram q=3
+            JACCARD, key = first two tokens (default 200k x 200k; published 5M x 5M)
 
 One step = one dk_match over every query record of this rank (blocking-table build,
-candidate generation, fused scoring, threshold, match gather to the host), with the index
-already resident in HBM.  N>1: one process per GPU (torchrun), replicated index, query
-records split into contiguous tiles per rank, match counts all-gathered and match lists
-gathered to rank 0 over RCCL inside the step.  Rank 0 prints one JSON line.
+candidate generation, fused scoring, threshold, match gather), with the index already
+resident in HBM.  N>1: one process per GPU (torchrun), replicated index, query records split
+into contiguous tiles per rank, match counts all-gathered and match lists gathered to rank 0
+over RCCL inside the step.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -23,6 +33,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "candidate pairs scored/sec (node) + records/sec deduped, 1/2/4/8 MI355X"
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
+DEFAULT_RECORDS = {"dedup": 1_000_000, "linkage": 1_000_000, "allpairs": 200_000, "longtext": 200_000}
 
 
 def parse():
@@ -30,37 +41,99 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--records", type=int, default=1_000_000)
+    ap.add_argument("--workload", default="dedup", choices=sorted(DEFAULT_RECORDS))
+    ap.add_argument("--records", type=int, default=None,
+                    help="dedup/allpairs: records; linkage/longtext: records per group")
+    ap.add_argument("--comparator", default="lev", choices=["lev", "jw"],
+                    help="allpairs: the field's comparator")
     ap.add_argument("--dup-frac", type=float, default=0.1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the oracle baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--only", default=None,
+                    help="diagnostic: comma-separated property names to keep (not a bench line)")
     return ap.parse_args()
 
 
-def build_data(n_records, dup_frac):
-    from dukehip import synth
-    n_dup = int(n_records * dup_frac)
-    p = synth.persons(n_records - n_dup, n_dup)
-    keys = synth.keys_config2(p)
-    return p, keys
+def prop(name, op, low, high, **kw):
+    return {"name": name, "comparator": op, "low": low, "high": high, **kw}
 
 
-def schema():
+def build_workload(args):
+    """The synthetic data, schema and queries of one BASELINE configuration."""
     from dukehip import _abi as A
-    # comparison order = record HashMap order of NAME/ADDRESS/DOB + synthetic properties
+    from dukehip import synth
+    n = args.records or DEFAULT_RECORDS[args.workload]
+    w = {"name": args.workload, "keys": [], "group": None, "threshold": 0.9, "maybe": 0.7}
+    if args.workload == "dedup":
+        n_dup = int(n * args.dup_frac)
+        p = synth.persons(n - n_dup, n_dup)
+        w.update(desc="BASELINE configs[1]: 1M synthetic person records dedup, key blocking "
+                      "K1=surname[0:3]+dob[0:4] K2=given[0:2]+dob[5:10]",
+                 props=[prop("NAME", A.CMP_JAROWINKLER, 0.1, 0.95),
+                        prop("ADDRESS", A.CMP_LEVENSHTEIN, 0.2, 0.8),
+                        prop("DOB", A.CMP_LEVENSHTEIN, 0.1, 0.85)],
+                 values={"NAME": p["name"], "ADDRESS": p["address"], "DOB": p["dob"]},
+                 keys=synth.keys_config2(p), mode=A.MODE_DEDUP, queries=np.arange(n))
+    elif args.workload == "linkage":
+        p, group = synth.linkage_persons(n)
+        w.update(desc=f"BASELINE configs[2]: person record linkage {n} x {len(group) - n}, QGram "
+                      "q=2 DICE/JACCARD + Numeric min-ratio 0.9, cross-group key blocking",
+                 props=[prop("NAME", A.CMP_QGRAM, 0.1, 0.95, q=2, formula=A.QGRAM_DICE),
+                        prop("ADDRESS", A.CMP_QGRAM, 0.2, 0.8, q=2, formula=A.QGRAM_JACCARD),
+                        prop("BIRTHYEAR", A.CMP_NUMERIC, 0.3, 0.7, min_ratio=0.9),
+                        prop("ZIP", A.CMP_NUMERIC, 0.4, 0.75, min_ratio=0.9)],
+                 values={"NAME": p["name"], "ADDRESS": p["address"], "BIRTHYEAR": p["birthyear"],
+                         "ZIP": p["zip"]},
+                 keys=synth.keys_config2(p), group=group, mode=A.MODE_LINKAGE,
+                 queries=np.arange(n, len(group)))
+    elif args.workload == "allpairs":
+        vals = synth.short_strings(n)
+        op = A.CMP_LEVENSHTEIN if args.comparator == "lev" else A.CMP_JAROWINKLER
+        w.update(desc=f"BASELINE configs[3]: {n} x {n} unblocked all-pairs (InMemoryDatabase), "
+                      f"one a-z field of 4-16 units, {args.comparator}",
+                 props=[prop("FIELD", op, 0.1, 0.95)], values={"FIELD": vals},
+                 mode=A.MODE_ALLPAIRS, queries=np.arange(n),
+                 threshold=0.85 if args.comparator == "lev" else 0.93, maybe=0.0)
+    else:  # longtext
+        texts, group = synth.long_texts(n)
+        w.update(desc=f"BASELINE configs[4]: text linkage {n} x {len(group) - n}, 64-256 units, "
+                      "WeightedLevenshtein + QGram q=3 JACCARD, key = first two tokens",
+                 props=[prop("TEXT", A.CMP_WEIGHTED_LEVENSHTEIN, 0.2, 0.9),
+                        prop("TEXTGRAMS", A.CMP_QGRAM, 0.3, 0.8, q=3, formula=A.QGRAM_JACCARD)],
+                 values={"TEXT": texts, "TEXTGRAMS": texts},
+                 keys=synth.keys_first_two_tokens(texts), group=group, mode=A.MODE_LINKAGE,
+                 queries=np.arange(n, len(group)))
+    w["n"] = len(next(iter(w["values"].values())))
+    w["queries"] = np.asarray(w["queries"], dtype=np.uint32)
+    # Processor.compare visits the record's HashMap order (data-source columns + ID and the
+    # ignored synthetic properties, App.java:309-323; dukeGroupNo in linkage)
     from dukehip.config import java_hashmap_order
-    order = [n for n in java_hashmap_order(["NAME", "ADDRESS", "DOB", "ID", "dukeOriginalEntityId",
-                                            "dukeDatasetId"]) if n in ("NAME", "ADDRESS", "DOB")]
-    spec = {"NAME": (A.CMP_JAROWINKLER, 0.1, 0.95), "ADDRESS": (A.CMP_LEVENSHTEIN, 0.2, 0.8),
-            "DOB": (A.CMP_LEVENSHTEIN, 0.1, 0.85)}
-    arr = (A.dk_property * 3)()
-    for i, name in enumerate(order):
-        c, lo, hi = spec[name]
-        arr[i] = A.dk_property(c, 2, 0, 0, lo, hi, 0.0)
-    s = A.dk_schema(3, arr, 0.9, 0.7, A.MODE_DEDUP, 2)
+    synth_props = ["ID", "dukeOriginalEntityId", "dukeDatasetId"]
+    if w["mode"] == A.MODE_LINKAGE:
+        synth_props.append("dukeGroupNo")
+    by = {p["name"]: p for p in w["props"]}
+    if args.only:
+        by = {k: v for k, v in by.items() if k in args.only.split(",")}
+    w["props"] = [by[k] for k in java_hashmap_order(list(by) + synth_props) if k in by]
+    return w
+
+
+def make_schema(w):
+    from dukehip import _abi as A
+    arr = (A.dk_property * len(w["props"]))()
+    for i, p in enumerate(w["props"]):
+        arr[i] = A.dk_property(p["comparator"], p.get("q", 2), p.get("formula", A.QGRAM_OVERLAP),
+                               p.get("tokenizer", A.QGRAM_BASIC), p["low"], p["high"],
+                               p.get("min_ratio", 0.0))
+    s = A.dk_schema(len(w["props"]), arr, w["threshold"], w["maybe"], w["mode"], len(w["keys"]))
     s._keep = arr
-    return s, order, spec
+    return s
+
+
+CMP_NAMES = {1: "Levenshtein", 2: "JaroWinkler", 3: "QGramComparator", 4: "ExactComparator",
+             5: "NumericComparator", 6: "WeightedLevenshtein", 7: "DiceCoefficientComparator",
+             8: "JaccardIndexComparator"}
 
 
 def main():
@@ -80,20 +153,18 @@ def main():
     from dukehip import synth
 
     t0 = time.time()
-    p, keys = build_data(args.records, args.dup_frac)
-    sch, order, spec = schema()
-    cols = [synth.column(p[{"NAME": "name", "ADDRESS": "address", "DOB": "dob"}[n]]) for n in order]
-    n = len(p["name"])
-    eng = dh.GpuEngine(sch, device=local)
-    eng.upsert(n, np.arange(n, dtype=np.uint64), cols,
-               key_columns=[synth.column(k) for k in keys])
+    w = build_workload(args)
+    n = w["n"]
+    eng = dh.GpuEngine(make_schema(w), device=local)
+    eng.upsert(n, np.arange(n, dtype=np.uint64), [synth.column(w["values"][p["name"]]) for p in w["props"]],
+               group=w["group"], key_columns=[synth.column(k) for k in w["keys"]] or None)
     t_index = time.time() - t0
     # contiguous query tile of this rank
-    q0, q1 = n * rank // world, n * (rank + 1) // world
-    queries = np.arange(q0, q1, dtype=np.uint32)
-
+    allq = w["queries"]
     from dukehip import dist as dshard
-    nq_max = dshard.max_tile(n, world)
+    q0, q1 = dshard.tile(len(allq), rank, world)
+    queries = allq[q0:q1]
+    nq_max = dshard.max_tile(len(allq), world)
     holder = {}
 
     def step():
@@ -151,7 +222,7 @@ def main():
         achieved = prof["score_bytes"] / score_s if score_s > 0 else 0.0
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_k_score.json")
-        if os.path.exists(pmc):
+        if w["name"] == "dedup" and os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         out = {
@@ -167,13 +238,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": "BASELINE configs[1]: 1M synthetic person records dedup, "
-                                   "key blocking K1=surname[0:3]+dob[0:4] K2=given[0:2]+dob[5:10]",
-                       "records": n, "pairs_per_step": pairs_step,
-                       "comparators": {k: ["Levenshtein", "JaroWinkler"][spec[k][0] == 2] for k in order},
-                       "threshold": 0.9, "maybe_threshold": 0.7,
+            "config": {"workload": w["desc"], "records": n, "queries": int(len(allq)),
+                       "pairs_per_step": pairs_step,
+                       "comparators": {p["name"]: CMP_NAMES[p["comparator"]] for p in w["props"]},
+                       "threshold": w["threshold"], "maybe_threshold": w["maybe"],
                        "parallelism": f"query-tile sharding x{world}, replicated index"},
-            "records_per_s": n / (ms_step / 1e3),
+            "records_per_s": len(allq) / (ms_step / 1e3),
             "matches_per_step": int(last.n) if last is not None else 0,
             "index_build_s": t_index,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
@@ -186,32 +256,34 @@ def main():
                                    ("ms_index", "ms_generate", "ms_score", "ms_gather", "ms_total")},
         }
         if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(p, keys, order, spec, last, args)
+            out["cpu_baseline"] = cpu_baseline(w, last, args)
         print(json.dumps(out), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
-def cpu_baseline(p, keys, order, spec, gpu_res, args):
+def cpu_baseline(w, gpu_res, args):
     """The C oracle (oracle/duke_oracle.c, a restatement of Duke's scoring loop) on a
     bounded sample: the first S query records, full candidate lists, host threads.  The
     same sample's match list is checked against the GPU's."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    field = {"NAME": "name", "ADDRESS": "address", "DOB": "dob"}
-    props = [{"comparator": spec[k][0], "low": spec[k][1], "high": spec[k][2]} for k in order]
-    ot = O.OracleTable(props, [p[field[k]] for k in order], keys=keys, threshold=0.9, maybe=0.7)
+    from dukehip import _abi as A
+    mode = {A.MODE_DEDUP: "dedup", A.MODE_LINKAGE: "linkage", A.MODE_ALLPAIRS: "allpairs"}[w["mode"]]
+    props = [{k: v for k, v in p.items() if k != "name"} for p in w["props"]]
+    ot = O.OracleTable(props, [w["values"][p["name"]] for p in w["props"]], keys=w["keys"],
+                       group=w["group"], threshold=w["threshold"], maybe=w["maybe"], mode=mode)
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    n = ot.n
-    probe = min(n, 2000)
-    r = ot.match(np.arange(probe, dtype=np.uint32), nthreads=threads)
+    allq = w["queries"]
+    probe = min(len(allq), 2000 if mode != "allpairs" else 64)
+    r = ot.match(allq[:probe], nthreads=threads)
     rate = r["pairs_scored"] / max(r["ms_score"] / 1e3, 1e-9)
     per_q = r["pairs_scored"] / probe
-    s = int(min(n, max(probe, args.cpu_seconds * rate / max(per_q, 1e-9))))
-    r = ot.match(np.arange(s, dtype=np.uint32), nthreads=threads)
+    s = int(min(len(allq), max(probe, args.cpu_seconds * rate / max(per_q, 1e-9))))
+    r = ot.match(allq[:s], nthreads=threads)
     e = int(gpu_res.first[s])
-    gq = np.repeat(np.arange(s, dtype=np.uint32), np.diff(gpu_res.first[: s + 1]).astype(np.int64))
+    gq = np.repeat(allq[:s], np.diff(gpu_res.first[: s + 1]).astype(np.int64))
     ok = (np.array_equal(r["query"], gq) and np.array_equal(r["candidate"], gpu_res.candidate[:e])
           and np.array_equal(r["prob"], gpu_res.prob[:e]) and np.array_equal(r["kind"], gpu_res.kind[:e]))
     cpu = ""
@@ -222,7 +294,7 @@ def cpu_baseline(p, keys, order, spec, gpu_res, args):
         pass
     return {"value": r["pairs_scored"] / (r["ms_score"] / 1e3), "unit": "pairs/s", "cores": threads,
             "kind": "port",
-            "sample": f"first {s} of {n} query records ({r['pairs_scored']} pairs), "
+            "sample": f"first {s} of {len(allq)} query records ({r['pairs_scored']} pairs), "
                       f"scoring loop timed, blocking-index build excluded ({r['ms_index']:.0f} ms)",
             "seconds": r["ms_score"] / 1e3, "cpu_model": cpu, "host_nproc": os.cpu_count(),
             "matches_identical_to_gpu": bool(ok)}
