@@ -291,7 +291,6 @@ __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str
 //    n1 == 1, makes row 0 of column j read the row-1 value of column j-1.  Cell:
 //    min(D(i-1,j) + w(s1[i-1]), D(i,j-1) + w(s2[j-1]), D(i-1,j-1) + cost).
 // ------------------------------------------------------------------------------------
-constexpr int kLongRowLanes = 16;  // lanes per candidate (one DPP row)
 
 // [Duke 1.2] comparators.WeightedLevenshtein.DefaultWeightEstimator: letters 1.0,
 // digits 2.0, punctuation 0.1, anything else 1.0
@@ -317,22 +316,45 @@ __device__ __forceinline__ double dpp_row_shr1(double old, double v) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// DPP wave_shr:1 (a gfx9-family control): lane l receives lane l-1's value across the
+// whole wave; lane 0 keeps `old`
+__device__ __forceinline__ int dpp_wave_shr1(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ double dpp_wave_shr1(double old, double v) {
+  const uint64_t o = (uint64_t)__double_as_longlong(old), x = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)o, (int)(uint32_t)x, 0x138, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(o >> 32), (int)(uint32_t)(x >> 32),
+                                                            0x138, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// the value of lane k-1 of this lane's G-lane group (k = 0 takes `top`)
+template <int G, typename T>
+__device__ __forceinline__ T from_left(T top, T v, int k) {
+  if (G == 16) return dpp_row_shr1(top, v);  // DPP rows are 16 lanes: lane 0 of a row keeps top
+  const T x = dpp_wave_shr1(top, v);
+  return k == 0 ? top : x;
+}
+
 // Per-wave LDS of the long-value section (inside the wave's Peq slice, zeroed on exit):
 // u16 s2 units [4 rows][kMaxLongUnits], f64 results [64], u32 lane list [64].
 constexpr int kLongS2Words = 4 * kMaxLongUnits * 2 / 8;  // u64 words of the s2 staging
 constexpr int kLongLdsWords = kLongS2Words + 64 + 32;
 static_assert(kLongLdsWords <= kPeqEntries, "long-value LDS must fit the Peq slice");
 
-template <int R, bool WL, typename CT>
+template <int G, int R, bool WL, typename CT>
 __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint64_t* lds, const CT* s1p,
                                         int n1, uint32_t g, uint32_t crow, int lc, int nneed) {
   using T = typename std::conditional<WL, double, int>::type;
   constexpr int UPW = 4 / (int)sizeof(CT);
+  constexpr int NG = 64 / G;  // candidates per round
   uint16_t* s2buf = reinterpret_cast<uint16_t*>(lds);
   double* res = reinterpret_cast<double*>(lds + kLongS2Words);
   const uint32_t* list = reinterpret_cast<const uint32_t*>(lds + kLongS2Words + 64);
   const int lane = (int)lane_id();
-  const int grp = lane >> 4, k = lane & 15;
+  const int grp = lane / G, k = lane % G;
   const int kstar = (n1 - 1) / R, rstar = n1 - kstar * R;
   uint16_t* row_s2 = s2buf + grp * kMaxLongUnits;
   // this lane's query rows
@@ -345,23 +367,23 @@ __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint
     w1[r] = WL ? wl_weight(c1[r]) : 0.0;
   }
   const CT* base = reinterpret_cast<const CT*>(D.units);
-  for (int r0 = 0; r0 < nneed; r0 += 4) {
+  for (int r0 = 0; r0 < nneed; r0 += NG) {
     const int idx = r0 + grp;
     const bool has = idx < nneed;
     const int src = has ? (int)list[idx] : 0;
-    // cross-lane reads with every lane active (a lane of a row without a pair may still
-    // be the source another row reads from)
+    // cross-lane reads with every lane active (a lane of a group without a pair may still
+    // be the source another group reads from)
     const uint32_t gg = (uint32_t)__shfl((int)g, src);
     const uint32_t cr = (uint32_t)__shfl((int)crow, src);
     const int lsrc = __shfl(lc, src);
     const int n2 = has ? lsrc : 0;
-    // stage the row's candidate value in LDS as u16 units
+    // stage the group's candidate value in LDS as u16 units
     const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + gg, rstride,
                                          D.rlmax / Str<CT>::UPW - 1}
                                : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[cr]), 1, 1 << 30};
     wave_lds_sync();  // previous round's reads of s2buf are done
     const int nw = (n2 + UPW - 1) / UPW;
-    for (int w = k; w < nw; w += kLongRowLanes) {
+    for (int w = k; w < nw; w += G) {
       const uint32_t x = s2.word(w);
 #pragma unroll
       for (int u = 0; u < UPW; ++u) row_s2[w * UPW + u] = (uint16_t)Str<CT>::unit(x, u);
@@ -383,7 +405,7 @@ __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint
       T top;
       if (WL) top = n1 == 1 ? col[0] : (T)(j == 1 ? n1 : j);
       else top = (T)j;
-      const T recv = dpp_row_shr1(top, bot);  // D(k*R, j)
+      const T recv = from_left<G>(top, bot, k);  // D(k*R, j)
       if (j >= 1 && j <= n2) {
         T up = recv, dg = prev;
         if (WL) {
@@ -413,19 +435,23 @@ __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint
       }
     }
     if (has && k == kstar) {
-      T v = col[0];
+      // col[rstar - 1] as a mask-or (a select chain becomes a dynamically indexed load)
+      uint64_t bits = 0;
 #pragma unroll
-      for (int r = 1; r < R; ++r) v = r + 1 == rstar ? col[r] : v;
+      for (int r = 0; r < R; ++r) {
+        const uint64_t b = WL ? (uint64_t)__double_as_longlong((double)col[r]) : (uint64_t)(uint32_t)(int)col[r];
+        bits |= b & (0ull - (uint64_t)(r + 1 == rstar));
+      }
       double sim;
       if (WL) {
         // [Duke 1.2] WeightedLevenshtein.compare
         const double maxlen = (double)max(n1, n2);
-        const double dist = (double)v;
+        const double dist = __longlong_as_double((long long)bits);
         sim = dist > maxlen ? 0.0 : 1.0 - (dist / maxlen);
       } else {
         // [Duke 1.2] Levenshtein.compare: 1 - min(dist, len) / len
         const int len = min(n1, n2);
-        sim = 1.0 - ((double)min((int)v, len) / (double)len);
+        sim = 1.0 - ((double)min((int)(uint32_t)bits, len) / (double)len);
       }
       res[src] = sim;
     }
@@ -447,11 +473,19 @@ __device__ __forceinline__ double long_sims(const DevProp& D, uint64_t rstride, 
   wave_lds_sync();
   const CT* s1p = reinterpret_cast<const CT*>(D.units) + D.off[q];
   // rows per lane: n1 is wave-uniform, so this is a scalar switch
-  if (n1 <= 16) long_dp<1, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 32) long_dp<2, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 64 || LR <= 4) long_dp<4, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 128 || LR <= 8) long_dp<(LR < 8 ? 4 : 8), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else long_dp<(LR < 16 ? 4 : 16), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  // query rows per lane: 16-lane groups (4 candidates a round) up to 64 rows, 32-lane
+  // groups (2 a round, wave_shr) beyond; R = rows / lanes rounded up, so most of a group's
+  // lanes hold rows and R <= 8 keeps the column, weights and units in VGPRs
+  if (n1 <= 16) long_dp<16, 1, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 32) long_dp<16, 2, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 48) long_dp<16, 3, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 64 || LR <= 4) long_dp<16, 4, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 96) long_dp<32, 3, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 128 || LR <= 8) long_dp<32, 4, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 160) long_dp<32, (LR < 16 ? 4 : 5), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 192) long_dp<32, (LR < 16 ? 4 : 6), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 224) long_dp<32, (LR < 16 ? 4 : 7), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else long_dp<32, (LR < 16 ? 4 : 8), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
   wave_lds_sync();
   if (need) sim = res[lane_id()];
   wave_lds_sync();
@@ -829,7 +863,8 @@ void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t n
 }
 
 template <int RMAX, int LR>
-__global__ __launch_bounds__(256) void k_score_long(const ScoreParams P, const PairSource S,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LR <= 8 ? 4 : 3, 8)))
+void k_score_long(const ScoreParams P, const PairSource S,
                                                     uint64_t slot0, uint64_t nslots, StageOut out) {
   score_body<RMAX, LR>(P, S, slot0, nslots, out);
 }
