@@ -281,7 +281,7 @@ struct dk_ctx {
   DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], rowof, sgroup[kMaxKeys];
   const uint32_t* rowof_p = nullptr;  // replica position -> row (rowof, or usable in ALLPAIRS)
   uint64_t rstride = 0;               // replica positions
-  DevBuf ranges, counts, qoff, pq, pc, tmp;
+  DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
   DevBuf counters, st_bcnt, st_bscored, st_bbytes, st_boff, st_prob, st_cand, st_qidx;
   PinnedBuf h_small;
   std::shared_ptr<ResultPool> pool = std::make_shared<ResultPool>();
@@ -848,11 +848,21 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   rc = allpairs ? build_replica(c, c->usable.as<uint32_t>(), M)
                 : build_replica(c, c->rowof.as<uint32_t>(), (uint64_t)nk * M);
   if (rc) return rc;
+  if (!allpairs) {  // replica-ordered identity / keys for the candidate filters
+    const uint64_t npos = (uint64_t)nk * M;
+    HIPCHK(c->rident.reserve(npos * 8 + 8, 0, s));
+    uint64_t* rk[kMaxKeys] = {};
+    for (int k = 0; k + 1 < nk; ++k) {
+      HIPCHK(c->rkeys[k].reserve(npos * 8 + 8, 0, s));
+      rk[k] = c->rkeys[k].as<uint64_t>();
+    }
+    HIPCHK(launch_replicate_rows(c->rowof.as<uint32_t>(), npos, c->ident.as<uint64_t>(),
+                                 c->rident.as<uint64_t>(), T, rk, s));
+  }
   c->prof.ms_index += t_index.stop();
 
   // ---- candidate counts per query -> slot offsets ----
   Timer t_gen(prof, s);
-  std::vector<uint64_t> qoff(nq + 1, 0);
   uint64_t total = 0, generated = 0, mpad = 0;
   if (!allpairs) {
     HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
@@ -865,14 +875,17 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
     }));
-    HIPCHK(hipMemcpyAsync(qoff.data(), c->qoff.p, (nq + 1) * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(c->h_small.as<uint64_t>() + 2, c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
+    uint64_t* hs = c->h_small.as<uint64_t>();
+    HIPCHK(hipMemcpyAsync(&hs[3], c->qoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&hs[2], c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    total = qoff[nq];
-    generated = c->h_small.as<uint64_t>()[2];
+    total = hs[3];
+    generated = hs[2];
+    // every wave of slots knows its query
+    HIPCHK(c->wq.reserve(total / 64 * 4 + 4, 0, s));
+    HIPCHK(launch_wavemap(c->qoff.as<uint64_t>(), nq, c->wq.as<uint32_t>(), s));
   } else {
     mpad = (M + 63) & ~(uint64_t)63;
-    for (uint64_t i = 0; i <= nq; ++i) qoff[i] = i * mpad;
     total = nq * mpad;
     generated = nq * M;
   }
@@ -882,10 +895,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   const uint64_t CH = (chunk_slots() + kScoreBlock - 1) / kScoreBlock * kScoreBlock;
   const uint64_t chunk = std::min(CH, std::max<uint64_t>(total, 1));
   const uint64_t nblk_max = (chunk + kScoreBlock - 1) / kScoreBlock;
-  if (!allpairs) {
-    HIPCHK(c->pq.reserve(chunk * 4 + 4, 0, s));
-    HIPCHK(c->pc.reserve(chunk * 4 + 4, 0, s));
-  }
   HIPCHK(c->st_bcnt.reserve(nblk_max * 4 + 4, 0, s));
   HIPCHK(c->st_bscored.reserve(nblk_max * 4 + 4, 0, s));
   HIPCHK(c->st_bbytes.reserve(nblk_max * 4 + 4, 0, s));
@@ -904,20 +913,21 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     const uint64_t nblk = (s1 - s0 + kScoreBlock - 1) / kScoreBlock;
     PairSource src{};
     src.queries = c->d_queries.as<uint32_t>();
+    src.m = M;
     if (allpairs) {
       src.allpairs = 1;
-      src.m = M;
       src.mpad = mpad;
     } else {
-      Timer t_emit(prof, s);
-      const uint64_t q0 = (uint64_t)(std::upper_bound(qoff.begin(), qoff.end(), s0) - qoff.begin()) - 1;
-      const uint64_t q1 = (uint64_t)(std::lower_bound(qoff.begin(), qoff.end(), s1) - qoff.begin());
-      HIPCHK(launch_emit(c->d_queries.as<uint32_t>(), q0, std::min(q1, nq), c->qoff.as<uint64_t>(),
-                         c->ranges.as<uint2>(), nq, T, c->ident.as<uint64_t>(), s0, s1,
-                         c->pq.as<uint32_t>(), c->pc.as<uint32_t>(), s));
-      c->prof.ms_generate += t_emit.stop();
-      src.pq = c->pq.as<uint32_t>();
-      src.pc = c->pc.as<uint32_t>();
+      src.wq = c->wq.as<uint32_t>();
+      src.qoff = c->qoff.as<uint64_t>();
+      src.ranges = c->ranges.as<uint2>();
+      src.nq = nq;
+      src.nkeys = nk;
+      src.rident = c->rident.as<uint64_t>();
+      for (int k = 0; k < nk; ++k) {
+        src.qkeys[k] = c->keys[k].as<uint64_t>();
+        src.rkeys[k] = c->rkeys[k].as<uint64_t>();
+      }
     }
     Timer t_score(prof, s);
     HIPCHK(launch_score(P, src, s0, s1 - s0, st, s));
@@ -1056,7 +1066,7 @@ int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
   if (r1 >= c->nrows || r2 >= c->nrows) return fail(DK_E_INVALID, "row out of range");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  DevBuf buf;  // [0..3] query row, query index, replica position 0, rowof[0]; then staging
+  DevBuf buf;  // [0] query row, [3] rowof[0] (the one replica position); then staging
   HIPCHK(buf.reserve(8192, 0, s));
   uint32_t host[4] = {r1, 0u, 0u, r2};
   HIPCHK(hipMemsetAsync(buf.p, 0, 8192, s));
@@ -1071,10 +1081,12 @@ int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
   ScoreParams P = make_params(c);
   P.threshold = -INFINITY;  // every non-NaN probability is emitted
   P.maybe = 0.0;
-  PairSource src{};
+  PairSource src{};  // one all-pairs slot: query r1 against replica position 0 (row r2)
   src.queries = buf.as<uint32_t>();
-  src.pq = buf.as<uint32_t>() + 1;
-  src.pc = buf.as<uint32_t>() + 2;
+  src.allpairs = 1;
+  src.m = 1;
+  src.mpad = 64;
+  src.same_ok = 1;  // Processor.compare scores a record against itself too
   HIPCHK(launch_score(P, src, 0, 1, st, s));
   uint32_t n = 0;
   double p = NAN;

@@ -83,14 +83,23 @@ struct ScoreParams {
 // Where the (query, candidate) of a slot comes from.  Every query's slots are padded to
 // a multiple of 64, so each wave of k_score holds exactly one query.
 struct PairSource {
-  // blocked modes: materialised chunk of slots
-  const uint32_t* pq;  // query index (into the query list)
-  const uint32_t* pc;  // replica position of the candidate, or kSentinel
-  // ALLPAIRS: implicit slots s -> (s / mpad, replica position s % mpad if < m)
   const uint32_t* queries;  // query rows
-  uint64_t m;
-  uint64_t mpad;            // m rounded up to a wave (64)
+  // blocked modes: slot s of query qi (qoff[qi] <= s < qoff[qi+1]) is candidate t = s -
+  // qoff[qi] of its concatenated key-function ranges; t past their total is padding
+  const uint32_t* wq;       // global wave (slot / 64) -> query index
+  const uint64_t* qoff;     // query index -> first slot
+  const uint2* ranges;      // [k * nq + qi]: candidate range of query qi in sorted table k
+  uint64_t nq;
+  int32_t nkeys;
   int32_t allpairs;
+  const uint64_t* qkeys[kMaxKeys];  // key of every row (the query side's keys)
+  const uint64_t* rident;   // per replica position: ident of its row (Processor.isSameAs)
+  const uint64_t* rkeys[kMaxKeys];  // per replica position: key j of its row, j < nkeys - 1
+  // ALLPAIRS: slot s -> (s / mpad, replica position s % mpad if < m)
+  uint64_t m;               // usable rows (= replica positions per key function)
+  uint64_t mpad;            // m rounded up to a wave (64)
+  int32_t same_ok;          // score pairs of one identity too (dk_compare_rows)
+  int32_t pad;
 };
 
 // Per-chunk staging of the score kernel.  Block b (256 slots) writes its emitted entries,
@@ -170,10 +179,12 @@ hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t
 // real[0] += the unpadded total
 hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint2* ranges,
                         uint64_t* counts, uint64_t* real, hipStream_t s);
-hipError_t launch_emit(const uint32_t* queries, uint64_t q0, uint64_t q1, const uint64_t* qoff,
-                       const uint2* ranges, uint64_t nq, const BlockTables& T,
-                       const uint64_t* ident, uint64_t s0, uint64_t s1, uint32_t* pq,
-                       uint32_t* pc, hipStream_t s);
+// wq[w] = qi for the waves of query qi's slots (qoff in slots, multiples of 64)
+hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s);
+// replica-ordered identity and keys 0..nkeys-2 of the rows at replica positions
+hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t npos, const uint64_t* ident,
+                                 uint64_t* rident, const BlockTables& T, uint64_t* const* rkeys,
+                                 hipStream_t s);
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                         uint64_t nslots, const StageOut& out, hipStream_t s);
 hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s);

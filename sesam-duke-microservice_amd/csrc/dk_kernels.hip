@@ -19,6 +19,10 @@
 
 namespace dk {
 
+struct RowKeys {
+  uint64_t* p[kMaxKeys];
+};
+
 // ------------------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------------------
@@ -754,25 +758,47 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
 
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = idx < nslots;
+  const uint64_t s = slot0 + min(idx, nslots - 1);
   uint32_t qi = 0, g = 0;
   if (S.allpairs) {
     // slots of a query: [qi * mpad, qi * mpad + m), mpad = m rounded up to 64
-    const uint64_t s = slot0 + min(idx, nslots - 1);
     qi = (uint32_t)(s / S.mpad);
     const uint64_t t = s - (uint64_t)qi * S.mpad;
     valid = valid && t < S.m;
     g = valid ? (uint32_t)t : 0u;
   } else {
-    qi = S.pq[min(idx, nslots - 1)];
-    const uint32_t w = valid ? S.pc[idx] : kSentinel;
-    valid = w != kSentinel;
-    g = valid ? w : 0u;  // lanes without a pair read replica position 0 (always in range)
+    qi = S.wq[s >> 6];  // one query per wave by construction (padded slot layout)
   }
-  // one query per wave by construction (padded slot layout)
   qi = __builtin_amdgcn_readfirstlane(qi);
   const uint32_t q = __builtin_amdgcn_readfirstlane(S.queries[qi]);
+  if (!S.allpairs) {
+    // Candidate t of the query: key function k's range first, then (group, row) order
+    // inside it.  Filters: isSameAs (identity), and "already a candidate under an
+    // earlier key function" (Duke returns candidates as a set).  The ranges and the
+    // query's keys are wave-uniform.
+    uint64_t t = s - S.qoff[qi];
+    int k = -1;
+    for (int kk = 0; kk < S.nkeys; ++kk) {
+      const uint2 r = S.ranges[(uint64_t)kk * S.nq + qi];
+      const uint64_t len = (uint64_t)(r.y - r.x);
+      if (k < 0) {
+        if (t < len) {
+          k = kk;
+          g = (uint32_t)((uint64_t)kk * S.m + r.x + t);
+        } else {
+          t -= len;
+        }
+      }
+    }
+    valid = valid && k >= 0;
+    if (!valid) g = 0u;  // lanes without a pair read replica position 0 (always in range)
+    bool ok = S.rident[g] != P.ident[q];
+    for (int j = 0; j < S.nkeys - 1; ++j)
+      if (j < k) ok = ok && S.rkeys[j][g] != S.qkeys[j][q];
+    valid = valid && ok;
+  }
   const uint32_t crow = P.rowof[g];
-  if (S.allpairs) valid = valid && P.ident[crow] != P.ident[q];  // Processor.isSameAs
+  if (S.allpairs && !S.same_ok) valid = valid && P.ident[crow] != P.ident[q];  // Processor.isSameAs
   wave_lds_sync();
 
   double prob = 0.5;
@@ -1015,54 +1041,25 @@ __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const
   if (lane_id() == 0 && w) atomicAdd((unsigned long long*)real, (unsigned long long)w);
 }
 
-// One wave per query (grid-stride): writes the query's candidate slots that fall in
-// [s0, s1) as replica positions.  Slot order inside a query = key function, then (group,
-// row) order of the sorted table.  Filters: isSameAs (identity) and "already a candidate
-// under an earlier key function" (Duke returns candidates as a set).  Slots past the
-// query's candidates up to its next multiple of 64 are padding (kSentinel).
-__global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ queries, uint64_t q0,
-                                              uint64_t q1, const uint64_t* __restrict__ qoff,
-                                              const uint2* __restrict__ ranges, uint64_t nq,
-                                              const BlockTables T, const uint64_t* __restrict__ ident,
-                                              uint64_t s0, uint64_t s1, uint32_t* __restrict__ pq,
-                                              uint32_t* __restrict__ pc) {
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t qi = q0 + wave; qi < q1; qi += nwaves) {
-    const uint64_t qa = qoff[qi], qb = qoff[qi + 1];
-    const uint64_t a = max(qa, s0), b = min(qb, s1);
-    if (a >= b) continue;
-    const uint32_t q = queries[qi];
-    const uint64_t idq = ident[q];
-    uint64_t real = 0;
-    for (int k = 0; k < T.nkeys; ++k) {
-      const uint2 r = ranges[(uint64_t)k * nq + qi];
-      real += r.y - r.x;
-    }
-    for (uint64_t s = a + lane; s < b; s += 64) {
-      uint64_t t = s - qa;
-      pq[s - s0] = (uint32_t)qi;
-      if (t >= real) {  // padding up to the query's last wave
-        pc[s - s0] = kSentinel;
-        continue;
-      }
-      int k = 0;
-      uint2 r = ranges[qi];
-      for (; k < T.nkeys - 1; ++k) {
-        r = ranges[(uint64_t)k * nq + qi];
-        const uint64_t len = (uint64_t)(r.y - r.x);
-        if (t < len) break;
-        t -= len;
-      }
-      if (k == T.nkeys - 1) r = ranges[(uint64_t)k * nq + qi];
-      const uint64_t gpos = (uint64_t)k * T.m + r.x + t;
-      const uint32_t c = T.rowof[gpos];
-      bool ok = ident[c] != idq;
-      for (int j = 0; j < k && ok; ++j) ok = T.keys[j][c] != T.keys[j][q];
-      pc[s - s0] = ok ? (uint32_t)gpos : kSentinel;
-    }
-  }
+// wq[w] = qi for every wave w of query qi's slots (one thread per query, its waves in a
+// short loop: a query spans a few waves on average)
+__global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32_t* __restrict__ wq) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  for (uint64_t w = qoff[i] >> 6, e = qoff[i + 1] >> 6; w < e; ++w) wq[w] = (uint32_t)i;
+}
+
+// replica-ordered identity and keys (the score kernel's candidate filters read them
+// coalesced, 64 consecutive positions per wave)
+__global__ __launch_bounds__(256) void k_replicate_rows(const uint32_t* __restrict__ rowof, uint64_t npos,
+                                                        const uint64_t* __restrict__ ident,
+                                                        uint64_t* __restrict__ rident, const BlockTables T,
+                                                        RowKeys rk) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= npos) return;
+  const uint32_t row = rowof[g];
+  rident[g] = ident[row];
+  for (int j = 0; j < T.nkeys - 1; ++j) rk.p[j][g] = T.keys[j][row];
 }
 
 // ------------------------------------------------------------------------------------
@@ -1181,14 +1178,19 @@ hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables&
   return hipGetLastError();
 }
 
-hipError_t launch_emit(const uint32_t* queries, uint64_t q0, uint64_t q1, const uint64_t* qoff,
-                       const uint2* ranges, uint64_t nq, const BlockTables& T,
-                       const uint64_t* ident, uint64_t s0, uint64_t s1, uint32_t* pq,
-                       uint32_t* pc, hipStream_t s) {
-  if (q1 <= q0 || s1 <= s0) return hipSuccess;
-  const uint64_t waves = q1 - q0;
-  const unsigned blocks = (unsigned)std::min<uint64_t>((waves + 3) / 4, 256u * 32u);
-  k_emit<<<blocks, 256, 0, s>>>(queries, q0, q1, qoff, ranges, nq, T, ident, s0, s1, pq, pc);
+hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s) {
+  DK_LAUNCH_GUARD(nq);
+  k_wavemap<<<grid1d(nq), 256, 0, s>>>(qoff, nq, wq);
+  return hipGetLastError();
+}
+
+hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t npos, const uint64_t* ident,
+                                 uint64_t* rident, const BlockTables& T, uint64_t* const* rkeys,
+                                 hipStream_t s) {
+  DK_LAUNCH_GUARD(npos);
+  RowKeys rk{};
+  for (int j = 0; j < T.nkeys - 1; ++j) rk.p[j] = rkeys[j];
+  k_replicate_rows<<<grid1d(npos), 256, 0, s>>>(rowof, npos, ident, rident, T, rk);
   return hipGetLastError();
 }
 
