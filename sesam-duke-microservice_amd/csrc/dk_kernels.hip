@@ -528,82 +528,76 @@ __device__ __forceinline__ double jarowinkler(Str<CT> s1, int n1, Str<CT> s2, in
 }
 
 // [Duke 1.2] comparators.JaroWinkler.similarity with the query's Peq table (both values
-// <= 64 units).  s1 is the shorter value (the query on a tie).
-//  * candidate shorter (rows = candidate units): row i's first match is the lowest set
-//    bit of Peq[cand[i]] inside the window over the query — one LDS read per row.
-//  * query shorter or equal (rows = query units): sweep the candidate's units j in order;
-//    Peq[cand[j]] gives every query row holding that unit, masked to the rows whose
-//    window contains j and not yet matched; the found step j is kept in six bit-planes,
-//    read back row by row for the transposition count.
+// <= 64 units).  s1 is the shorter value (the query on a tie).  One sweep over the
+// candidate's units j serves both cases, so lanes of either kind share it:
+//  * candidate shorter (s1 = candidate, rows = its units): row j's first match is the
+//    lowest set bit of Peq[cand[j]] inside the window over the query;
+//  * query shorter or equal (rows = query units): Peq[cand[j]] gives every query row
+//    holding that unit, masked to the rows whose window contains j and not yet matched
+//    (Duke takes the FIRST match in the window); the step j that matched each row is kept
+//    in six bit-planes.  The transposition count (a row matching before the previous
+//    matched row did) then comes bit-parallel: each plane's bit is carried from one
+//    matched row to the next by an add through the unmatched rows between them, and a
+//    bit-sliced compare of the two 6-bit steps counts the descents.
+__device__ __forceinline__ uint64_t carry_to_next(uint64_t plane, uint64_t found) {
+  // bit i of the result = bit of `plane` at the matched row before matched row i
+  return (((plane & found) << 1) + ~found) & found;
+}
+
 template <typename CT>
 __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str<CT>& qs, int nq,
                                                   const Str<CT>& cs, int nc, bool act) {
   if (act && str_equal(qs, nq, cs, nc)) act = false;  // 1.0 below
   const bool rows_cand = act && nc < nq;
   const bool rows_query = act && !rows_cand;
-  int c = 0, t = 0;
-  {
-    const int md = nq >> 1;
-    int prev = -1;
-    constexpr int UPW = Str<CT>::UPW;
-    for (int k = 0; rows_cand && k * UPW < nc; ++k) {
-      const uint32_t w = cs.word(k);
+  // window over the query: [j - md, j + md) for candidate row j (md = |query| / 2), or the
+  // rows i with j in [i - md, i + md) (md = |candidate| / 2) — both as [lo_off + j, hi_off + j)
+  const int md = rows_cand ? (nq >> 1) : (nc >> 1);
+  const int lo_off = rows_cand ? -md : 1 - md, hi_off = rows_cand ? md : md + 1;
+  int c = 0, t = 0, prev = -1;
+  uint64_t found = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
+  const int maxn = act ? nc : 0;
+  int wmax = maxn;
+  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
+  constexpr int UPW = Str<CT>::UPW;
+  for (int k = 0; k * UPW < wmax; ++k) {
+    const uint32_t w = cs.word_any(k);  // units past maxn are never used (j < maxn)
 #pragma unroll
-      for (int u = 0; u < UPW; ++u) {
-        const int i = k * UPW + u;
-        if (i < nc) {
-          const uint64_t e = peq_eq<CT>(peq, Str<CT>::unit(w, u));
-          const uint64_t m = e & range_mask(max(0, i - md), min(nq, i + md));
-          if (m) {
-            const int j = ffs64(m);
-            ++c;
-            if (prev != -1 && j < prev) ++t;
-            prev = j;
-          }
-        }
-      }
+    for (int u = 0; u < UPW; ++u) {
+      const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
+      uint64_t e = 0;
+      if (j < maxn)
+        e = peq_eq<CT>(peq, Str<CT>::unit(w, u)) & range_mask(max(0, j + lo_off), min(nq, j + hi_off));
+      // candidate rows: first match of row j
+      const uint64_t ec = rows_cand ? e : 0ull;
+      const int jj = ffs64(ec | (1ull << 63));
+      const bool has = ec != 0;
+      c += has ? 1 : 0;
+      t += (has && prev != -1 && jj < prev) ? 1 : 0;
+      prev = has ? jj : prev;
+      // query rows: rows first matched at step j
+      const uint64_t m = rows_query ? (e & ~found) : 0ull;
+      found |= m;
+      if (j & 1) p0 |= m;
+      if (j & 2) p1 |= m;
+      if (j & 4) p2 |= m;
+      if (j & 8) p3 |= m;
+      if (j & 16) p4 |= m;
+      if (j & 32) p5 |= m;
     }
   }
-  if (__ballot(rows_query)) {
-    const int md = nc >> 1;
-    uint64_t found = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
-    const int maxn = rows_query ? nc : 0;
-    int wmax = maxn;
-    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
-    constexpr int UPW = Str<CT>::UPW;
-    for (int k = 0; k * UPW < wmax; ++k) {
-      const uint32_t w = cs.word_any(k);  // units past maxn are never used (j < maxn)
+  if (rows_query) {
+    c = __popcll(found);
+    // descents p(i) < p(previous matched row), MSB-first bit-sliced compare
+    const uint64_t P[6] = {p0, p1, p2, p3, p4, p5};
+    uint64_t lt = 0, eq = ~0ull;
 #pragma unroll
-      for (int u = 0; u < UPW; ++u) {
-        const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
-        uint64_t m = 0;
-        if (j < maxn) {
-          const uint64_t r = peq_eq<CT>(peq, Str<CT>::unit(w, u));
-          m = r & range_mask(max(0, j - md + 1), min(nq, j + md + 1)) & ~found;
-        }
-        found |= m;
-        if (j & 1) p0 |= m;
-        if (j & 2) p1 |= m;
-        if (j & 4) p2 |= m;
-        if (j & 8) p3 |= m;
-        if (j & 16) p4 |= m;
-        if (j & 32) p5 |= m;
-      }
+    for (int b = 5; b >= 0; --b) {
+      const uint64_t a = P[b], q = carry_to_next(P[b], found);
+      lt |= eq & ~a & q;
+      eq &= ~(a ^ q);
     }
-    if (rows_query) {
-      c = __popcll(found);
-      int prev = -1;
-      uint64_t f = found;
-      while (f) {
-        const int i = ffs64(f);
-        f &= f - 1ull;
-        const int p = (int)((p0 >> i) & 1ull) | (int)(((p1 >> i) & 1ull) << 1) |
-                      (int)(((p2 >> i) & 1ull) << 2) | (int)(((p3 >> i) & 1ull) << 3) |
-                      (int)(((p4 >> i) & 1ull) << 4) | (int)(((p5 >> i) & 1ull) << 5);
-        if (prev != -1 && p < prev) ++t;
-        prev = p;
-      }
-    }
+    t = __popcll(lt & found);
   }
   if (!act) return 1.0;  // equal values (inactive lanes discard the result)
   if (c == 0) return 0.0;
