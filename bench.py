@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the oracle baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--device-results", action="store_true",
+                    help="diagnostic: keep the N=1 match list in HBM (no device->host copy)")
     ap.add_argument("--only", default=None,
                     help="diagnostic: comma-separated property names to keep (not a bench line)")
     return ap.parse_args()
@@ -172,7 +174,7 @@ def main():
         if old is not None:
             old.close()                       # hand the result memory back to the pool
         if dist is None:
-            res = eng.match(queries)          # entries land in pinned host memory
+            res = eng.match(queries, on_device=args.device_results)  # pinned host memory
             holder["res"] = res
             return res, res.pairs_scored
         # N>1: entries stay in HBM; RCCL all-gathers the per-rank counts, then gathers
