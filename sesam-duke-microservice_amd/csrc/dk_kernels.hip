@@ -632,6 +632,61 @@ __device__ __forceinline__ int count_members(const uint64_t* __restrict__ g1, in
   return hit;
 }
 
+// |Q ∩ C| with the query's gram set Q in a per-wave LDS hash table (open addressing,
+// load <= 1/2, key + 1 stored so 0 marks an empty slot; the caller excludes a set holding
+// the all-ones code) and each lane probing its candidate's grams in order — the loads of a
+// lane's own list are independent of the probes, so they are issued one gram ahead instead
+// of the data-dependent two-list merge.  Wave-uniform call; the table is cleared on exit
+// (the LDS slice is the query's Peq table between properties, all zero).
+constexpr int kQgramHashMax = 128;  // grams of a query held in the table (<= 256 slots)
+
+__device__ __forceinline__ uint32_t gram_hash(uint64_t code, int lt) {
+  return (((uint32_t)code ^ (uint32_t)(code >> 32)) * 0x9E3779B1u) >> (32 - lt);
+}
+
+__device__ __forceinline__ int qgram_common_hashed(uint64_t* tab, const uint64_t* __restrict__ g1, int m1,
+                                                   const uint64_t* __restrict__ g2, int m2) {
+  const int lt = m1 <= 32 ? 6 : (m1 <= 64 ? 7 : 8);
+  const uint32_t tmask = (1u << lt) - 1u;
+  for (int i = (int)lane_id(); i < m1; i += 64) {
+    const uint64_t key = g1[i] + 1ull;
+    uint32_t h = gram_hash(g1[i], lt);
+    while (atomicCAS((unsigned long long*)&tab[h], 0ull, (unsigned long long)key) != 0ull)
+      h = (h + 1u) & tmask;  // the set is unique: a taken slot holds another gram
+  }
+  wave_lds_sync();
+  // the lane's grams in chunks of 8 independent loads (clamped indices: no branch around a
+  // load), the next chunk in flight while the current one probes
+  int common = 0;
+  constexpr int CH = 8;
+  uint64_t cur[CH], nxt[CH];
+#pragma unroll
+  for (int u = 0; u < CH; ++u) cur[u] = g2[min(u, max(m2 - 1, 0))];
+  for (int k0 = 0; k0 < m2; k0 += CH) {
+#pragma unroll
+    for (int u = 0; u < CH; ++u) nxt[u] = g2[min(k0 + CH + u, max(m2 - 1, 0))];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      if (k0 + u < m2) {
+        const uint64_t key = cur[u] + 1ull;
+        uint32_t h = gram_hash(cur[u], lt);
+        for (;;) {
+          const uint64_t v = tab[h];
+          if (v == key) { ++common; break; }
+          if (v == 0ull) break;
+          h = (h + 1u) & tmask;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) cur[u] = nxt[u];
+  }
+  wave_lds_sync();
+  for (int e = (int)lane_id(); e <= (int)tmask; e += 64) tab[e] = 0ull;
+  wave_lds_sync();
+  return common;
+}
+
 __device__ __forceinline__ int intersect_sorted(const uint64_t* __restrict__ g1, int m1,
                                                 const uint64_t* __restrict__ g2, int m2) {
   int i = 0, j = 0, common = 0;
@@ -703,18 +758,26 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
     case DK_CMP_EXACT:
       if (cmp) sim = str_equal(s1, lq, s2, lc) ? 1.0 : 0.0;
       break;
-    case DK_CMP_QGRAM:
-      if (cmp) {
-        if (str_equal(s1, lq, s2, lc)) {
+    case DK_CMP_QGRAM: {
+      const bool same = cmp && str_equal(s1, lq, s2, lc);
+      const int m1 = (int)__builtin_amdgcn_readfirstlane((uint32_t)D.gcnt[q]);
+      const uint64_t* g1 = D.grams + D.goff[q];
+      if (m1 > 0 && m1 <= kQgramHashMax && g1[m1 - 1] != ~0ull) {  // wave-uniform
+        sim = same ? 1.0 : 0.0;
+        const int m2 = cmp && !same ? (int)D.rgcnt[g] : 0;
+        const int common = qgram_common_hashed(peq, g1, m1, D.grams + D.rgoff[g], m2);
+        if (m2 > 0) sim = qgram_formula(common, m1, m2, D.formula);
+      } else if (cmp) {
+        if (same) {
           sim = 1.0;
         } else {
-          const int m1 = D.gcnt[q], m2 = D.rgcnt[g];
+          const int m2 = D.rgcnt[g];
           if (m1 == 0 || m2 == 0) sim = 0.0;
-          else sim = qgram_formula(intersect_sorted(D.grams + D.goff[q], m1, D.grams + D.rgoff[g], m2),
-                                   m1, m2, D.formula);
+          else sim = qgram_formula(intersect_sorted(g1, m1, D.grams + D.rgoff[g], m2), m1, m2, D.formula);
         }
       }
       break;
+    }
     case DK_CMP_DICE_TOKENS:
     case DK_CMP_JACCARD_TOKENS:
       if (cmp) {
