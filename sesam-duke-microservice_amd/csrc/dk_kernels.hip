@@ -665,17 +665,26 @@ __device__ __forceinline__ int qgram_common_hashed(uint64_t* tab, const uint64_t
   for (int k0 = 0; k0 < m2; k0 += CH) {
 #pragma unroll
     for (int u = 0; u < CH; ++u) nxt[u] = g2[min(k0 + CH + u, max(m2 - 1, 0))];
+    // first probes of the chunk issued together (one LDS latency for 8 grams); a slot
+    // holding another gram sends that gram down its probe sequence
+    uint32_t h[CH];
+    uint64_t v[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      h[u] = gram_hash(cur[u], lt);
+      v[u] = tab[h[u]];
+    }
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
       if (k0 + u < m2) {
         const uint64_t key = cur[u] + 1ull;
-        uint32_t h = gram_hash(cur[u], lt);
-        for (;;) {
-          const uint64_t v = tab[h];
-          if (v == key) { ++common; break; }
-          if (v == 0ull) break;
-          h = (h + 1u) & tmask;
+        uint64_t x = v[u];
+        uint32_t hh = h[u];
+        while (x != key && x != 0ull) {
+          hh = (hh + 1u) & tmask;
+          x = tab[hh];
         }
+        common += x == key ? 1 : 0;
       }
     }
 #pragma unroll
