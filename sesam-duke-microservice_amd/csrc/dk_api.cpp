@@ -227,10 +227,12 @@ struct PropState {
   uint64_t units_used = 0; // code units
   uint64_t grams_used = 0;
   int maxlen = 0;
+  int maxgrams = 0;        // longest code list of a value
   DevBuf off, len, units, num, numok, goff, gcnt, grams;
   // candidate replica of the current dk_match (see dk_internal.h)
   int rlmax = 0;
-  DevBuf rlen, runits, rnum, rnumok, rgoff, rgcnt;
+  int rgmax = 0;
+  DevBuf rlen, runits, rnum, rnumok, rgoff, rgcnt, rgrams;
 };
 
 // Result memory (device list + pinned host copy), pooled per ctx and handed back by
@@ -516,6 +518,7 @@ static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, 
         return fail(DK_E_UNSUPPORTED, "property %d: %zu q-grams / tokens", pidx, g.size());
       goff[i] = (uint32_t)(P.grams_used + grams.size());
       gcnt[i] = (uint16_t)g.size();
+      P.maxgrams = std::max<int>(P.maxgrams, (int)g.size());
       grams.insert(grams.end(), g.begin(), g.end());
     }
   }
@@ -713,6 +716,8 @@ static ScoreParams make_params(const dk_ctx* c) {
     D.rnumok = S.rnumok.as<uint8_t>();
     D.rgoff = S.rgoff.as<uint32_t>();
     D.rgcnt = S.rgcnt.as<uint16_t>();
+    D.rgrams = S.rgrams.as<uint64_t>();
+    D.rgmax = S.rgmax;
   }
   return P;
 }
@@ -741,6 +746,8 @@ static int build_replica(dk_ctx* c, const uint32_t* rowof, uint64_t npos) {
       HIPCHK(S.rgoff.reserve(npos * 4 + 8, 0, s));
       HIPCHK(S.rgcnt.reserve(npos * 2 + 8, 0, s));
     }
+    S.rgmax = op == DK_CMP_QGRAM && S.maxgrams <= kMaxReplicaGrams ? std::max(S.maxgrams, 1) : 0;
+    if (S.rgmax) HIPCHK(S.rgrams.reserve(npos * (uint64_t)S.rgmax * 8 + 64, 0, s));
     ReplicaJob J{};
     J.width = W;
     J.rlmax = S.rlmax;
@@ -760,6 +767,9 @@ static int build_replica(dk_ctx* c, const uint32_t* rowof, uint64_t npos) {
     J.rnumok = S.rnumok.as<uint8_t>();
     J.rgoff = S.rgoff.as<uint32_t>();
     J.rgcnt = S.rgcnt.as<uint16_t>();
+    J.rgmax = S.rgmax;
+    J.grams = S.grams.as<uint64_t>();
+    J.rgrams = S.rgrams.as<uint64_t>();
     HIPCHK(launch_replicate(J, rowof, npos, s));
   }
   return DK_OK;

@@ -15,6 +15,7 @@ constexpr uint16_t kMissing = 0xFFFF;  // length sentinel: record has no value
 constexpr int kMaxUnits = 64;          // Levenshtein query limit of the lane-per-pair DP
 constexpr int kMaxLongUnits = 256;     // WeightedLevenshtein / long Levenshtein value limit
 constexpr int kMaxReplicaUnits = 64;   // longer columns are read in place (canonical arena)
+constexpr int kMaxReplicaGrams = 64;   // QGram sets with more grams are read in place
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // filtered candidate slot
 
 // comparators whose values carry a precomputed sorted code list (goff/gcnt/grams):
@@ -40,7 +41,8 @@ constexpr uint8_t kDeleted = 2;  // dukeDeleted == "true" (IncrementalLuceneData
 //    rowof[g] = k-th table's i-th row — and per property its values in that order:
 //    rlen[g], runits transposed [unit j][g] (so the 64 lanes of a wave, which hold 64
 //    consecutive candidates, read unit j of their values as 64 consecutive elements),
-//    rnum/rnumok, rgoff/rgcnt.
+//    rnum/rnumok, rgoff/rgcnt, and for QGram sets of <= kMaxReplicaGrams grams the codes
+//    transposed rgrams[k][g] (zero past a set's count).
 // ---------------------------------------------------------------------------------------
 
 struct DevProp {
@@ -65,6 +67,9 @@ struct DevProp {
   const uint8_t* rnumok;
   const uint32_t* rgoff;
   const uint16_t* rgcnt;
+  const uint64_t* rgrams;  // QGram: [k * rstride + g], k < rgmax (0 = read grams in place)
+  int32_t rgmax;
+  int32_t pad2;
 };
 
 struct ScoreParams {
@@ -145,6 +150,7 @@ struct ReplicaJob {
   int32_t rlmax;      // 0: no unit replica (long values, or non-string comparator)
   int32_t has_num;
   int32_t has_qgram;
+  int32_t rgmax;      // QGram replica rows (0: none)
   uint64_t stride;    // replica positions
   const uint32_t* off;
   const uint16_t* len;
@@ -159,6 +165,8 @@ struct ReplicaJob {
   uint8_t* rnumok;
   uint32_t* rgoff;
   uint16_t* rgcnt;
+  const uint64_t* grams;
+  uint64_t* rgrams;
 };
 
 // ---- launchers (dk_kernels.hip) ----

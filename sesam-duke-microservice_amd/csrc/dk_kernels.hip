@@ -645,7 +645,8 @@ __device__ __forceinline__ uint32_t gram_hash(uint64_t code, int lt) {
 }
 
 __device__ __forceinline__ int qgram_common_hashed(uint64_t* tab, const uint64_t* __restrict__ g1, int m1,
-                                                   const uint64_t* __restrict__ g2, int m2) {
+                                                   const uint64_t* __restrict__ g2, uint64_t gstride,
+                                                   int gmax, int m2) {
   const int lt = m1 <= 32 ? 6 : (m1 <= 64 ? 7 : 8);
   const uint32_t tmask = (1u << lt) - 1u;
   for (int i = (int)lane_id(); i < m1; i += 64) {
@@ -661,10 +662,10 @@ __device__ __forceinline__ int qgram_common_hashed(uint64_t* tab, const uint64_t
   constexpr int CH = 8;
   uint64_t cur[CH], nxt[CH];
 #pragma unroll
-  for (int u = 0; u < CH; ++u) cur[u] = g2[min(u, max(m2 - 1, 0))];
+  for (int u = 0; u < CH; ++u) cur[u] = g2[(uint64_t)min(u, gmax) * gstride];
   for (int k0 = 0; k0 < m2; k0 += CH) {
 #pragma unroll
-    for (int u = 0; u < CH; ++u) nxt[u] = g2[min(k0 + CH + u, max(m2 - 1, 0))];
+    for (int u = 0; u < CH; ++u) nxt[u] = g2[(uint64_t)min(k0 + CH + u, gmax) * gstride];
     // first probes of the chunk issued together (one LDS latency for 8 grams); a slot
     // holding another gram sends that gram down its probe sequence
     uint32_t h[CH];
@@ -774,7 +775,10 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
       if (m1 > 0 && m1 <= kQgramHashMax && g1[m1 - 1] != ~0ull) {  // wave-uniform
         sim = same ? 1.0 : 0.0;
         const int m2 = cmp && !same ? (int)D.rgcnt[g] : 0;
-        const int common = qgram_common_hashed(peq, g1, m1, D.grams + D.rgoff[g], m2);
+        // candidate codes: the transposed replica (coalesced), or in place
+        const int common = D.rgmax
+            ? qgram_common_hashed(peq, g1, m1, D.rgrams + g, rstride, D.rgmax - 1, m2)
+            : qgram_common_hashed(peq, g1, m1, D.grams + D.rgoff[g], 1, max(m2 - 1, 0), m2);
         if (m2 > 0) sim = qgram_formula(common, m1, m2, D.formula);
       } else if (cmp) {
         if (same) {
@@ -1049,6 +1053,11 @@ __global__ __launch_bounds__(256) void k_replicate(const ReplicaJob J, const uin
   if (J.has_qgram) {
     J.rgoff[g] = J.goff[row];
     J.rgcnt[g] = J.gcnt[row];
+    if (J.rgmax) {  // codes transposed: the 64 lanes of a score wave read row k as 512 B
+      const uint64_t* src = J.grams + J.goff[row];
+      const int m = l == (int)kMissing ? 0 : (int)J.gcnt[row];
+      for (int k = 0; k < J.rgmax; ++k) J.rgrams[(uint64_t)k * J.stride + g] = k < m ? src[k] : 0ull;
+    }
   }
 }
 
