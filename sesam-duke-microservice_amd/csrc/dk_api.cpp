@@ -716,8 +716,9 @@ static ScoreParams make_params(const dk_ctx* c) {
     D.rnumok = S.rnumok.as<uint8_t>();
     D.rgoff = S.rgoff.as<uint32_t>();
     D.rgcnt = S.rgcnt.as<uint16_t>();
-    D.rgrams = S.rgrams.as<uint64_t>();
+    D.rgrams = S.rgrams.p;
     D.rgmax = S.rgmax;
+    D.rg32 = 16 * S.cfg.qgram_q + (S.cfg.qgram_tokenizer == DK_QGRAM_POSITIONAL ? 16 : 0) <= 32;
   }
   return P;
 }
@@ -747,7 +748,10 @@ static int build_replica(dk_ctx* c, const uint32_t* rowof, uint64_t npos) {
       HIPCHK(S.rgcnt.reserve(npos * 2 + 8, 0, s));
     }
     S.rgmax = op == DK_CMP_QGRAM && S.maxgrams <= kMaxReplicaGrams ? std::max(S.maxgrams, 1) : 0;
-    if (S.rgmax) HIPCHK(S.rgrams.reserve(npos * (uint64_t)S.rgmax * 8 + 64, 0, s));
+    // codes pack 16 bits per unit (+16 for the POSITIONAL index): q <= 2 fits in a u32
+    const int gram_bits = 16 * S.cfg.qgram_q + (S.cfg.qgram_tokenizer == DK_QGRAM_POSITIONAL ? 16 : 0);
+    const int rgw = gram_bits <= 32 ? 4 : 8;
+    if (S.rgmax) HIPCHK(S.rgrams.reserve(npos * (uint64_t)S.rgmax * rgw + 64, 0, s));
     ReplicaJob J{};
     J.width = W;
     J.rlmax = S.rlmax;
@@ -768,8 +772,9 @@ static int build_replica(dk_ctx* c, const uint32_t* rowof, uint64_t npos) {
     J.rgoff = S.rgoff.as<uint32_t>();
     J.rgcnt = S.rgcnt.as<uint16_t>();
     J.rgmax = S.rgmax;
+    J.rg32 = rgw == 4;
     J.grams = S.grams.as<uint64_t>();
-    J.rgrams = S.rgrams.as<uint64_t>();
+    J.rgrams = S.rgrams.p;
     HIPCHK(launch_replicate(J, rowof, npos, s));
   }
   return DK_OK;

@@ -67,9 +67,9 @@ struct DevProp {
   const uint8_t* rnumok;
   const uint32_t* rgoff;
   const uint16_t* rgcnt;
-  const uint64_t* rgrams;  // QGram: [k * rstride + g], k < rgmax (0 = read grams in place)
+  const void* rgrams;      // QGram: [k * rstride + g], k < rgmax (0 = read grams in place)
   int32_t rgmax;
-  int32_t pad2;
+  int32_t rg32;            // replica codes are u32 (every code of the property < 2^32)
 };
 
 struct ScoreParams {
@@ -151,6 +151,7 @@ struct ReplicaJob {
   int32_t has_num;
   int32_t has_qgram;
   int32_t rgmax;      // QGram replica rows (0: none)
+  int32_t rg32;       // u32 replica codes
   uint64_t stride;    // replica positions
   const uint32_t* off;
   const uint16_t* len;
@@ -166,7 +167,7 @@ struct ReplicaJob {
   uint32_t* rgoff;
   uint16_t* rgcnt;
   const uint64_t* grams;
-  uint64_t* rgrams;
+  void* rgrams;
 };
 
 // ---- launchers (dk_kernels.hip) ----

@@ -644,8 +644,9 @@ __device__ __forceinline__ uint32_t gram_hash(uint64_t code, int lt) {
   return (((uint32_t)code ^ (uint32_t)(code >> 32)) * 0x9E3779B1u) >> (32 - lt);
 }
 
+template <typename GT>
 __device__ __forceinline__ int qgram_common_hashed(uint64_t* tab, const uint64_t* __restrict__ g1, int m1,
-                                                   const uint64_t* __restrict__ g2, uint64_t gstride,
+                                                   const GT* __restrict__ g2, uint64_t gstride,
                                                    int gmax, int m2) {
   const int lt = m1 <= 32 ? 6 : (m1 <= 64 ? 7 : 8);
   const uint32_t tmask = (1u << lt) - 1u;
@@ -662,10 +663,10 @@ __device__ __forceinline__ int qgram_common_hashed(uint64_t* tab, const uint64_t
   constexpr int CH = 8;
   uint64_t cur[CH], nxt[CH];
 #pragma unroll
-  for (int u = 0; u < CH; ++u) cur[u] = g2[(uint64_t)min(u, gmax) * gstride];
+  for (int u = 0; u < CH; ++u) cur[u] = (uint64_t)g2[(uint64_t)min(u, gmax) * gstride];
   for (int k0 = 0; k0 < m2; k0 += CH) {
 #pragma unroll
-    for (int u = 0; u < CH; ++u) nxt[u] = g2[(uint64_t)min(k0 + CH + u, gmax) * gstride];
+    for (int u = 0; u < CH; ++u) nxt[u] = (uint64_t)g2[(uint64_t)min(k0 + CH + u, gmax) * gstride];
     // first probes of the chunk issued together (one LDS latency for 8 grams); a slot
     // holding another gram sends that gram down its probe sequence
     uint32_t h[CH];
@@ -776,9 +777,12 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
         sim = same ? 1.0 : 0.0;
         const int m2 = cmp && !same ? (int)D.rgcnt[g] : 0;
         // candidate codes: the transposed replica (coalesced), or in place
-        const int common = D.rgmax
-            ? qgram_common_hashed(peq, g1, m1, D.rgrams + g, rstride, D.rgmax - 1, m2)
-            : qgram_common_hashed(peq, g1, m1, D.grams + D.rgoff[g], 1, max(m2 - 1, 0), m2);
+        const int common =
+            !D.rgmax ? qgram_common_hashed(peq, g1, m1, D.grams + D.rgoff[g], 1, max(m2 - 1, 0), m2)
+            : D.rg32 ? qgram_common_hashed(peq, g1, m1, reinterpret_cast<const uint32_t*>(D.rgrams) + g,
+                                           rstride, D.rgmax - 1, m2)
+                     : qgram_common_hashed(peq, g1, m1, reinterpret_cast<const uint64_t*>(D.rgrams) + g,
+                                           rstride, D.rgmax - 1, m2);
         if (m2 > 0) sim = qgram_formula(common, m1, m2, D.formula);
       } else if (cmp) {
         if (same) {
@@ -1056,7 +1060,13 @@ __global__ __launch_bounds__(256) void k_replicate(const ReplicaJob J, const uin
     if (J.rgmax) {  // codes transposed: the 64 lanes of a score wave read row k as 512 B
       const uint64_t* src = J.grams + J.goff[row];
       const int m = l == (int)kMissing ? 0 : (int)J.gcnt[row];
-      for (int k = 0; k < J.rgmax; ++k) J.rgrams[(uint64_t)k * J.stride + g] = k < m ? src[k] : 0ull;
+      if (J.rg32) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(J.rgrams);
+        for (int k = 0; k < J.rgmax; ++k) dst[(uint64_t)k * J.stride + g] = k < m ? (uint32_t)src[k] : 0u;
+      } else {
+        uint64_t* dst = reinterpret_cast<uint64_t*>(J.rgrams);
+        for (int k = 0; k < J.rgmax; ++k) dst[(uint64_t)k * J.stride + g] = k < m ? src[k] : 0ull;
+      }
     }
   }
 }
