@@ -17,6 +17,10 @@
 
 #include "dk_internal.h"
 
+#ifndef DK_WAVES_SHORT
+#define DK_WAVES_SHORT 5  // k_score waves per SIMD up to 40 Levenshtein rows
+#endif
+
 namespace dk {
 
 struct RowKeys {
@@ -957,7 +961,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
 // latency-bound: 5 waves/SIMD up to 40 rows, 4 above); the long-value variants (LR > 0)
 // carry the systolic DP's f64 rows and take what the register allocator needs.
 template <int RMAX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? 5 : 4, 8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? DK_WAVES_SHORT : 4, 8)))
 void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
   score_body<RMAX, 0>(P, S, slot0, nslots, out);
 }
