@@ -155,6 +155,13 @@ typedef struct dk_ctx dk_ctx;
 int dk_create(const dk_schema* schema, int device, dk_ctx** out);
 void dk_destroy(dk_ctx* ctx);
 int dk_upsert(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
+/* IncrementalLuceneDatabase.setIndexingIsDisabled(true) (IncrementalLuceneDatabase.java:95,
+ * 498-512) as the httptransform endpoint uses it (App.java:1130-1132): appends the batch as
+ * query-only rows -- dk_match accepts them as queries, they are never candidates and do not
+ * supersede the indexed version of their ID.  Normal dk_upsert is refused (DK_E_STATE)
+ * until dk_drop_transient removes them again (App.java:1174-1175, indexing re-enabled). */
+int dk_upsert_transient(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
+int dk_drop_transient(dk_ctx* ctx);
 int dk_match(dk_ctx* ctx, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out);
 /* device-to-device copy of a result's entries (any of the pointers may be NULL); the
  * destination buffers live on the ctx's device */

@@ -279,6 +279,12 @@ struct dk_ctx {
   std::unordered_map<uint64_t, uint32_t> ident_row;
   std::vector<std::unordered_map<std::u16string, uint64_t>> intern;
   int key_style = 0;  // 0 unset, 1 u64 keys, 2 interned strings
+  // transient rows (dk_upsert_transient): the newest rows from transient_row0 on; the
+  // arena fills at that point, restored by dk_drop_transient
+  bool transient = false;
+  uint64_t transient_row0 = 0;
+  struct ArenaMark { uint64_t units, grams; int maxlen, maxgrams; };
+  std::vector<ArenaMark> transient_mark;
   // match scratch
   DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], rowof, sgroup[kMaxKeys];
   const uint32_t* rowof_p = nullptr;  // replica position -> row (rowof, or usable in ALLPAIRS)
@@ -548,8 +554,10 @@ static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, 
   return DK_OK;
 }
 
-int dk_upsert(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
+static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool transient) {
   if (!c || !b) return fail(DK_E_INVALID, "NULL argument");
+  if (!transient && c->transient)
+    return fail(DK_E_STATE, "transient rows present: dk_drop_transient before indexing");
   if (b->n == 0) return DK_OK;
   if (!b->ident) return fail(DK_E_INVALID, "batch.ident is NULL");
   if (c->schema.nprops > 0 && !b->columns) return fail(DK_E_INVALID, "batch.columns is NULL");
@@ -570,11 +578,17 @@ int dk_upsert(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
   const uint64_t n = b->n, row0 = c->nrows;
   HIPCHK(grow_rows(c, row0 + n));
   hipStream_t s = c->stream;
+  if (transient && !c->transient) {
+    c->transient_row0 = row0;
+    c->transient_mark.clear();
+    for (auto& p : c->P) c->transient_mark.push_back({p.units_used, p.grams_used, p.maxlen, p.maxgrams});
+  }
 
-  // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517)
-  std::vector<uint8_t> flags(n);
+  // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517);
+  // transient rows are neither alive (never candidates) nor entered in the ID map
+  std::vector<uint8_t> flags(n, 0);
   std::vector<uint32_t> dead;
-  for (uint64_t i = 0; i < n; ++i) {
+  for (uint64_t i = 0; i < n && !transient; ++i) {
     flags[i] = kAlive | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
     auto it = c->ident_row.find(b->ident[i]);
     if (it != c->ident_row.end()) {
@@ -630,8 +644,37 @@ int dk_upsert(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
   }
   HIPCHK(hipStreamSynchronize(s));
   c->nrows += n;
+  if (transient) c->transient = true;
   if (rows_out)
     for (uint64_t i = 0; i < n; ++i) rows_out[i] = (uint32_t)(row0 + i);
+  return DK_OK;
+}
+
+int dk_upsert(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
+  return upsert_rows(c, b, rows_out, false);
+}
+
+// IncrementalLuceneDatabase.setIndexingIsDisabled(true) (:95-96, :498-512) around the
+// httptransform batch (App.java:1130-1132, 1174-1175): the batch is matched against the
+// index without entering it.
+int dk_upsert_transient(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
+  return upsert_rows(c, b, rows_out, true);
+}
+
+int dk_drop_transient(dk_ctx* c) {
+  if (!c) return fail(DK_E_INVALID, "NULL argument");
+  if (!c->transient) return DK_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->nrows = c->transient_row0;
+  for (size_t p = 0; p < c->P.size(); ++p) {
+    const auto& m = c->transient_mark[p];
+    c->P[p].units_used = m.units;
+    c->P[p].grams_used = m.grams;
+    c->P[p].maxlen = m.maxlen;
+    c->P[p].maxgrams = m.maxgrams;
+  }
+  c->transient = false;
   return DK_OK;
 }
 

@@ -25,7 +25,8 @@ KIND_MATCH, KIND_MAYBE = 1, 2
 
 MATCH_HOST, MATCH_DEVICE = 0, 1
 
-EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_match", "dk_result_copy_to_device",
+EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
+           "dk_match", "dk_result_copy_to_device",
            "dk_free_result",
            "dk_compare_rows", "dk_num_rows", "dk_set_profiling", "dk_get_profile",
            "dk_reset_profile", "dk_last_error", "dk_abi_version")
@@ -94,6 +95,8 @@ def load():
     L.dk_destroy.argtypes = [vp]
     L.dk_destroy.restype = None
     L.dk_upsert.argtypes = [vp, C.POINTER(dk_batch), vp]
+    L.dk_upsert_transient.argtypes = [vp, C.POINTER(dk_batch), vp]
+    L.dk_drop_transient.argtypes = [vp]
     L.dk_match.argtypes = [vp, vp, C.c_uint64, C.c_int, C.POINTER(C.POINTER(dk_result))]
     L.dk_result_copy_to_device.argtypes = [C.POINTER(dk_result), vp, vp, vp, vp]
     L.dk_result_copy_to_device.restype = C.c_int

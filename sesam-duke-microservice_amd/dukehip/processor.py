@@ -135,9 +135,11 @@ class GpuEngine:
     def num_rows(self):
         return int(self.lib.dk_num_rows(self.ctx))
 
-    def upsert(self, n, ident, columns, group=None, deleted=None, keys=None, key_columns=None):
+    def upsert(self, n, ident, columns, group=None, deleted=None, keys=None, key_columns=None,
+               transient=False):
         """columns: list of A.Column (schema order); keys: uint64 array [nkeys, n] or
-        key_columns: list of A.Column.  Returns the assigned rows."""
+        key_columns: list of A.Column.  Returns the assigned rows.  transient=True appends
+        query-only rows (dk_upsert_transient) that :meth:`drop_transient` removes."""
         ident = np.ascontiguousarray(ident, dtype=np.uint64)
         group = None if group is None else np.ascontiguousarray(group, dtype=np.uint8)
         deleted = None if deleted is None else np.ascontiguousarray(deleted, dtype=np.uint8)
@@ -151,8 +153,12 @@ class GpuEngine:
             kc = (A.dk_column * max(1, len(key_columns)))(*[c.c() for c in key_columns])
         b = A.dk_batch(n, ident.ctypes.data, A.ptr(group), A.ptr(deleted), cols, kptr, kc)
         rows = np.zeros(max(1, n), dtype=np.uint32)
-        A.check(self.lib.dk_upsert(self.ctx, C.byref(b), rows.ctypes.data))
+        fn = self.lib.dk_upsert_transient if transient else self.lib.dk_upsert
+        A.check(fn(self.ctx, C.byref(b), rows.ctypes.data))
         return rows[:n]
+
+    def drop_transient(self):
+        A.check(self.lib.dk_drop_transient(self.ctx))
 
     def match(self, query_rows, on_device=False):
         q = np.ascontiguousarray(query_rows, dtype=np.uint32)
@@ -199,8 +205,18 @@ class GpuBlockingDatabase:
         self.by_id = {}         # ID -> row of the live version
         self._ident = {}        # ID string -> dense identity number
         self.overwrite = False
+        self.indexing_disabled = False
+        self._transient_row0 = None
 
     # --- Database API (IncrementalLuceneDatabase.java) ---
+    def set_indexing_is_disabled(self, disabled):
+        """IncrementalLuceneDatabase.setIndexingIsDisabled (:95): while disabled, index()
+        is a no-op (:499-502) and a processed batch is matched without entering the
+        index (App.java:1130-1132, the httptransform endpoint)."""
+        self.indexing_disabled = bool(disabled)
+        if not self.indexing_disabled:
+            self.drop_transient()
+
     def set_overwrite(self, overwrite):
         self.overwrite = bool(overwrite)
 
@@ -208,6 +224,8 @@ class GpuBlockingDatabase:
         return True
 
     def index(self, record: Record):
+        if self.indexing_disabled:
+            return
         self.pending.append(record)
 
     def commit(self):
@@ -221,8 +239,18 @@ class GpuBlockingDatabase:
     def close(self):
         self.engine.close()
 
+    def drop_transient(self):
+        """Removes the query-only rows of a batch processed with indexing disabled."""
+        if self._transient_row0 is not None:
+            self.engine.drop_transient()
+            del self.rows[self._transient_row0:]
+            self._transient_row0 = None
+
     # --- bulk path ---
-    def index_batch(self, records):
+    def index_batch(self, records, transient=None):
+        """Column-packs and upserts `records`; with indexing disabled (or transient=True)
+        they become query-only rows instead.  Returns their rows."""
+        transient = self.indexing_disabled if transient is None else bool(transient)
         n = len(records)
         if n == 0:
             return np.zeros(0, np.uint32)
@@ -252,10 +280,13 @@ class GpuBlockingDatabase:
             key_cols = [A.Column.from_strings([kf.make_key(r) for r in records])
                         for kf in self.key_functions]
         rows = self.engine.upsert(n, ident, cols, group=group, deleted=deleted,
-                                  key_columns=key_cols)
+                                  key_columns=key_cols, transient=transient)
+        if transient and self._transient_row0 is None:
+            self._transient_row0 = len(self.rows)
         for r, row in zip(records, rows):
             self.rows.append(r)
-            self.by_id[r.get_value(ID_PROPERTY)] = int(row)
+            if not transient:
+                self.by_id[r.get_value(ID_PROPERTY)] = int(row)
         return rows
 
 
@@ -296,6 +327,8 @@ class GpuProcessor:
         self._replay(records, res)
         for l in self.listeners:
             l.batch_done()
+        if self.database.indexing_disabled:
+            self.database.drop_transient()   # the batch never entered the index
         return res
 
     def _replay(self, records, res: MatchResult):

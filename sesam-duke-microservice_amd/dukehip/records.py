@@ -57,10 +57,16 @@ def _gson_as_string(el):
     return str(el)
 
 
+class JsonNumber(str):
+    """A JSON number kept as its source text (Gson's LazilyParsedNumber): getAsString and
+    re-serialisation both give the literal back unchanged."""
+    __slots__ = ()
+
+
 def parse_entities(body: str):
     """POST body -> (entities, single_entity) like App.java:955-965: an array, or one object.
     Numbers keep their JSON text (Gson's LazilyParsedNumber.toString)."""
-    doc = json.loads(body, parse_float=str, parse_int=str)
+    doc = json.loads(body, parse_float=JsonNumber, parse_int=JsonNumber)
     if isinstance(doc, list):
         return doc, False
     return [doc], True

@@ -356,3 +356,81 @@ def test_unsupported_value_length(cmp):
     with pytest.raises(dh.DukeHipError):
         eng.upsert(1, [1], [dh.Column.from_strings(["x" * 257])], key_columns=[dh.Column.from_strings(["k"])])
     eng.close()
+
+
+def test_transient_rows_httptransform_mode():
+    """dk_upsert_transient (setIndexingIsDisabled(true), App.java:1130-1132): the batch is
+    matched against the index without entering it, then dropped; the index is unchanged."""
+    p, props, vals, keys = persons_case(900, 300, 12)
+    n = len(vals[0])
+    n1, m = 800, n - 800
+    group = np.where(np.arange(n) % 2 == 0, 1, 2).astype(np.uint8)
+    ident = np.arange(n, dtype=np.uint64)
+    ident[n1:n1 + 40] = ident[:40]        # posted again: isSameAs skips the indexed version
+    eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "linkage", len(keys)))
+
+    def up(a, b, transient=False):
+        return eng.upsert(b - a, ident[a:b], [dh.Column.from_strings(v[a:b]) for v in vals],
+                          group=group[a:b], key_columns=[dh.Column.from_strings(k[a:b]) for k in keys],
+                          transient=transient)
+
+    up(0, n1)
+    rows = up(n1, n, transient=True)
+    assert list(rows) == list(range(n1, n))
+    with pytest.raises(dh.DukeHipError):
+        up(0, 10)                         # indexing refused while transient rows exist
+    res = eng.match(rows)
+    alive = np.r_[np.ones(n1, np.uint8), np.zeros(m, np.uint8)]
+    ot = O.OracleTable(props, vals, keys=list(keys), ident=ident, group=group, alive=alive,
+                       threshold=0.9, maybe=0.7, mode="linkage")
+    ref = ot.match(rows)
+    assert res.n > 0
+    assert_same(res, ref)
+    res.close()
+    # queries from the index itself never see the transient rows
+    q = np.arange(0, n1, 7, dtype=np.uint32)
+    assert_same(eng.match(q), ot.match(q))
+    eng.drop_transient()
+    assert eng.num_rows == n1
+    # the arenas are reused: a normal batch after the drop scores like a fresh index
+    up(n1, n)
+    alive2 = np.ones(n, np.uint8)
+    alive2[:40] = 0                       # superseded by the re-posted IDs
+    ot2 = O.OracleTable(props, vals, keys=list(keys), ident=ident, group=group, alive=alive2,
+                        threshold=0.9, maybe=0.7, mode="linkage")
+    q = np.arange(n, dtype=np.uint32)
+    assert_same(eng.match(q), ot2.match(q))
+    eng.close()
+
+
+def test_httptransform_duke_links_bulk_equals_listener():
+    """GpuProcessor with indexing disabled -> entity_links from the match arrays equals
+    BaseLinkDatabaseMatchListener's per-callback map; the index is left unchanged."""
+    from dukehip import links as L
+    from dukehip.config import DataSource, DataSourceColumn
+    cfg = dh.DukeConfig([dh.Property("NAME", dh.Comparator("no.priv.garshol.duke.comparators.JaroWinkler"), 0.1, 0.95),
+                         dh.Property("ADDRESS", dh.Comparator("no.priv.garshol.duke.comparators.Levenshtein"), 0.2, 0.8)],
+                        threshold=0.85, maybe_threshold=0.6, linkage=True)
+    p = synth.persons(300, 150, seed=21)
+    n = len(p["name"])
+    ents = [{"_id": str(i), "name": p["name"][i], "address": p["address"][i], "extra": None}
+            for i in range(n)]
+    cols = [DataSourceColumn("name", "NAME", None), DataSourceColumn("address", "ADDRESS", None)]
+    src1 = DataSource("crm", cols, 1)
+    src2 = DataSource("erp", cols, 2)
+    db = dh.GpuBlockingDatabase(cfg, [dh.PartsKey(("NAME", None, 0, 2))])
+    proc = dh.GpuProcessor(cfg, db)
+    proc.deduplicate(dh.records_from_entities(ents[:300], src1))
+    before = db.engine.num_rows
+    lis = L.EntityLinksListener()
+    proc.add_match_listener(lis)
+    db.set_indexing_is_disabled(True)
+    recs = dh.records_from_entities(ents[300:], src2)
+    res = proc.deduplicate(recs)
+    db.set_indexing_is_disabled(False)
+    assert db.engine.num_rows == before and len(db.rows) == before
+    bulk = L.entity_links(res, recs, db.rows)
+    assert bulk == lis.links() and len(bulk) > 0
+    body = L.http_transform_response(ents[300:], False, bulk)
+    assert '"duke_links":[{"datasetId":"crm"' in body and '"extra"' not in body
+    db.close()
