@@ -86,10 +86,11 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise DukeHipError(DK_E_STATE, f"{LIB_PATH} not built: run `make -C "
+    path = os.environ.get("DUKEHIP_LIB") or LIB_PATH   # A/B builds (`make -C csrc variant`)
+    if not os.path.exists(path):
+        raise DukeHipError(DK_E_STATE, f"{path} not built: run `make -C "
                            f"{os.path.join(PKG_DIR, 'csrc')}` or __graft_entry__.build()")
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp = C.c_void_p
     L.dk_create.argtypes = [C.POINTER(dk_schema), C.c_int, C.POINTER(vp)]
     L.dk_destroy.argtypes = [vp]
