@@ -50,6 +50,7 @@ __global__ __launch_bounds__(256) void k(unsigned* out, int iters, unsigned a, u
         if constexpr (K == 27) asm volatile("v_add_u16 %0, %0, %1" : "+v"(x[i]) : "v"(y), "v"(z) : "vcc");
         if constexpr (K == 28) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(x[i]) : "v"(y), "v"(z) : "vcc");
         if constexpr (K == 29) asm volatile("v_cmp_lt_u32 vcc, %0, %1" : "+v"(x[i]) : "v"(y), "v"(z) : "vcc");
+        if constexpr (K == 30) asm volatile("v_pk_minimum3_f16 %0, %0, %1, %2" : "+v"(x[i]) : "v"(y), "v"(z) : "vcc");
       }
     }
   }
@@ -131,6 +132,7 @@ int main() {
   run("add_i16", k<27>, b8, 1000, 128, d);
   run("or3", k<28>, b8, 1000, 128, d);
   run("cmp_lt", k<29>, b8, 1000, 128, d);
+  run("pk_minimum3_f16", k<30>, b8, 1000, 128, d);
   for (int w : {1, 2, 4, 8}) {
     char nm[32];
     snprintf(nm, sizeof nm, "dep min3 w%d", w);

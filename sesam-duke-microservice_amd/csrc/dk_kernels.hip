@@ -238,9 +238,133 @@ __device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1,
   return L.result;
 }
 
+// ------------------------------------------------------------------------------------
+// The same DP with two rows per VGPR.  The column is split into a top half (rows 1..H)
+// and a bottom half (rows H+1..2H), the bottom half running one column behind: at step t
+// the register of pair i holds (lo) top row i of column t and (hi) bottom row H+i of
+// column t-1.  The two halves of a register are then independent, so one packed 3-way
+// min + one 32-bit add (values < 2^15, no carry crosses the halves) computes two cells.
+// Bottom row H+1 reads top row H of columns t-1 / t-2 (kept from earlier steps).
+//
+// Values are biased by B = 0x4000 - (maxdist + 1): a cell exceeds Duke's maxdist exactly
+// when its bit 14 is set (values stay below 0x7000), so the cutoff test "column minimum > maxdist" is an AND of the
+// column's cells (v_bitop3), not a min chain.  The test of column t-1 reads the top half's
+// AND from step t-1 and the bottom half's from step t.
+//
+// Outcome contract: when the cutoff fires this returns maxdist + 1 rather than Duke's
+// column minimum.  Both exceed min(n1, n2) / 2, so Levenshtein.compare's similarity is
+// < 0.5 either way and PropertyImpl maps the pair to `low` (the distance itself is never
+// reported).  Likewise the last column's cutoff is not tested: a cut-off value and
+// D(n1, n2-1) are then both > maxdist.
+//
+// Boundaries (Duke's virtual first row / first column, re-indexed): D(0, t) = t + 1,
+// D(i, -1) = i.  Before step 0 the registers hold top column -1 (D(i,-1) = i) and an
+// all-BIG bottom "column -2"; bottom's step-0 costs are all 1, which turns that into
+// D(H+i, -1) = H + i.
+// ------------------------------------------------------------------------------------
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(us2, a),
+                                                                __builtin_bit_cast(us2, b)));
+}
+
+// min of three packed pairs.  Default: one v_pk_minimum3_f16 — every DP value is kept in
+// [0x3F00, 0x7000], positive normal half floats, whose order is their bit patterns' order
+// (no NaN, infinity, denormal or sign bit can occur), so the f16 minimum is the u16 minimum.
+__device__ __forceinline__ uint32_t pk_min3_u16(uint32_t a, uint32_t b, uint32_t c) {
+#ifdef DK_LEV_PKMIN
+  return pk_min_u16(a, pk_min_u16(b, c));
+#else
+  uint32_t r;
+  asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#endif
+}
+
+template <int R, typename CT>
+__device__ __forceinline__ int compact_distance_pk(const uint64_t* peq, int n1, const Str<CT>& s2,
+                                                   int n2, bool act) {
+  constexpr int UPW = Str<CT>::UPW;
+  constexpr int H = R / 2;
+  constexpr int TAIL = R <= 32 ? 4 : 8;  // rows past n1 lie in (R - TAIL, R]
+  constexpr int NC = (H + 15) / 16;      // cost words
+  constexpr uint32_t BIG = 0x7000u;
+  const int maxdist = min(n1, n2) >> 1;
+  const uint32_t B = 0x4000u - (uint32_t)(maxdist + 1);
+  uint32_t P[H + 1];
+#pragma unroll
+  for (int i = 1; i <= H; ++i) P[i] = ((uint32_t)i + B) | (BIG << 16);
+  // the cutoff AND skips rows past n1 (wave-uniform: scalar masks)
+  uint32_t tm[H + 1];
+#pragma unroll
+  for (int i = 1; i <= H; ++i)
+    tm[i] = (i > n1 ? 0x4000u : 0u) | (H + i > n1 ? 0x40000000u : 0u);
+  const bool bottom_result = n1 > H;
+  int result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
+  bool live = act && n2 > 1;
+  const int fin = n2 - 1 + (bottom_result ? 1 : 0);  // step at which D(n1, n2-1) is known
+
+  uint32_t w = act ? s2.word(0) : 0u;
+  uint32_t wn = s2.word_any(1);
+  uint64_t ne_cur = ~peq_eq<CT>(peq, Str<CT>::unit(w, 0));
+  uint64_t ne_prev = ~0ull;
+  uint32_t h1 = 0, h2 = BIG;  // top row H of columns t-1, t-2 (h1 is read from P[H])
+  uint32_t acc_prev = 0;
+  for (int t = 0; live; ++t) {
+    const int tn = t + 1;
+    if (tn % UPW == 0) {
+      w = wn;
+      wn = s2.word_any(tn / UPW + 1);
+    }
+    const uint64_t ne_nx = ~peq_eq<CT>(peq, Str<CT>::unit(w, tn % UPW));
+    uint32_t C[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      C[c] = ((uint32_t)(ne_cur >> (16 * c)) & 0xFFFFu) | ((uint32_t)(ne_prev >> (H + 16 * c)) << 16);
+    h1 = P[H] & 0xFFFFu;
+    uint32_t above = ((uint32_t)t + 1u + B) | (h1 << 16);
+    uint32_t diag = ((uint32_t)t + B) | (h2 << 16);
+    uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 1; i <= H; ++i) {
+      const uint32_t cost = (C[(i - 1) >> 4] >> ((i - 1) & 15)) & 0x10001u;
+      const uint32_t left = P[i];
+      const uint32_t v = pk_min3_u16(above, diag, left) + cost;
+      diag = left;
+      P[i] = v;
+      above = v;
+      if (H + i > R - TAIL) acc &= v | tm[i];
+      else acc &= v;
+    }
+    h2 = h1;
+    if (t >= 2 && (acc_prev & acc & 0x40004000u) == 0x40004000u) {  // column t-1 cut off
+      result = maxdist + 1;
+      live = false;
+    } else if (t == fin) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int row = R - TAIL + 1; row <= R; ++row)
+        if (row == n1) r = row <= H ? (P[row] & 0xFFFFu) : (P[row - H] >> 16);
+      result = (int)(r - B);
+      live = false;
+    }
+    acc_prev = acc;
+    ne_prev = ne_cur;
+    ne_cur = ne_nx;
+  }
+  return result;
+}
+
 // [Duke 1.2] comparators.Levenshtein.compare.  RMAX: the largest row bucket this kernel
 // variant instantiates (the host picks the variant from the longest Levenshtein value),
 // which bounds the VGPRs of the whole fused kernel and so its occupancy.
+#ifdef DK_LEV_SCALAR
+#define DK_LEV_DP compact_distance_peq
+#else
+#define DK_LEV_DP compact_distance_pk
+#endif
+
 template <int RMAX, typename CT>
 __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str<CT>& s1, int n1,
                                                   const Str<CT>& s2, int n2, bool act) {
@@ -257,18 +381,18 @@ __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str
   // row buckets of 4 up to 32 rows, of 8 above (n1 is wave-uniform: a scalar switch)
   int d;
   switch ((n1 + 3) >> 2) {
-    case 1: d = compact_distance_peq<4>(peq, n1, s2, n2, run); break;
-    case 2: d = compact_distance_peq<8>(peq, n1, s2, n2, run); break;
-    case 3: d = compact_distance_peq<12>(peq, n1, s2, n2, run); break;
-    case 4: d = compact_distance_peq<16>(peq, n1, s2, n2, run); break;
-    case 5: d = compact_distance_peq<20>(peq, n1, s2, n2, run); break;
-    case 6: d = compact_distance_peq<24>(peq, n1, s2, n2, run); break;
-    case 7: d = compact_distance_peq<28>(peq, n1, s2, n2, run); break;
-    case 8: d = compact_distance_peq<32>(peq, n1, s2, n2, run); break;
-    case 9: case 10: d = compact_distance_peq<(RMAX < 40 ? 4 : 40)>(peq, n1, s2, n2, run); break;
-    case 11: case 12: d = compact_distance_peq<(RMAX < 48 ? 4 : 48)>(peq, n1, s2, n2, run); break;
-    case 13: case 14: d = compact_distance_peq<(RMAX < 56 ? 4 : 56)>(peq, n1, s2, n2, run); break;
-    default: d = compact_distance_peq<(RMAX < 64 ? 4 : 64)>(peq, n1, s2, n2, run); break;
+    case 1: d = DK_LEV_DP<4>(peq, n1, s2, n2, run); break;
+    case 2: d = DK_LEV_DP<8>(peq, n1, s2, n2, run); break;
+    case 3: d = DK_LEV_DP<12>(peq, n1, s2, n2, run); break;
+    case 4: d = DK_LEV_DP<16>(peq, n1, s2, n2, run); break;
+    case 5: d = DK_LEV_DP<20>(peq, n1, s2, n2, run); break;
+    case 6: d = DK_LEV_DP<24>(peq, n1, s2, n2, run); break;
+    case 7: d = DK_LEV_DP<28>(peq, n1, s2, n2, run); break;
+    case 8: d = DK_LEV_DP<32>(peq, n1, s2, n2, run); break;
+    case 9: case 10: d = DK_LEV_DP<(RMAX < 40 ? 4 : 40)>(peq, n1, s2, n2, run); break;
+    case 11: case 12: d = DK_LEV_DP<(RMAX < 48 ? 4 : 48)>(peq, n1, s2, n2, run); break;
+    case 13: case 14: d = DK_LEV_DP<(RMAX < 56 ? 4 : 56)>(peq, n1, s2, n2, run); break;
+    default: d = DK_LEV_DP<(RMAX < 64 ? 4 : 64)>(peq, n1, s2, n2, run); break;
   }
   if (run) {
     const int dist = min(d, len);
