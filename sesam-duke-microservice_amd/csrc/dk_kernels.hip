@@ -17,6 +17,9 @@
 
 #include "dk_internal.h"
 
+#ifndef DK_JW_NARROW
+#define DK_JW_NARROW 32  // JaroWinkler on 32-bit position masks up to this query length
+#endif
 #ifndef DK_WAVES_SHORT
 #define DK_WAVES_SHORT 5  // k_score waves per SIMD up to 40 Levenshtein rows
 #endif
@@ -667,12 +670,37 @@ __device__ __forceinline__ double jarowinkler(Str<CT> s1, int n1, Str<CT> s2, in
 //    matched row did) then comes bit-parallel: each plane's bit is carried from one
 //    matched row to the next by an add through the unmatched rows between them, and a
 //    bit-sliced compare of the two 6-bit steps counts the descents.
-__device__ __forceinline__ uint64_t carry_to_next(uint64_t plane, uint64_t found) {
+template <typename MT>
+__device__ __forceinline__ MT carry_to_next(MT plane, MT found) {
   // bit i of the result = bit of `plane` at the matched row before matched row i
   return (((plane & found) << 1) + ~found) & found;
 }
 
-template <typename CT>
+// Peq lookups and window masks at the width of the query's position masks: 32 bits when
+// the query value has <= 32 units (wave-uniform), which halves the mask arithmetic and
+// reads only the low half of each 64-bit Peq entry.
+template <typename MT, typename CT>
+__device__ __forceinline__ MT peq_eq_t(const uint64_t* peq, uint32_t x) {
+  if (sizeof(MT) == 8) return (MT)peq_eq<CT>(peq, x);
+  const uint32_t* p32 = reinterpret_cast<const uint32_t*>(peq);  // little-endian low halves
+  if (sizeof(CT) == 1) return (MT)p32[2 * x];
+  return (MT)(p32[2 * (x & 0xFF)] & p32[2 * (256 + (x >> 8))]);
+}
+
+template <typename MT>
+__device__ __forceinline__ MT range_mask_t(int lo, int hi) {  // bits [lo, hi), 0<=lo<=hi<=width
+  if (sizeof(MT) == 8) return (MT)range_mask(lo, hi);
+  const uint32_t up = hi >= 32 ? ~0u : ((1u << hi) - 1u);
+  const uint32_t dn = lo >= 32 ? ~0u : ((1u << lo) - 1u);
+  return (MT)(up & ~dn);
+}
+
+template <typename MT>
+__device__ __forceinline__ int popc_t(MT m) {
+  return sizeof(MT) == 8 ? __popcll((uint64_t)m) : __popc((uint32_t)m);
+}
+
+template <typename MT, typename CT>
 __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str<CT>& qs, int nq,
                                                   const Str<CT>& cs, int nc, bool act) {
   if (act && str_equal(qs, nq, cs, nc)) act = false;  // 1.0 below
@@ -683,7 +711,7 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
   const int md = rows_cand ? (nq >> 1) : (nc >> 1);
   const int lo_off = rows_cand ? -md : 1 - md, hi_off = rows_cand ? md : md + 1;
   int c = 0, t = 0, prev = -1;
-  uint64_t found = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
+  MT found = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
   const int maxn = act ? nc : 0;
   int wmax = maxn;
   for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
@@ -693,18 +721,19 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
 #pragma unroll
     for (int u = 0; u < UPW; ++u) {
       const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
-      uint64_t e = 0;
+      MT e = 0;
       if (j < maxn)
-        e = peq_eq<CT>(peq, Str<CT>::unit(w, u)) & range_mask(max(0, j + lo_off), min(nq, j + hi_off));
+        e = peq_eq_t<MT, CT>(peq, Str<CT>::unit(w, u)) &
+            range_mask_t<MT>(max(0, j + lo_off), min(nq, j + hi_off));
       // candidate rows: first match of row j
-      const uint64_t ec = rows_cand ? e : 0ull;
-      const int jj = ffs64(ec | (1ull << 63));
+      const MT ec = rows_cand ? e : (MT)0;
+      const int jj = ffs64((uint64_t)ec | (1ull << 63));
       const bool has = ec != 0;
       c += has ? 1 : 0;
       t += (has && prev != -1 && jj < prev) ? 1 : 0;
       prev = has ? jj : prev;
       // query rows: rows first matched at step j
-      const uint64_t m = rows_query ? (e & ~found) : 0ull;
+      const MT m = rows_query ? (MT)(e & ~found) : (MT)0;
       found |= m;
       if (j & 1) p0 |= m;
       if (j & 2) p1 |= m;
@@ -715,17 +744,17 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
     }
   }
   if (rows_query) {
-    c = __popcll(found);
+    c = popc_t(found);
     // descents p(i) < p(previous matched row), MSB-first bit-sliced compare
-    const uint64_t P[6] = {p0, p1, p2, p3, p4, p5};
-    uint64_t lt = 0, eq = ~0ull;
+    const MT P[6] = {p0, p1, p2, p3, p4, p5};
+    MT lt = 0, eq = (MT)~(MT)0;
 #pragma unroll
     for (int b = 5; b >= 0; --b) {
-      const uint64_t a = P[b], q = carry_to_next(P[b], found);
+      const MT a = P[b], q = carry_to_next<MT>(P[b], found);
       lt |= eq & ~a & q;
       eq &= ~(a ^ q);
     }
-    t = __popcll(lt & found);
+    t = popc_t<MT>(lt & found);
   }
   if (!act) return 1.0;  // equal values (inactive lanes discard the result)
   if (c == 0) return 0.0;
@@ -887,7 +916,8 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
       if (table) {
         peq_set(peq, base + D.off[q], lq, true);
         sim = D.op == DK_CMP_LEVENSHTEIN ? levenshtein_peq<RMAX>(peq, s1, lq, s2, lc, cmp)
-                                         : jarowinkler_peq(peq, s1, lq, s2, lc, cmp);
+                 : (lq <= DK_JW_NARROW ? jarowinkler_peq<uint32_t>(peq, s1, lq, s2, lc, cmp)
+                             : jarowinkler_peq<uint64_t>(peq, s1, lq, s2, lc, cmp));
         peq_set(peq, base + D.off[q], lq, false);
       } else if (cmp) {
         sim = jarowinkler(s1, lq, s2, lc);
