@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the oracle baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--gather", default="shm", choices=["shm", "rccl"],
+                    help="N>1 result gather: shm = every GPU copies its tile's list into its "
+                         "slice of one shared host mapping (rank 0 reads it in place); rccl = "
+                         "device lists gathered to GPU 0 over xGMI, then copied to the host")
     ap.add_argument("--device-results", action="store_true",
                     help="diagnostic: keep the N=1 match list in HBM (no device->host copy)")
     ap.add_argument("--only", default=None,
@@ -145,11 +149,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # DUKEHIP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a device);
+    # the driver's runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("DUKEHIP_DIST_BACKEND", "nccl")
+    if world > 1:
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    cdev = dev if backend == "nccl" else torch.device("cpu")   # where collectives run
+    if world > 1 and backend != "nccl" and args.gather == "rccl":
+        raise SystemExit("--gather rccl needs the nccl (RCCL) backend")
 
     import dukehip as dh
     from dukehip import synth
@@ -168,6 +183,16 @@ def main():
     queries = allq[q0:q1]
     nq_max = dshard.max_tile(len(allq), world)
     holder = {}
+    shared = None
+    if dist is not None and args.gather == "shm":
+        # size this rank's result region from one untimed device-mode match (the same
+        # queries every step), with headroom; the regions form one shared host mapping
+        probe = eng.match(queries, on_device=True)
+        cap = torch.tensor([probe.n], dtype=torch.int64, device=cdev)
+        probe.close()
+        dist.all_reduce(cap, op=dist.ReduceOp.MAX)
+        shared = dshard.SharedRegionGather(dist, torch, cdev, eng, nq_max,
+                                           int(cap.item() * 1.05) + 4096, world, rank)
 
     def step():
         old = holder.pop("res", None)
@@ -177,6 +202,14 @@ def main():
             res = eng.match(queries, on_device=args.device_results)  # pinned host memory
             holder["res"] = res
             return res, res.pairs_scored
+        if shared is not None:
+            # N>1, shm gather: the list goes to this rank's slice of the shared host mapping
+            # (overlapped chunk copies over this GPU's own link); the all-gather of counts
+            # completes the exchange, after which rank 0 holds the node list in place
+            res = eng.match(queries)
+            total = shared.exchange(len(queries), res.n, res.pairs_scored)
+            holder["res"] = res
+            return res, total
         # N>1: entries stay in HBM; RCCL all-gathers the per-rank counts, then gathers
         # every rank's match list (first / candidate / prob / kind) to rank 0 over xGMI,
         # which moves the node's list to the host.
@@ -186,7 +219,7 @@ def main():
             torch.cuda.synchronize()
             res.copy_to_device(first.data_ptr(), cand.data_ptr(), prob.data_ptr(), kind.data_ptr())
 
-        _, total = dshard.gather_matches(dist, torch, dev, len(queries), res.n, res.pairs_scored,
+        _, total = dshard.gather_matches(dist, torch, cdev, len(queries), res.n, res.pairs_scored,
                                          fill, world, rank, nq_max)
         holder["res"] = res
         return res, total
@@ -211,7 +244,7 @@ def main():
     eng.set_profiling(False)
     prof = eng.profile()
     if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        tt = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     ms_step = el / args.steps * 1e3
@@ -244,9 +277,11 @@ def main():
                        "pairs_per_step": pairs_step,
                        "comparators": {p["name"]: CMP_NAMES[p["comparator"]] for p in w["props"]},
                        "threshold": w["threshold"], "maybe_threshold": w["maybe"],
-                       "parallelism": f"query-tile sharding x{world}, replicated index"},
+                       "parallelism": f"query-tile sharding x{world}, replicated index"
+                                      + (f", {args.gather} result gather" if world > 1 else "")},
             "records_per_s": len(allq) / (ms_step / 1e3),
-            "matches_per_step": int(last.n) if last is not None else 0,
+            "matches_per_step": (sum(c[0] for c in shared.counts) if shared is not None
+                                 else int(last.n) if last is not None else 0),
             "index_build_s": t_index,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
@@ -260,6 +295,11 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(w, last, args)
         print(json.dumps(out), flush=True)
+    last = None
+    holder.clear()
+    if shared is not None:
+        dist.barrier()   # rank 0 is done with the lists
+        shared.close()
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

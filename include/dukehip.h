@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DK_ABI_VERSION 1
+#define DK_ABI_VERSION 2
 
 /* status codes */
 #define DK_OK 0
@@ -168,6 +168,25 @@ int dk_match(dk_ctx* ctx, const uint32_t* query_rows, uint64_t nq, int flags, dk
 int dk_result_copy_to_device(const dk_result* result, uint64_t* first, uint32_t* candidate,
                              double* prob, uint8_t* kind);
 void dk_free_result(dk_result* result);
+
+/* Caller-owned host memory for the entries of later DK_MATCH_HOST calls, instead of the
+ * library's pinned pool: e.g. this rank's slice of one node-wide shared mapping, so every
+ * GPU copies its query tile's match list over its own PCIe link into memory the listener
+ * process (rank 0) reads directly -- the multi-GPU result gather of SURVEY §8e without a
+ * second hop through one GPU (dukehip.dist).  The library registers the range with the
+ * HIP runtime (page-locks it) until the region is replaced, cleared (base NULL) or the ctx
+ * destroyed.  Layout: dk_result_region_layout.  The dk_result of a match in the region
+ * points into it and is overwritten by the next dk_match.  A match list that does not fit
+ * fails with DK_E_NOMEM; more than max_queries queries with DK_E_INVALID. */
+typedef struct dk_region_layout {
+  uint64_t capacity;         /* entries the region holds */
+  uint64_t first_offset;     /* u64 first[max_queries + 1] */
+  uint64_t prob_offset;      /* f64 prob[capacity] */
+  uint64_t candidate_offset; /* u32 candidate[capacity] */
+  uint64_t kind_offset;      /* u8 kind[capacity] */
+} dk_region_layout;
+int dk_result_region_layout(uint64_t bytes, uint64_t max_queries, dk_region_layout* out);
+int dk_set_result_region(dk_ctx* ctx, void* base, uint64_t bytes, uint64_t max_queries);
 int dk_compare_rows(dk_ctx* ctx, uint32_t r1, uint32_t r2, double* prob);
 uint64_t dk_num_rows(const dk_ctx* ctx);
 int dk_set_profiling(dk_ctx* ctx, int on);

@@ -293,6 +293,16 @@ struct dk_ctx {
   DevBuf counters, st_bcnt, st_bscored, st_bbytes, st_boff, st_prob, st_cand, st_qidx;
   PinnedBuf h_small;
   std::shared_ptr<ResultPool> pool = std::make_shared<ResultPool>();
+  // caller-owned host region for DK_MATCH_HOST entries (dk_set_result_region), registered
+  // with the HIP runtime so the chunk copies DMA straight into it
+  struct Region {
+    uint8_t* base = nullptr;
+    uint64_t bytes = 0, max_queries = 0, cap = 0;
+    uint64_t* first = nullptr;
+    double* prob = nullptr;
+    uint32_t* cand = nullptr;
+    uint8_t* kind = nullptr;
+  } region;
   // profiling (Processor.setPerformanceProfiling)
   bool profiling = false;
   dk_profile prof{};
@@ -415,6 +425,7 @@ void dk_destroy(dk_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->copy_stream);
+  if (c->region.base) (void)hipHostUnregister(c->region.base);
   hipStream_t s = c->stream, cs = c->copy_stream;
   hipEvent_t ev = c->chunk_done;
   delete c;
@@ -1012,7 +1023,20 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(),
                    B.d_qidx.as<uint32_t>()};
       HIPCHK(launch_compact(st, c->st_boff.as<uint64_t>(), nblk, nm, ml, s));
-      if (!(flags & DK_MATCH_DEVICE)) {
+      if (!(flags & DK_MATCH_DEVICE) && c->region.base) {
+        // caller region: same overlapped copies, into the registered caller memory
+        if (need > c->region.cap) {
+          (void)hipStreamSynchronize(c->copy_stream);
+          return fail(DK_E_NOMEM, "match list needs more than %llu entries; the result region "
+                      "holds %llu", (unsigned long long)need, (unsigned long long)c->region.cap);
+        }
+        HIPCHK(hipEventRecord(c->chunk_done, s));
+        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->chunk_done, 0));
+        hipStream_t cs = c->copy_stream;
+        HIPCHK(hipMemcpyAsync(c->region.cand + nm, B.d_cand.as<uint32_t>() + nm, add * 4, hipMemcpyDeviceToHost, cs));
+        HIPCHK(hipMemcpyAsync(c->region.prob + nm, B.d_prob.as<double>() + nm, add * 8, hipMemcpyDeviceToHost, cs));
+        HIPCHK(hipMemcpyAsync(c->region.kind + nm, B.d_kind.as<uint8_t>() + nm, add, hipMemcpyDeviceToHost, cs));
+      } else if (!(flags & DK_MATCH_DEVICE)) {
         // overlap: this chunk's entries go to pinned host memory on the copy stream while
         // the next chunk scores
         if (need * 8 > B.h_prob.bytes || need * 4 > B.h_cand.bytes || need > B.h_kind.bytes) {
@@ -1048,7 +1072,14 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   HIPCHK(launch_first(B.d_qidx.as<uint32_t>(), nm, nq, B.d_first.as<uint64_t>(), s));
   R->r.nqueries = nq;
   R->r.n = nm;
-  if (!(flags & DK_MATCH_DEVICE)) {
+  if (!(flags & DK_MATCH_DEVICE) && c->region.base) {
+    HIPCHK(hipStreamSynchronize(c->copy_stream));  // chunk copies landed
+    HIPCHK(hipMemcpyAsync(c->region.first, B.d_first.p, (nq + 1) * 8, hipMemcpyDeviceToHost, s));
+    R->r.first = c->region.first;
+    R->r.candidate = c->region.cand;
+    R->r.prob = c->region.prob;
+    R->r.kind = c->region.kind;
+  } else if (!(flags & DK_MATCH_DEVICE)) {
     HIPCHK(hipStreamSynchronize(c->copy_stream));  // chunk copies landed
     HIPCHK(B.h_first.reserve((nq + 1) * 8));
     HIPCHK(B.h_cand.reserve(nm * 4 + 4, nm * 4));
@@ -1077,6 +1108,9 @@ int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_r
       return fail(DK_E_INVALID, "query row %u not in the index (%llu rows)", query_rows[i],
                   (unsigned long long)c->nrows);
   if (nq >= (1ull << 32)) return fail(DK_E_UNSUPPORTED, "too many queries");
+  if (c->region.base && !(flags & DK_MATCH_DEVICE) && nq > c->region.max_queries)
+    return fail(DK_E_INVALID, "%llu queries; the result region was laid out for %llu",
+                (unsigned long long)nq, (unsigned long long)c->region.max_queries);
   HIPCHK(hipSetDevice(c->device));
   ResultHolder* R = new (std::nothrow) ResultHolder();
   if (!R) return fail(DK_E_NOMEM, "out of host memory");
@@ -1108,6 +1142,47 @@ int dk_result_copy_to_device(const dk_result* r, uint64_t* first, uint32_t* cand
     if (kind) HIPCHK(hipMemcpyAsync(kind, B.d_kind.p, r->n, hipMemcpyDeviceToDevice, s));
   }
   HIPCHK(hipStreamSynchronize(s));
+  return DK_OK;
+}
+
+int dk_result_region_layout(uint64_t bytes, uint64_t max_queries, dk_region_layout* out) {
+  if (!out) return fail(DK_E_INVALID, "out is NULL");
+  const uint64_t head = (max_queries + 1) * 8;
+  if (bytes < head) return fail(DK_E_INVALID, "region of %llu bytes cannot hold %llu queries",
+                                (unsigned long long)bytes, (unsigned long long)max_queries);
+  const uint64_t cap = (bytes - head) / 13;  // 8 (prob) + 4 (candidate) + 1 (kind) per entry
+  out->capacity = cap;
+  out->first_offset = 0;
+  out->prob_offset = head;
+  out->candidate_offset = head + cap * 8;
+  out->kind_offset = head + cap * 12;
+  return DK_OK;
+}
+
+int dk_set_result_region(dk_ctx* c, void* base, uint64_t bytes, uint64_t max_queries) {
+  if (!c) return fail(DK_E_INVALID, "ctx is NULL");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->copy_stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->region.base) {
+    (void)hipHostUnregister(c->region.base);
+    c->region = dk_ctx::Region{};
+  }
+  if (!base) return DK_OK;
+  if (reinterpret_cast<uintptr_t>(base) & 7) return fail(DK_E_INVALID, "region base not 8-byte aligned");
+  dk_region_layout L{};
+  int rc = dk_result_region_layout(bytes, max_queries, &L);
+  if (rc) return rc;
+  HIPCHK(hipHostRegister(base, bytes, hipHostRegisterDefault));
+  uint8_t* b = static_cast<uint8_t*>(base);
+  c->region.base = b;
+  c->region.bytes = bytes;
+  c->region.max_queries = max_queries;
+  c->region.cap = L.capacity;
+  c->region.first = reinterpret_cast<uint64_t*>(b + L.first_offset);
+  c->region.prob = reinterpret_cast<double*>(b + L.prob_offset);
+  c->region.cand = reinterpret_cast<uint32_t*>(b + L.candidate_offset);
+  c->region.kind = b + L.kind_offset;
   return DK_OK;
 }
 

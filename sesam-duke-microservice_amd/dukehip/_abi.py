@@ -27,7 +27,7 @@ MATCH_HOST, MATCH_DEVICE = 0, 1
 
 EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
            "dk_match", "dk_result_copy_to_device",
-           "dk_free_result",
+           "dk_free_result", "dk_result_region_layout", "dk_set_result_region",
            "dk_compare_rows", "dk_num_rows", "dk_set_profiling", "dk_get_profile",
            "dk_reset_profile", "dk_last_error", "dk_abi_version")
 
@@ -68,6 +68,12 @@ class dk_result(C.Structure):
                 ("pairs_generated", C.c_uint64)]
 
 
+class dk_region_layout(C.Structure):
+    _fields_ = [("capacity", C.c_uint64), ("first_offset", C.c_uint64),
+                ("prob_offset", C.c_uint64), ("candidate_offset", C.c_uint64),
+                ("kind_offset", C.c_uint64)]
+
+
 class dk_profile(C.Structure):
     _fields_ = [("ms_index", C.c_double), ("ms_generate", C.c_double), ("ms_score", C.c_double),
                 ("ms_gather", C.c_double), ("ms_total", C.c_double),
@@ -103,6 +109,8 @@ def load():
     L.dk_result_copy_to_device.restype = C.c_int
     L.dk_free_result.argtypes = [C.POINTER(dk_result)]
     L.dk_free_result.restype = None
+    L.dk_result_region_layout.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(dk_region_layout)]
+    L.dk_set_result_region.argtypes = [vp, vp, C.c_uint64, C.c_uint64]
     L.dk_compare_rows.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
     L.dk_num_rows.argtypes = [vp]
     L.dk_num_rows.restype = C.c_uint64
@@ -112,6 +120,7 @@ def load():
     L.dk_last_error.restype = C.c_char_p
     L.dk_abi_version.restype = C.c_int
     for f in ("dk_create", "dk_upsert", "dk_match", "dk_compare_rows", "dk_set_profiling",
+              "dk_result_region_layout", "dk_set_result_region",
               "dk_get_profile", "dk_reset_profile"):
         getattr(L, f).restype = C.c_int
     _lib = L
@@ -122,6 +131,31 @@ def check(rc):
     if rc != DK_OK:
         raise DukeHipError(rc, load().dk_last_error().decode("utf-8", "replace"))
     return rc
+
+
+def region_layout(nbytes, max_queries):
+    """dk_result_region_layout: where a result region keeps first / prob / candidate / kind."""
+    out = dk_region_layout()
+    check(load().dk_result_region_layout(int(nbytes), int(max_queries), C.byref(out)))
+    return {name: int(getattr(out, name)) for name, _ in out._fields_}
+
+
+def region_bytes(max_queries, capacity):
+    """Smallest region holding max_queries queries and `capacity` entries."""
+    return (int(max_queries) + 1) * 8 + int(capacity) * 13
+
+
+def region_views(buf, max_queries, nq, n):
+    """numpy views of a result region (any buffer, e.g. another rank's slice of a shared
+    mapping): first[nq+1], candidate[n], prob[n], kind[n]."""
+    lay = region_layout(len(buf), max_queries)
+    if n > lay["capacity"] or nq > max_queries:
+        raise ValueError("result larger than its region")
+    b = np.frombuffer(buf, dtype=np.uint8)
+    return {"first": b[:(nq + 1) * 8].view(np.uint64),
+            "candidate": b[lay["candidate_offset"]:lay["candidate_offset"] + 4 * n].view(np.uint32),
+            "prob": b[lay["prob_offset"]:lay["prob_offset"] + 8 * n].view(np.float64),
+            "kind": b[lay["kind_offset"]:lay["kind_offset"] + n]}
 
 
 def ptr(a):

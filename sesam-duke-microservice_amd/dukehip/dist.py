@@ -5,12 +5,29 @@ same batches into its own dk_ctx); query records are split into contiguous tiles
 rank, so a query's candidates, scores and decisions are computed on exactly one rank.  The
 only exchange is the result gather: all-gather the per-rank match counts, then gather
 every rank's match list (first / candidate / prob / kind) to rank 0, which owns the
-MatchListener replay.  With the "nccl" backend (RCCL on ROCm) the tensors are device
-tensors and travel over xGMI; the same code runs on CPU tensors with "gloo" (tests).
+MatchListener replay.  Two ways to move the lists:
+
+* ``SharedRegionGather`` (default): every rank's dk_match copies its tile's list over its own
+  GPU's PCIe link into its slice of ONE node-wide shared host mapping (dk_set_result_region,
+  overlapped with scoring as on one GPU); the exchange is an all-gather of the per-rank
+  counts, after which rank 0 reads the whole node list in place.  The listener runs on the
+  host, so this is the shortest path: no list crosses xGMI and then funnels through GPU 0's
+  single host link.
+* ``gather_matches``: device-resident lists gathered to GPU 0 over RCCL/xGMI, then moved to
+  the host by rank 0.  With the "nccl" backend (RCCL on ROCm) the tensors are device
+  tensors; the same code runs on CPU tensors with "gloo" (tests).
 """
 from __future__ import annotations
 
+import mmap
+import os
+import tempfile
+
 import numpy as np
+
+from . import _abi as A
+
+PAGE = mmap.PAGESIZE
 
 
 def tile(n, rank, world):
@@ -68,3 +85,70 @@ def concat_ranks(ranks):
             "candidate": np.concatenate([r["candidate"] for r in ranks]),
             "prob": np.concatenate([r["prob"] for r in ranks]),
             "kind": np.concatenate([r["kind"] for r in ranks])}
+
+
+class SharedRegionGather:
+    """Node-wide shared host mapping with one result region per rank (SURVEY §8e exchange).
+
+    Collective: every rank constructs it with the same (nq_max, capacity).  Rank 0 creates
+    the file under /dev/shm, every rank maps it and hands its page-aligned slice to its
+    engine (dk_set_result_region registers it with HIP); the file is unlinked as soon as all
+    ranks hold the mapping, so nothing is left behind.  After :meth:`exchange` of a step,
+    rank 0 reads every rank's list in place (:meth:`rank_lists`).  A rank must not start its
+    next dk_match while rank 0 still reads the previous lists (callers barrier between
+    replay and the next batch)."""
+
+    def __init__(self, dist, torch, device, engine, nq_max, capacity, world, rank,
+                 shm_dir="/dev/shm"):
+        self.dist, self.torch, self.device = dist, torch, device
+        self.world, self.rank, self.nq_max = world, rank, int(nq_max)
+        self.slice_bytes = -(-A.region_bytes(nq_max, capacity) // PAGE) * PAGE
+        total = self.slice_bytes * world
+        name = [None]
+        if rank == 0:
+            d = shm_dir if os.path.isdir(shm_dir) else None
+            fd, path = tempfile.mkstemp(prefix="dukehip_results_", dir=d)
+            os.ftruncate(fd, total)
+            os.close(fd)
+            name = [path]
+        dist.broadcast_object_list(name, src=0)
+        self.path = name[0]
+        with open(self.path, "r+b") as f:
+            self.map = mmap.mmap(f.fileno(), total)
+        dist.barrier()
+        if rank == 0:
+            os.unlink(self.path)
+        self.slices = [memoryview(self.map)[r * self.slice_bytes:(r + 1) * self.slice_bytes]
+                       for r in range(world)]
+        self.engine = engine
+        if engine is not None:
+            engine.set_result_region(self.slices[rank], self.nq_max)
+        self.counts = None
+
+    def exchange(self, nq, n, scored):
+        """All-gather of (entries, pairs scored, queries) per rank: after it every rank's
+        list is complete in the mapping.  Returns the node's pairs scored."""
+        torch = self.torch
+        cnt = torch.tensor([n, scored, nq], dtype=torch.int64, device=self.device)
+        allc = [torch.zeros_like(cnt) for _ in range(self.world)]
+        self.dist.all_gather(allc, cnt)
+        self.counts = [tuple(int(v) for v in c.cpu()) for c in allc]
+        return sum(c[1] for c in self.counts)
+
+    def rank_lists(self):
+        """Rank 0: every rank's {first, candidate, prob, kind} views, in rank (= query) order
+        (concat_ranks joins them)."""
+        return [A.region_views(self.slices[r], self.nq_max, nqr, nr)
+                for r, (nr, _, nqr) in enumerate(self.counts)]
+
+    def close(self):
+        if self.engine is not None and self.engine.ctx:
+            self.engine.set_result_region(None, 0)
+        self.engine = None
+        for mv in self.slices:
+            mv.release()
+        self.slices = []
+        try:
+            self.map.close()
+        except BufferError:  # a caller still holds views of the lists; GC unmaps
+            pass

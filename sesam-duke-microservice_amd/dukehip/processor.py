@@ -123,6 +123,7 @@ class GpuEngine:
     def close(self):
         if self.ctx:
             self.lib.dk_destroy(self.ctx)
+            self._region = None
             self.ctx = C.c_void_p()
 
     def __del__(self):
@@ -166,6 +167,18 @@ class GpuEngine:
         A.check(self.lib.dk_match(self.ctx, q.ctypes.data if q.size else None, q.size,
                                   A.MATCH_DEVICE if on_device else A.MATCH_HOST, C.byref(res)))
         return MatchResult(self.lib, res, q)
+
+    def set_result_region(self, buf, max_queries):
+        """dk_set_result_region: host-mode match lists land in `buf` (a writable buffer, e.g.
+        this rank's slice of a node-wide shared mapping) instead of the library's pool.
+        buf=None goes back to the pool.  The engine keeps a reference to `buf`."""
+        if buf is None:
+            A.check(self.lib.dk_set_result_region(self.ctx, None, 0, 0))
+            self._region = None
+            return
+        arr = np.frombuffer(buf, dtype=np.uint8)
+        A.check(self.lib.dk_set_result_region(self.ctx, arr.ctypes.data, arr.size, int(max_queries)))
+        self._region = (buf, arr)
 
     def compare_rows(self, r1, r2):
         out = C.c_double()

@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
 
 def test_abi_version_and_error_text():
     lib = A.load()
-    assert lib.dk_abi_version() == 1
+    assert lib.dk_abi_version() == 2
     assert isinstance(lib.dk_last_error(), bytes)
 
 
@@ -59,6 +59,9 @@ int main(void) {
   S(dk_profile) F(dk_profile, ms_index) F(dk_profile, ms_generate) F(dk_profile, ms_score)
   F(dk_profile, ms_gather) F(dk_profile, ms_total) F(dk_profile, score_launches)
   F(dk_profile, pairs_scored) F(dk_profile, pairs_generated) F(dk_profile, score_bytes)
+  S(dk_region_layout) F(dk_region_layout, capacity) F(dk_region_layout, first_offset)
+  F(dk_region_layout, prob_offset) F(dk_region_layout, candidate_offset)
+  F(dk_region_layout, kind_offset)
   return 0;
 }
 """
@@ -104,3 +107,23 @@ def test_schema_validation_rejects_unsupported():
     assert b"no GPU kernel" in lib.dk_last_error()
     s = A.dk_schema(1, arr, 0.9, 0.0, A.MODE_DEDUP, 0)
     assert lib.dk_create(C.byref(s), 0, C.byref(ctx)) == A.DK_E_INVALID
+
+
+def test_result_region_layout():
+    """dk_result_region_layout (host-only arithmetic): the four arrays are disjoint, aligned
+    and inside the region; region_views reads them back."""
+    import numpy as np
+    lay = A.region_layout(A.region_bytes(10, 100), 10)
+    assert lay["capacity"] == 100 and lay["first_offset"] == 0 and lay["prob_offset"] == 88
+    assert lay["candidate_offset"] == 88 + 800 and lay["kind_offset"] == 88 + 1200
+    assert lay["prob_offset"] % 8 == 0 and lay["candidate_offset"] % 4 == 0
+    buf = bytearray(A.region_bytes(10, 100) + 5)
+    v = A.region_views(buf, 10, 3, 7)
+    v["first"][:] = [0, 2, 2, 7]
+    v["candidate"][:] = np.arange(7)
+    v["prob"][:] = 0.5
+    v["kind"][:] = 1
+    w = A.region_views(buf, 10, 3, 7)
+    assert list(w["first"]) == [0, 2, 2, 7] and w["prob"].sum() == 3.5 and w["kind"].sum() == 7
+    with pytest.raises(A.DukeHipError):
+        A.region_layout(8, 10)

@@ -10,6 +10,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from dukehip import _abi as A
 from dukehip import dist as dshard
 
 N = 1003
@@ -57,6 +58,38 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+def _region_worker(rank, world, port, out):
+    """SharedRegionGather: each rank writes its tile into its slice of the shared mapping
+    (what dk_match does through dk_set_result_region); rank 0 reads the node list in place."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    q0, q1 = dshard.tile(N, rank, world)
+    first, cand, prob, kind = full_list(N)
+    a, b = int(first[q0]), int(first[q1])
+    nq_max = dshard.max_tile(N, world)
+    g = dshard.SharedRegionGather(dist, torch, torch.device("cpu"), None, nq_max, 800, world, rank)
+    ok = True
+    for step in range(2):  # the mapping is reused across batches
+        v = A.region_views(g.slices[rank], nq_max, q1 - q0, b - a)
+        v["first"][:] = (first[q0:q1 + 1] - a).astype(np.uint64)
+        v["candidate"][:] = cand[a:b]
+        v["prob"][:] = prob[a:b] + step
+        v["kind"][:] = kind[a:b]
+        total = g.exchange(q1 - q0, b - a, 10 * (q1 - q0))
+        if rank == 0:
+            got = dshard.concat_ranks(g.rank_lists())
+            ok = ok and (np.array_equal(got["first"], first) and np.array_equal(got["candidate"], cand)
+                         and np.array_equal(got["prob"], prob + step)
+                         and np.array_equal(got["kind"], kind) and total == 10 * N)
+        dist.barrier()
+    if rank == 0:
+        out.put(bool(ok and not os.path.exists(g.path)))
+    g.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -87,3 +120,16 @@ def test_gather_world2_gloo(world):
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
 
+
+
+def test_shared_region_gather_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_region_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True

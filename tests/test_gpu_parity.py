@@ -434,3 +434,44 @@ def test_httptransform_duke_links_bulk_equals_listener():
     body = L.http_transform_response(ents[300:], False, bulk)
     assert '"duke_links":[{"datasetId":"crm"' in body and '"extra"' not in body
     db.close()
+
+
+def test_result_region_matches_pool(monkeypatch):
+    """dk_set_result_region: the list lands in caller memory (here an anonymous mmap, as a
+    rank's slice of the node-wide shared mapping is) identical to the pooled host result;
+    a list that does not fit fails with DK_E_NOMEM, too many queries with DK_E_INVALID."""
+    import mmap
+    p, props, vals, keys = persons_case(900, 300, 8)
+    monkeypatch.setenv("DK_CHUNK_SLOTS", "4096")   # several overlapped chunk copies
+    n = len(vals[0])
+    eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", 2))
+    eng.upsert(n, np.arange(n), [dh.Column.from_strings(v) for v in vals],
+               key_columns=[dh.Column.from_strings(k) for k in keys])
+    q = np.arange(n, dtype=np.uint32)
+    ref = eng.match(q)
+    ref_arrays = [ref.first.copy(), ref.candidate.copy(), ref.prob.copy(), ref.kind.copy()]
+    ref.close()
+    assert len(ref_arrays[1]) > 0
+    buf = mmap.mmap(-1, A.region_bytes(n, len(ref_arrays[1]) + 100))
+    eng.set_result_region(buf, n)
+    for _ in range(2):
+        res = eng.match(q)
+        v = A.region_views(buf, n, n, res.n)
+        for got, want in zip((res.first, res.candidate, res.prob, res.kind), ref_arrays):
+            assert np.array_equal(got, want)
+        for got, want in zip((v["first"], v["candidate"], v["prob"], v["kind"]), ref_arrays):
+            assert np.array_equal(got, want)
+        res.close()
+    with pytest.raises(A.DukeHipError) as e:
+        eng.match(np.arange(n + 1, dtype=np.uint32) % n)
+    assert e.value.code == A.DK_E_INVALID
+    small = mmap.mmap(-1, A.region_bytes(n, 10))
+    eng.set_result_region(small, n)
+    with pytest.raises(A.DukeHipError) as e:
+        eng.match(q)
+    assert e.value.code == A.DK_E_NOMEM
+    eng.set_result_region(None, 0)
+    res = eng.match(q)
+    assert np.array_equal(res.prob, ref_arrays[2])
+    res.close()
+    eng.close()
