@@ -287,6 +287,12 @@ struct dk_ctx {
   std::vector<ArenaMark> transient_mark;
   // match scratch
   DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], rowof, sgroup[kMaxKeys];
+  // The blocking tables + candidate replica are index state: built by the first dk_match
+  // after the index changed (Duke's blocking database keeps its sorted key maps at index
+  // time; the reference's Lucene index is likewise maintained by index/commit, not by the
+  // query, IncrementalLuceneDatabase.java:146-165,498-575) and reused until the next change.
+  uint64_t index_gen = 1, tables_gen = 0, tables_m = 0;
+  BlockTables tables{};
   const uint32_t* rowof_p = nullptr;  // replica position -> row (rowof, or usable in ALLPAIRS)
   uint64_t rstride = 0;               // replica positions
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
@@ -570,6 +576,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   if (!transient && c->transient)
     return fail(DK_E_STATE, "transient rows present: dk_drop_transient before indexing");
   if (b->n == 0) return DK_OK;
+  c->index_gen++;  // also when the upsert fails part-way (tombstones may already be written)
   if (!b->ident) return fail(DK_E_INVALID, "batch.ident is NULL");
   if (c->schema.nprops > 0 && !b->columns) return fail(DK_E_INVALID, "batch.columns is NULL");
   if (c->schema.mode == DK_MODE_LINKAGE && !b->group)
@@ -655,6 +662,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   }
   HIPCHK(hipStreamSynchronize(s));
   c->nrows += n;
+  c->index_gen++;
   if (transient) c->transient = true;
   if (rows_out)
     for (uint64_t i = 0; i < n; ++i) rows_out[i] = (uint32_t)(row0 + i);
@@ -678,6 +686,7 @@ int dk_drop_transient(dk_ctx* c) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->nrows = c->transient_row0;
+  c->index_gen++;
   for (size_t p = 0; p < c->P.size(); ++p) {
     const auto& m = c->transient_mark[p];
     c->P[p].units_used = m.units;
@@ -887,9 +896,14 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   // ---- index: usable rows + per key function sort by (key, group, row) ----
   Timer t_index(prof, s);
   uint64_t M = 0;
-  int rc = build_usable(c, &M);
-  if (rc) return rc;
+  int rc = 0;
   BlockTables T{};
+  if (c->tables_gen == c->index_gen) {
+    T = c->tables;
+    M = c->tables_m;
+  } else {
+  rc = build_usable(c, &M);
+  if (rc) return rc;
   T.nkeys = nk;
   T.linkage = c->schema.mode == DK_MODE_LINKAGE;
   T.group = c->group.as<uint8_t>();
@@ -927,6 +941,10 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     }
     HIPCHK(launch_replicate_rows(c->rowof.as<uint32_t>(), npos, c->ident.as<uint64_t>(),
                                  c->rident.as<uint64_t>(), T, rk, s));
+  }
+  c->tables = T;
+  c->tables_m = M;
+  c->tables_gen = c->index_gen;
   }
   c->prof.ms_index += t_index.stop();
 

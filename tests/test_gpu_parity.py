@@ -475,3 +475,33 @@ def test_result_region_matches_pool(monkeypatch):
     assert np.array_equal(res.prob, ref_arrays[2])
     res.close()
     eng.close()
+
+
+def test_tables_rebuilt_after_each_upsert():
+    """The blocking tables are index state reused across dk_match calls; every upsert
+    (incl. re-upserted IDs and deleted rows) must be visible to the next match."""
+    p, props, vals, keys = persons_case(600, 300, 9)
+    n = len(vals[0])
+    rng = np.random.default_rng(9)
+    deleted = (rng.random(n) < 0.05).astype(np.uint8)
+    ident = np.arange(n, dtype=np.uint64)
+    ident[700:740] = ident[:40]
+    eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", len(keys)))
+    for a, b in [(0, 500), (500, 800), (800, n)]:
+        eng.upsert(b - a, ident[a:b], [dh.Column.from_strings(v[a:b]) for v in vals],
+                   deleted=deleted[a:b],
+                   key_columns=[dh.Column.from_strings(k[a:b]) for k in keys])
+        alive = np.ones(b, np.uint8)
+        last = {}
+        for r in range(b):
+            if int(ident[r]) in last:
+                alive[last[int(ident[r])]] = 0
+            last[int(ident[r])] = r
+        ot = O.OracleTable(props, [v[:b] for v in vals], keys=[k[:b] for k in keys],
+                           ident=ident[:b], deleted=deleted[:b], alive=alive,
+                           threshold=0.9, maybe=0.7)
+        for q in (np.arange(a, b, dtype=np.uint32), np.arange(0, b, 3, dtype=np.uint32)):
+            res = eng.match(q)   # the second match reuses the tables the first one built
+            assert_same(res, ot.match(q))
+            res.close()
+    eng.close()
