@@ -290,7 +290,8 @@ def main():
                          "avg_launch_ms": prof["ms_score"] / launches,
                          "bytes_per_launch": prof["score_bytes"] / launches},
             "phases_ms_per_step": {k: prof[k] / args.steps for k in
-                                   ("ms_index", "ms_generate", "ms_score", "ms_gather", "ms_total")},
+                                   ("ms_index", "ms_generate", "ms_score", "ms_gather", "ms_copy",
+                                    "ms_total")},
         }
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(w, last, args)

@@ -148,6 +148,7 @@ typedef struct dk_profile {
   uint64_t pairs_scored;
   uint64_t pairs_generated;
   uint64_t score_bytes;   /* algorithmic operand bytes of the scored pairs */
+  double ms_copy;         /* device->host copies of the match list (copy stream, overlapped) */
 } dk_profile;
 
 typedef struct dk_ctx dk_ctx;

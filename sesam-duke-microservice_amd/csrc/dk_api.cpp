@@ -296,7 +296,16 @@ struct dk_ctx {
   const uint32_t* rowof_p = nullptr;  // replica position -> row (rowof, or usable in ALLPAIRS)
   uint64_t rstride = 0;               // replica positions
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
-  DevBuf counters, st_bcnt, st_bscored, st_bbytes, st_boff, st_prob, st_cand, st_qidx;
+  DevBuf counters;
+  struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx; };
+  StageBufs stage[2];                          // double-buffered per-chunk staging
+  hipEvent_t count_ready[2] = {nullptr, nullptr};  // a chunk's entry count reached hs[]
+  hipEvent_t compact_done[2] = {nullptr, nullptr}; // a chunk's staging set was drained
+  // deferred profiling spans (Timer), resolved after dk_match's final synchronisation
+  struct Span { hipEvent_t a, b; double* acc; };
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_next = 0;
+  std::vector<Span> spans;
   PinnedBuf h_small;
   std::shared_ptr<ResultPool> pool = std::make_shared<ResultPool>();
   // caller-owned host region for DK_MATCH_HOST entries (dk_set_result_region), registered
@@ -412,6 +421,10 @@ int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
+  for (int b = 0; b < 2 && e == hipSuccess; ++b)
+    e = hipEventCreateWithFlags(&c->count_ready[b], hipEventDisableTiming);
+  for (int b = 0; b < 2 && e == hipSuccess; ++b)
+    e = hipEventCreateWithFlags(&c->compact_done[b], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->chunk_done, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
@@ -434,6 +447,11 @@ void dk_destroy(dk_ctx* c) {
   if (c->region.base) (void)hipHostUnregister(c->region.base);
   hipStream_t s = c->stream, cs = c->copy_stream;
   hipEvent_t ev = c->chunk_done;
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->count_ready)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->compact_done)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   if (ev) (void)hipEventDestroy(ev);
   if (cs) (void)hipStreamDestroy(cs);
@@ -702,30 +720,49 @@ int dk_drop_transient(dk_ctx* c) {
 // dk_match: Processor.deduplicate's match loop over the given query rows
 // ----------------------------------------------------------------------------------------
 namespace {
+// Profiling spans (dk_set_profiling): events recorded around stream work and resolved
+// after dk_match's final synchronisation, so profiling never stalls the host pipeline.
 struct Timer {
-  hipEvent_t a = nullptr, b = nullptr;
-  bool on;
+  dk_ctx* c;
+  double* acc;
   hipStream_t s;
-  Timer(bool enabled, hipStream_t st) : on(enabled), s(st) {
-    if (on) {
-      (void)hipEventCreate(&a);
-      (void)hipEventCreate(&b);
-      (void)hipEventRecord(a, s);
-    }
-  }
-  double stop() {
-    if (!on) return 0.0;
-    (void)hipEventRecord(b, s);
-    (void)hipEventSynchronize(b);
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, a, b);
-    return ms;
-  }
-  ~Timer() {
-    if (a) (void)hipEventDestroy(a);
-    if (b) (void)hipEventDestroy(b);
-  }
+  hipEvent_t a = nullptr;
+  Timer(dk_ctx* ctx, double* target, hipStream_t st);
+  void stop();
+  ~Timer() { stop(); }
 };
+
+static hipEvent_t pooled_event(dk_ctx* c) {
+  if (c->ev_next == c->ev_pool.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    c->ev_pool.push_back(e);
+  }
+  return c->ev_pool[c->ev_next++];
+}
+
+Timer::Timer(dk_ctx* ctx, double* target, hipStream_t st) : c(ctx), acc(target), s(st) {
+  if (!c->profiling) return;
+  a = pooled_event(c);
+  if (a) (void)hipEventRecord(a, s);
+}
+
+void Timer::stop() {
+  if (!a) return;
+  hipEvent_t b = pooled_event(c);
+  if (b && hipEventRecord(b, s) == hipSuccess) c->spans.push_back(dk_ctx::Span{a, b, acc});
+  a = nullptr;
+}
+
+// every span's events have completed (called after the final stream synchronisation)
+static void resolve_spans(dk_ctx* c) {
+  for (const auto& sp : c->spans) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, sp.a, sp.b) == hipSuccess) *sp.acc += ms;
+  }
+  c->spans.clear();
+  c->ev_next = 0;
+}
 
 uint64_t chunk_slots() {
   const char* e = getenv("DK_CHUNK_SLOTS");
@@ -885,7 +922,8 @@ static int build_usable(dk_ctx* c, uint64_t* m_out) {
 static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
                      ResultHolder* R) {
   hipStream_t s = c->stream;
-  const bool prof = c->profiling;
+  c->spans.clear();   // left over by a failed call
+  c->ev_next = 0;
   const auto t0 = std::chrono::steady_clock::now();
   const int nk = c->schema.nkeys;
   const bool allpairs = c->schema.mode == DK_MODE_ALLPAIRS;
@@ -894,7 +932,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
 
   // ---- index: usable rows + per key function sort by (key, group, row) ----
-  Timer t_index(prof, s);
+  Timer t_index(c, &c->prof.ms_index, s);
   uint64_t M = 0;
   int rc = 0;
   BlockTables T{};
@@ -946,10 +984,10 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   c->tables_m = M;
   c->tables_gen = c->index_gen;
   }
-  c->prof.ms_index += t_index.stop();
+  t_index.stop();
 
   // ---- candidate counts per query -> slot offsets ----
-  Timer t_gen(prof, s);
+  Timer t_gen(c, &c->prof.ms_generate, s);
   uint64_t total = 0, generated = 0, mpad = 0;
   if (!allpairs) {
     HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
@@ -976,103 +1014,159 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     total = nq * mpad;
     generated = nq * M;
   }
-  c->prof.ms_generate += t_gen.stop();
+  t_gen.stop();
 
   const ScoreParams P = make_params(c);
   const uint64_t CH = (chunk_slots() + kScoreBlock - 1) / kScoreBlock * kScoreBlock;
   const uint64_t chunk = std::min(CH, std::max<uint64_t>(total, 1));
   const uint64_t nblk_max = (chunk + kScoreBlock - 1) / kScoreBlock;
-  HIPCHK(c->st_bcnt.reserve(nblk_max * 4 + 4, 0, s));
-  HIPCHK(c->st_bscored.reserve(nblk_max * 4 + 4, 0, s));
-  HIPCHK(c->st_bbytes.reserve(nblk_max * 4 + 4, 0, s));
-  HIPCHK(c->st_boff.reserve(nblk_max * 8 + 8, 0, s));
-  HIPCHK(c->st_prob.reserve(nblk_max * kScoreBlock * 8, 0, s));
-  HIPCHK(c->st_cand.reserve(nblk_max * kScoreBlock * 4, 0, s));
-  HIPCHK(c->st_qidx.reserve(nblk_max * kScoreBlock * 4, 0, s));
+  // two staging sets: chunk i+1 scores into one while chunk i's entries are compacted
+  // out of the other, so the host never waits between score launches
+  StageOut st[2];
+  for (int b = 0; b < 2; ++b) {
+    dk_ctx::StageBufs& G = c->stage[b];
+    HIPCHK(G.bcnt.reserve(nblk_max * 4 + 4, 0, s));
+    HIPCHK(G.bscored.reserve(nblk_max * 4 + 4, 0, s));
+    HIPCHK(G.bbytes.reserve(nblk_max * 4 + 4, 0, s));
+    HIPCHK(G.boff.reserve(nblk_max * 8 + 8, 0, s));
+    HIPCHK(G.prob.reserve(nblk_max * kScoreBlock * 8, 0, s));
+    HIPCHK(G.cand.reserve(nblk_max * kScoreBlock * 4, 0, s));
+    HIPCHK(G.qidx.reserve(nblk_max * kScoreBlock * 4, 0, s));
+    st[b] = StageOut{c->counters.as<uint64_t>(), G.bcnt.as<uint32_t>(), G.bscored.as<uint32_t>(),
+                     G.bbytes.as<uint32_t>(), G.prob.as<double>(), G.cand.as<uint32_t>(),
+                     G.qidx.as<uint32_t>()};
+  }
   HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * sizeof(uint64_t), s));
-  StageOut st{c->counters.as<uint64_t>(), c->st_bcnt.as<uint32_t>(), c->st_bscored.as<uint32_t>(),
-              c->st_bbytes.as<uint32_t>(), c->st_prob.as<double>(), c->st_cand.as<uint32_t>(),
-              c->st_qidx.as<uint32_t>()};
   ResultBufs& B = *R->bufs;
   uint64_t nm = 0;  // entries so far
-  for (uint64_t s0 = 0; s0 < total; s0 += CH) {
-    const uint64_t s1 = std::min(total, s0 + CH);
-    const uint64_t nblk = (s1 - s0 + kScoreBlock - 1) / kScoreBlock;
-    PairSource src{};
-    src.queries = c->d_queries.as<uint32_t>();
-    src.m = M;
-    if (allpairs) {
-      src.allpairs = 1;
-      src.mpad = mpad;
-    } else {
-      src.wq = c->wq.as<uint32_t>();
-      src.qoff = c->qoff.as<uint64_t>();
-      src.ranges = c->ranges.as<uint2>();
-      src.nq = nq;
-      src.nkeys = nk;
-      src.rident = c->rident.as<uint64_t>();
-      for (int k = 0; k < nk; ++k) {
-        src.qkeys[k] = c->keys[k].as<uint64_t>();
-        src.rkeys[k] = c->rkeys[k].as<uint64_t>();
-      }
+  // chunk boundaries: full chunks, then the last two chunks' worth halved down to CH/16, so
+  // the copy of the final chunk's entries (not overlapped with scoring) is short
+  std::vector<uint64_t> bounds{0};
+  {
+    const uint64_t min_chunk = std::max<uint64_t>(kScoreBlock, CH / 16 / kScoreBlock * kScoreBlock);
+    uint64_t at = 0;
+    while (at < total) {
+      const uint64_t rem = total - at;
+      uint64_t len = rem > CH ? CH : rem;
+      if (rem <= 2 * CH && rem > min_chunk && !(flags & DK_MATCH_DEVICE))
+        len = std::max(min_chunk, (rem / 2 + kScoreBlock - 1) / kScoreBlock * kScoreBlock);
+      at = std::min(total, at + len);
+      bounds.push_back(at);
     }
-    Timer t_score(prof, s);
-    HIPCHK(launch_score(P, src, s0, s1 - s0, st, s));
-    c->prof.ms_score += t_score.stop();
-    HIPCHK(launch_reduce_blocks(st, nblk, s));
-    c->prof.score_launches += 1;
-    // block-ordered compaction of this chunk's entries onto the match list
-    Timer t_gather(prof, s);
-    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
-      return exclusive_scan_u32_u64(t, b, c->st_bcnt.as<uint32_t>(), c->st_boff.as<uint64_t>(), nblk, s);
-    }));
-    uint64_t* hs = c->h_small.as<uint64_t>();
-    hs[1] = 0;
-    HIPCHK(hipMemcpyAsync(&hs[0], c->st_boff.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&hs[1], c->st_bcnt.as<uint32_t>() + nblk - 1, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    const uint64_t add = hs[0] + (hs[1] & 0xFFFFFFFFu);
+  }
+  PairSource src{};
+  src.queries = c->d_queries.as<uint32_t>();
+  src.m = M;
+  if (allpairs) {
+    src.allpairs = 1;
+    src.mpad = mpad;
+  } else {
+    src.wq = c->wq.as<uint32_t>();
+    src.qoff = c->qoff.as<uint64_t>();
+    src.ranges = c->ranges.as<uint2>();
+    src.nq = nq;
+    src.nkeys = nk;
+    src.rident = c->rident.as<uint64_t>();
+    for (int k = 0; k < nk; ++k) {
+      src.qkeys[k] = c->keys[k].as<uint64_t>();
+      src.rkeys[k] = c->rkeys[k].as<uint64_t>();
+    }
+  }
+  uint64_t* hs = c->h_small.as<uint64_t>();
+  hipStream_t cs = c->copy_stream;
+  // Chunk ci scores on the main stream; its block-ordered compaction onto the match list and
+  // (host modes) the copy of its entries run on the copy stream, beside the next chunk's
+  // scoring.  Staging set ci&1 is reused by chunk ci+2 once compact_done[ci&1] fired.
+  auto compact_chunk = [&](size_t ci) -> int {
+    const int b = (int)(ci & 1);
+    HIPCHK(hipEventSynchronize(c->count_ready[b]));  // entry count of chunk ci is in hs[]
+    const uint64_t nblk = (bounds[ci + 1] - bounds[ci] + kScoreBlock - 1) / kScoreBlock;
+    const uint64_t add = hs[4 + 2 * b] + (hs[5 + 2 * b] & 0xFFFFFFFFu);
     if (add) {
       const uint64_t need = nm + add;
-      HIPCHK(B.d_cand.reserve(need * 4, nm * 4, s));
-      HIPCHK(B.d_kind.reserve(need, nm, s));
-      HIPCHK(B.d_prob.reserve(need * 8, nm * 8, s));
-      HIPCHK(B.d_qidx.reserve(need * 4, nm * 4, s));
+      HIPCHK(B.d_cand.reserve(need * 4, nm * 4, cs));
+      HIPCHK(B.d_kind.reserve(need, nm, cs));
+      HIPCHK(B.d_prob.reserve(need * 8, nm * 8, cs));
+      HIPCHK(B.d_qidx.reserve(need * 4, nm * 4, cs));
       MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(),
                    B.d_qidx.as<uint32_t>()};
-      HIPCHK(launch_compact(st, c->st_boff.as<uint64_t>(), nblk, nm, ml, s));
-      if (!(flags & DK_MATCH_DEVICE) && c->region.base) {
-        // caller region: same overlapped copies, into the registered caller memory
-        if (need > c->region.cap) {
-          (void)hipStreamSynchronize(c->copy_stream);
-          return fail(DK_E_NOMEM, "match list needs more than %llu entries; the result region "
-                      "holds %llu", (unsigned long long)need, (unsigned long long)c->region.cap);
+      HIPCHK(hipStreamWaitEvent(cs, c->count_ready[b], 0));
+      {
+        Timer t_gather(c, &c->prof.ms_gather, cs);
+        HIPCHK(launch_compact(st[b], c->stage[b].boff.as<uint64_t>(), nblk, nm, ml, cs));
+        t_gather.stop();
+      }
+      if (!(flags & DK_MATCH_DEVICE)) {
+        uint32_t* hc;
+        double* hp;
+        uint8_t* hk;
+        if (c->region.base) {  // caller region (dk_set_result_region)
+          if (need > c->region.cap) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamSynchronize(cs);
+            return fail(DK_E_NOMEM, "match list needs more than %llu entries; the result region "
+                        "holds %llu", (unsigned long long)need, (unsigned long long)c->region.cap);
+          }
+          hc = c->region.cand;
+          hp = c->region.prob;
+          hk = c->region.kind;
+        } else {  // the pooled pinned buffers
+          if (need * 8 > B.h_prob.bytes || need * 4 > B.h_cand.bytes || need > B.h_kind.bytes) {
+            HIPCHK(hipStreamSynchronize(cs));
+            HIPCHK(B.h_cand.reserve(need * 4, nm * 4));
+            HIPCHK(B.h_prob.reserve(need * 8, nm * 8));
+            HIPCHK(B.h_kind.reserve(need, nm));
+          }
+          hc = B.h_cand.as<uint32_t>();
+          hp = B.h_prob.as<double>();
+          hk = B.h_kind.as<uint8_t>();
         }
-        HIPCHK(hipEventRecord(c->chunk_done, s));
-        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->chunk_done, 0));
-        hipStream_t cs = c->copy_stream;
-        HIPCHK(hipMemcpyAsync(c->region.cand + nm, B.d_cand.as<uint32_t>() + nm, add * 4, hipMemcpyDeviceToHost, cs));
-        HIPCHK(hipMemcpyAsync(c->region.prob + nm, B.d_prob.as<double>() + nm, add * 8, hipMemcpyDeviceToHost, cs));
-        HIPCHK(hipMemcpyAsync(c->region.kind + nm, B.d_kind.as<uint8_t>() + nm, add, hipMemcpyDeviceToHost, cs));
-      } else if (!(flags & DK_MATCH_DEVICE)) {
-        // overlap: this chunk's entries go to pinned host memory on the copy stream while
-        // the next chunk scores
-        if (need * 8 > B.h_prob.bytes || need * 4 > B.h_cand.bytes || need > B.h_kind.bytes) {
-          HIPCHK(hipStreamSynchronize(c->copy_stream));
-          HIPCHK(B.h_cand.reserve(need * 4, nm * 4));
-          HIPCHK(B.h_prob.reserve(need * 8, nm * 8));
-          HIPCHK(B.h_kind.reserve(need, nm));
-        }
-        HIPCHK(hipEventRecord(c->chunk_done, s));
-        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->chunk_done, 0));
-        hipStream_t cs = c->copy_stream;
-        HIPCHK(hipMemcpyAsync(B.h_cand.as<uint32_t>() + nm, B.d_cand.as<uint32_t>() + nm, add * 4, hipMemcpyDeviceToHost, cs));
-        HIPCHK(hipMemcpyAsync(B.h_prob.as<double>() + nm, B.d_prob.as<double>() + nm, add * 8, hipMemcpyDeviceToHost, cs));
-        HIPCHK(hipMemcpyAsync(B.h_kind.as<uint8_t>() + nm, B.d_kind.as<uint8_t>() + nm, add, hipMemcpyDeviceToHost, cs));
+        Timer t_copy(c, &c->prof.ms_copy, cs);
+        HIPCHK(hipMemcpyAsync(hc + nm, B.d_cand.as<uint32_t>() + nm, add * 4, hipMemcpyDeviceToHost, cs));
+        HIPCHK(hipMemcpyAsync(hp + nm, B.d_prob.as<double>() + nm, add * 8, hipMemcpyDeviceToHost, cs));
+        HIPCHK(hipMemcpyAsync(hk + nm, B.d_kind.as<uint8_t>() + nm, add, hipMemcpyDeviceToHost, cs));
+        t_copy.stop();
       }
       nm = need;
     }
-    c->prof.ms_gather += t_gather.stop();
+    HIPCHK(hipEventRecord(c->compact_done[b], cs));
+    return DK_OK;
+  };
+  const size_t nchunks = bounds.size() - 1;
+  for (size_t ci = 0; ci < nchunks; ++ci) {
+    const int b = (int)(ci & 1);
+    const uint64_t s0 = bounds[ci], s1 = bounds[ci + 1];
+    const uint64_t nblk = (s1 - s0 + kScoreBlock - 1) / kScoreBlock;
+    if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging b drained
+    {
+      Timer t_score(c, &c->prof.ms_score, s);
+      HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
+      t_score.stop();
+    }
+    HIPCHK(launch_reduce_blocks(st[b], nblk, s));
+    c->prof.score_launches += 1;
+    {
+      Timer t_gather(c, &c->prof.ms_gather, s);
+      HIPCHK(with_tmp(c, [&](void* t, size_t& bytes) {
+        return exclusive_scan_u32_u64(t, bytes, st[b].bcnt, c->stage[b].boff.as<uint64_t>(), nblk, s);
+      }));
+      hs[5 + 2 * b] = 0;
+      HIPCHK(hipMemcpyAsync(&hs[4 + 2 * b], c->stage[b].boff.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(&hs[5 + 2 * b], st[b].bcnt + nblk - 1, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipEventRecord(c->count_ready[b], s));
+      t_gather.stop();
+    }
+    // the previous chunk's count is ready once its scan ran (before this chunk's score
+    // started): its compaction and copies are issued while this chunk scores
+    if (ci > 0) {
+      int rc2 = compact_chunk(ci - 1);
+      if (rc2) return rc2;
+    }
+  }
+  if (nchunks) {
+    int rc2 = compact_chunk(nchunks - 1);
+    if (rc2) return rc2;
+    HIPCHK(hipStreamWaitEvent(s, c->compact_done[(nchunks - 1) & 1], 0));  // list complete
   }
   HIPCHK(hipMemcpyAsync(c->h_small.p, c->counters.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -1085,7 +1179,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   c->prof.score_bytes += sbytes;
 
   // ---- per-query entry offsets, then (DK_MATCH_HOST) the copy into pinned host memory ----
-  Timer t_gather(prof, s);
+  Timer t_gather(c, &c->prof.ms_gather, s);
   HIPCHK(B.d_first.reserve((nq + 1) * 8, 0, s));
   HIPCHK(launch_first(B.d_qidx.as<uint32_t>(), nm, nq, B.d_first.as<uint64_t>(), s));
   R->r.nqueries = nq;
@@ -1110,7 +1204,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     R->r.kind = B.h_kind.as<uint8_t>();
   }
   HIPCHK(hipStreamSynchronize(s));
-  c->prof.ms_gather += t_gather.stop();
+  t_gather.stop();
+  resolve_spans(c);
   c->prof.ms_total +=
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return DK_OK;

@@ -78,7 +78,8 @@ class dk_profile(C.Structure):
     _fields_ = [("ms_index", C.c_double), ("ms_generate", C.c_double), ("ms_score", C.c_double),
                 ("ms_gather", C.c_double), ("ms_total", C.c_double),
                 ("score_launches", C.c_uint64), ("pairs_scored", C.c_uint64),
-                ("pairs_generated", C.c_uint64), ("score_bytes", C.c_uint64)]
+                ("pairs_generated", C.c_uint64), ("score_bytes", C.c_uint64),
+                ("ms_copy", C.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
