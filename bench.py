@@ -173,8 +173,17 @@ def main():
     w = build_workload(args)
     n = w["n"]
     eng = dh.GpuEngine(make_schema(w), device=local)
-    eng.upsert(n, np.arange(n, dtype=np.uint64), [synth.column(w["values"][p["name"]]) for p in w["props"]],
-               group=w["group"], key_columns=[synth.column(k) for k in w["keys"]] or None)
+    torch.cuda.synchronize()
+    # records/sec deduped: the batch's host pack (strings -> SoA columns) and
+    # dk_upsert, plus one dk_match of the batch (the step below)
+    t_pack = time.perf_counter()
+    cols = [synth.column(w["values"][p["name"]]) for p in w["props"]]
+    kcols = [synth.column(k) for k in w["keys"]] or None
+    t_up = time.perf_counter()
+    eng.upsert(n, np.arange(n, dtype=np.uint64), cols, group=w["group"], key_columns=kcols)
+    t_upsert = time.perf_counter() - t_up
+    t_pack = t_up - t_pack
+    del cols, kcols
     t_index = time.time() - t0
     # contiguous query tile of this rank
     allq = w["queries"]
@@ -259,7 +268,12 @@ def main():
         pmc = os.path.join(ROOT, "profiles", "pmc_k_score.json")
         if w["name"] == "dedup" and os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                pj = json.load(f)
+            # the PMC run's HBM bytes per scored pair, at this run's pairs per launch
+            if pj.get("hbm_bytes_per_pair"):
+                traffic = pj["hbm_bytes_per_pair"] * prof["pairs_scored"] / launches
+            else:
+                traffic = pj.get("hbm_bytes_per_launch")
         out = {
             "metric": METRIC,
             "value": value,
@@ -280,6 +294,9 @@ def main():
                        "parallelism": f"query-tile sharding x{world}, replicated index"
                                       + (f", {args.gather} result gather" if world > 1 else "")},
             "records_per_s": len(allq) / (ms_step / 1e3),
+            "records_per_s_end_to_end": len(allq) / (t_pack + t_upsert + ms_step / 1e3),
+            "host_pack_s": t_pack,
+            "upsert_s": t_upsert,
             "matches_per_step": (sum(c[0] for c in shared.counts) if shared is not None
                                  else int(last.n) if last is not None else 0),
             "index_build_s": t_index,

@@ -45,6 +45,16 @@ def main():
     write_kb = res["write"][0].get("WRITE_SIZE", 0.0)
     v, s = res["valu"][0], res["stall"][0]
     per_launch = (2.0 * fetch_kb + write_kb) * 1024.0 / n
+    # pairs scored by the profiled command (its bench.py JSON line), for a per-pair figure
+    # that bench.py scales to its own launch mix
+    pairs = None
+    try:
+        for line in open(os.path.join(pmcdir, "fetch.log")):
+            if line.startswith("{"):
+                d = json.loads(line)
+                pairs = d["config"]["pairs_per_step"] * d["steps"] + d["config"]["pairs_per_step"] * d["warmup"]
+    except (OSError, ValueError, KeyError):
+        pass
     summary = {
         "kernel": "k_score",
         "launches_profiled": n,
@@ -52,6 +62,8 @@ def main():
         "write_size_kib_total": write_kb,
         "hbm_bytes_per_launch": per_launch,
         "hbm_bytes_per_launch_uncorrected": (fetch_kb + write_kb) * 1024.0 / n,
+        "pairs_profiled": pairs,
+        "hbm_bytes_per_pair": (2.0 * fetch_kb + write_kb) * 1024.0 / pairs if pairs else None,
         "valu_insts_per_wave": v.get("SQ_INSTS_VALU", 0) / max(1.0, v.get("SQ_WAVES", 1)),
         "valu_thread_utilization": v.get("SQ_THREAD_CYCLES_VALU", 0) /
                                    max(1.0, v.get("SQ_ACTIVE_INST_VALU", 1) * 64),

@@ -23,6 +23,12 @@
 #ifndef DK_WAVES_SHORT
 #define DK_WAVES_SHORT 5  // k_score waves per SIMD up to 40 Levenshtein rows
 #endif
+#ifndef DK_WAVES_LONG8
+#define DK_WAVES_LONG8 5  // k_score_long waves per SIMD, <= 8 DP rows per lane
+#endif
+#ifndef DK_WAVES_LONG16
+#define DK_WAVES_LONG16 5  // k_score_long waves per SIMD, 16 DP rows per lane (A/B: 4/3 -> 5/5 is +13% on longtext despite more spills)
+#endif
 
 namespace dk {
 
@@ -1121,7 +1127,7 @@ void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t n
 }
 
 template <int RMAX, int LR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LR <= 8 ? 4 : 3, 8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LR <= 8 ? DK_WAVES_LONG8 : DK_WAVES_LONG16, 8)))
 void k_score_long(const ScoreParams P, const PairSource S,
                                                     uint64_t slot0, uint64_t nslots, StageOut out) {
   score_body<RMAX, LR>(P, S, slot0, nslots, out);
