@@ -177,7 +177,41 @@ class Column:
 
     @classmethod
     def from_strings(cls, values):
-        """values: iterable of str or None.  Latin-1-only columns pack one byte per unit."""
+        """values: iterable of str or None.  Latin-1-only columns pack one byte per unit.
+
+        One join + one encode for the whole column (no per-value encode): a Latin-1 column's
+        per-value unit counts are the str lengths; a UTF-16 column's are too unless it holds
+        characters outside the BMP (two units each), which falls back to per-value lengths."""
+        vals = list(values)
+        anymiss = None in vals
+        missing = [v is None for v in vals] if anymiss else None
+        joined = "".join("" if v is None else v for v in vals) if anymiss else "".join(vals)
+        n = len(vals)
+        try:
+            units = np.frombuffer(joined.encode("latin-1"), dtype=np.uint8)
+            lens = np.fromiter(((0 if v is None else len(v)) for v in vals) if anymiss
+                               else map(len, vals), dtype=np.int64, count=n)
+        except UnicodeEncodeError:
+            units = np.frombuffer(joined.encode("utf-16-le", "surrogatepass"), dtype=np.uint16)
+            if units.size == len(joined):
+                lens = np.fromiter(((0 if v is None else len(v)) for v in vals), dtype=np.int64,
+                                   count=n)
+            else:
+                lens = np.fromiter(((0 if v is None else
+                                     len(v.encode("utf-16-le", "surrogatepass")) // 2)
+                                    for v in vals), dtype=np.int64, count=n)
+        offs = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        if units.size == 0:
+            units = np.zeros(1, dtype=units.dtype)
+        present = None
+        if anymiss:
+            present = (~np.asarray(missing, dtype=bool)).astype(np.uint8)
+        return cls(offs, units, present)
+
+    @classmethod
+    def from_strings_per_value(cls, values):
+        """Reference packing, one encode per value (tests compare from_strings with it)."""
         vals = list(values)
         enc = []
         wide = False

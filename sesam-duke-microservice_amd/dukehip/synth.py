@@ -234,7 +234,4 @@ def ascii_column(values):
 
 
 def column(values):
-    try:
-        return ascii_column(values)
-    except UnicodeEncodeError:
-        return Column.from_strings(values)
+    return Column.from_strings(values)
