@@ -11,11 +11,14 @@ GPU configurations for measurement runs (not the headline line):
   longtext  configs[4]: text linkage, 64-256 chars, WeightedLevenshtein + QGram q=3
             JACCARD, key = first two tokens (default 200k x 200k; published 5M x 5M)
 
-One step = one dk_match over every query record of this rank (blocking-table build,
-candidate generation, fused scoring, threshold, match gather), with the index already
-resident in HBM.  N>1: one process per GPU (torchrun), replicated index, query records split
-into contiguous tiles per rank, match counts all-gathered and match lists gathered to rank 0
-over RCCL inside the step.  Rank 0 prints one JSON line.
+One step = one dk_match over every query record of this rank (candidate generation, fused
+scoring, threshold, match compaction and the copy of the match list to host memory), with
+the index already resident in HBM (its blocking tables are built by the first match after
+the upsert, in the warmup).  N>1: one process per GPU (torchrun), replicated index, query
+records split into contiguous tiles per rank; inside the step every rank copies its list
+into its slice of one shared host mapping and the per-rank counts are all-gathered over
+RCCL (--gather shm), or the lists are gathered to GPU 0 over RCCL (--gather rccl).  Rank 0
+prints one JSON line.
 """
 from __future__ import annotations
 
@@ -200,8 +203,16 @@ def main():
         cap = torch.tensor([probe.n], dtype=torch.int64, device=cdev)
         probe.close()
         dist.all_reduce(cap, op=dist.ReduceOp.MAX)
-        shared = dshard.SharedRegionGather(dist, torch, cdev, eng, nq_max,
-                                           int(cap.item() * 1.05) + 4096, world, rank)
+        try:
+            shared = dshard.SharedRegionGather(dist, torch, cdev, eng, nq_max,
+                                               int(cap.item() * 1.05) + 4096, world, rank)
+        except dshard.RegionUnavailable as e:   # all ranks: RCCL gather instead
+            if backend != "nccl":
+                raise
+            if rank == 0:
+                print(f"shm result gather unavailable ({e}); using --gather rccl",
+                      file=sys.stderr, flush=True)
+            args.gather = "rccl"
 
     def step():
         old = holder.pop("res", None)

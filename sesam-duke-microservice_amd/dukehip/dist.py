@@ -87,6 +87,10 @@ def concat_ranks(ranks):
             "kind": np.concatenate([r["kind"] for r in ranks])}
 
 
+class RegionUnavailable(RuntimeError):
+    """Raised on every rank when some rank cannot use the shared mapping."""
+
+
 class SharedRegionGather:
     """Node-wide shared host mapping with one result region per rank (SURVEY §8e exchange).
 
@@ -107,6 +111,10 @@ class SharedRegionGather:
         name = [None]
         if rank == 0:
             d = shm_dir if os.path.isdir(shm_dir) else None
+            if d is not None:
+                st = os.statvfs(d)   # a small /dev/shm (container default) would SIGBUS
+                if st.f_bavail * st.f_frsize < total + (64 << 20):
+                    d = None         # page-cache-backed file in the default temp dir
             fd, path = tempfile.mkstemp(prefix="dukehip_results_", dir=d)
             os.ftruncate(fd, total)
             os.close(fd)
@@ -121,8 +129,17 @@ class SharedRegionGather:
         self.slices = [memoryview(self.map)[r * self.slice_bytes:(r + 1) * self.slice_bytes]
                        for r in range(world)]
         self.engine = engine
+        ok = 1
         if engine is not None:
-            engine.set_result_region(self.slices[rank], self.nq_max)
+            try:
+                engine.set_result_region(self.slices[rank], self.nq_max)
+            except A.DukeHipError:
+                ok = 0
+        flag = torch.tensor([ok], dtype=torch.int64, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)   # every rank takes the same path
+        if int(flag.item()) == 0:
+            self.close()
+            raise RegionUnavailable("a rank could not register its result region")
         self.counts = None
 
     def exchange(self, nq, n, scored):
