@@ -20,9 +20,6 @@
 #ifndef DK_JW_NARROW
 #define DK_JW_NARROW 32  // JaroWinkler on 32-bit position masks up to this query length
 #endif
-#ifndef DK_LEV_CUT_EVERY
-#define DK_LEV_CUT_EVERY 1  // Levenshtein cutoff tested every this many DP columns (A/B: 4 and 8 are 2-8% slower)
-#endif
 #ifndef DK_WAVES_SHORT
 #define DK_WAVES_SHORT 5  // k_score waves per SIMD up to 40 Levenshtein rows
 #endif
@@ -346,25 +343,11 @@ __device__ __forceinline__ int compact_distance_pk(const uint64_t* peq, int n1, 
       diag = left;
       P[i] = v;
       above = v;
-    }
-    // The cutoff is tested on DK_LEV_CUT_EVERY-column strides only (the column pair t-1, t
-    // with t % CE == CE-1).  Testing later than Duke's loop does cannot change the result:
-    // once a column's minimum exceeds maxdist every later column's does too (each cell is
-    // >= the minimum of the previous column and of the top boundary j-1 > maxdist), so
-    // D(n1, n2) > maxdist and the similarity maps to `low` either way (levenshtein_peq).
-    constexpr int CE = DK_LEV_CUT_EVERY;
-    const bool chk = CE == 1 || (t % CE) >= CE - 2;  // wave-uniform: a scalar branch
-    if (chk) {
-      acc = 0xFFFFFFFFu;
-#pragma unroll
-      for (int i = 1; i <= H; ++i) {
-        if (H + i > R - TAIL) acc &= P[i] | tm[i];
-        else acc &= P[i];
-      }
+      if (H + i > R - TAIL) acc &= v | tm[i];
+      else acc &= v;
     }
     h2 = h1;
-    if (t >= 2 && (CE == 1 || t % CE == CE - 1) &&
-        (acc_prev & acc & 0x40004000u) == 0x40004000u) {  // column t-1 cut off
+    if (t >= 2 && (acc_prev & acc & 0x40004000u) == 0x40004000u) {  // column t-1 cut off
       result = maxdist + 1;
       live = false;
     } else if (t == fin) {
