@@ -57,6 +57,9 @@ def parse():
                     help="N>1 result gather: shm = every GPU copies its tile's list into its "
                          "slice of one shared host mapping (rank 0 reads it in place); rccl = "
                          "device lists gathered to GPU 0 over xGMI, then copied to the host")
+    ap.add_argument("--no-warm-batch", action="store_true",
+                    help="skip the warm-context re-upsert + match after the timed steps "
+                         "(PMC passes: one step's launches only)")
     ap.add_argument("--device-results", action="store_true",
                     help="diagnostic: keep the N=1 match list in HBM (no device->host copy)")
     ap.add_argument("--only", default=None,
@@ -340,7 +343,7 @@ def main():
         }
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(w, last, args)
-        if world == 1:
+        if world == 1 and not args.no_warm_batch:
             old = holder.pop("res", None)
             if old is not None:
                 old.close()
