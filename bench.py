@@ -12,13 +12,16 @@ GPU configurations for measurement runs (not the headline line):
             JACCARD, key = first two tokens (default 200k x 200k; published 5M x 5M)
 
 One step = one dk_match over every query record of this rank (candidate generation, fused
-scoring, threshold, match compaction and the copy of the match list to host memory), with
-the index already resident in HBM (its blocking tables are built by the first match after
-the upsert, in the warmup).  N>1: one process per GPU (torchrun), replicated index, query
-records split into contiguous tiles per rank; inside the step every rank copies its list
-into its slice of one shared host mapping and the per-rank counts are all-gathered over
-RCCL (--gather shm), or the lists are gathered to GPU 0 over RCCL (--gather rccl).  Rank 0
-prints one JSON line.
+scoring, threshold and the device-side compaction of the match list), with the index
+already resident in HBM (its blocking tables are built by the first match after the
+upsert, in the warmup) and the match list left in HBM: `value` is that rate.  The boundary
+hands the MatchListener its list in host memory, so the same step with the list copied to
+pinned host memory is timed after it and reported as `pcie_inclusive` (never `value`).
+N>1: one process per GPU (torchrun), replicated index, query records split into contiguous
+tiles per rank; every rank keeps its list in HBM and the per-rank counts are all-gathered
+over RCCL (--gather none, default); --gather shm also copies each tile's list into its
+slice of one shared host mapping, --gather rccl gathers the lists to GPU 0 over xGMI.
+Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -36,6 +39,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "candidate pairs scored/sec (node) + records/sec deduped, 1/2/4/8 MI355X"
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
+VALU_PEAK = 1024 * 2.4e9 / 2  # wave64 VALU instructions/s: 256 CUs x 4 SIMD-32, 2 cycles each
 DEFAULT_RECORDS = {"dedup": 1_000_000, "linkage": 1_000_000, "allpairs": 200_000, "longtext": 200_000}
 
 
@@ -52,16 +56,22 @@ def parse():
     ap.add_argument("--dup-frac", type=float, default=0.1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the oracle baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--gather", default="shm", choices=["shm", "rccl"],
-                    help="N>1 result gather: shm = every GPU copies its tile's list into its "
-                         "slice of one shared host mapping (rank 0 reads it in place); rccl = "
-                         "device lists gathered to GPU 0 over xGMI, then copied to the host")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (0 = every host core, os.cpu_count())")
+    ap.add_argument("--cpu-single-seconds", type=float, default=6.0,
+                    help="target CPU time of the single-core baseline sample (0 = skip)")
+    ap.add_argument("--gather", default="none", choices=["none", "shm", "rccl"],
+                    help="N>1 result path inside the timed steps: none = each rank's match "
+                         "list stays in its HBM and only the per-rank counts are all-gathered "
+                         "(the device-resident `value`); shm = every GPU also copies its "
+                         "tile's list into its slice of one shared host mapping (rank 0 reads "
+                         "it in place); rccl = device lists gathered to GPU 0 over xGMI")
+    ap.add_argument("--pcie-steps", type=int, default=3,
+                    help="N=1: extra steps with the match list copied to pinned host memory "
+                         "(the PCIe-inclusive rate, reported beside `value`; 0 = skip)")
     ap.add_argument("--no-warm-batch", action="store_true",
                     help="skip the warm-context re-upsert + match after the timed steps "
                          "(PMC passes: one step's launches only)")
-    ap.add_argument("--device-results", action="store_true",
-                    help="diagnostic: keep the N=1 match list in HBM (no device->host copy)")
     ap.add_argument("--only", default=None,
                     help="diagnostic: comma-separated property names to keep (not a bench line)")
     return ap.parse_args()
@@ -224,14 +234,25 @@ def main():
                       file=sys.stderr, flush=True)
             args.gather = "rccl"
 
-    def step():
+    def step(host=False):
         old = holder.pop("res", None)
         if old is not None:
             old.close()                       # hand the result memory back to the pool
         if dist is None:
-            res = eng.match(queries, on_device=args.device_results)  # pinned host memory
+            # the list stays in HBM (`value`), or is copied to pinned host memory (PCIe-
+            # inclusive line: the boundary hands the listener host buffers)
+            res = eng.match(queries, on_device=not host)
             holder["res"] = res
             return res, res.pairs_scored
+        if args.gather == "none":
+            # each rank's list stays in its HBM; the exchange is the all-gather of counts
+            res = eng.match(queries, on_device=True)
+            cnt = torch.tensor([res.n, res.pairs_scored, len(queries)], dtype=torch.int64, device=cdev)
+            allc = [torch.zeros_like(cnt) for _ in range(world)]
+            dist.all_gather(allc, cnt)
+            holder["res"] = res
+            holder["counts"] = [tuple(int(v) for v in c.cpu()) for c in allc]
+            return res, sum(c[1] for c in holder["counts"])
         if shared is not None:
             # N>1, shm gather: the list goes to this rank's slice of the shared host mapping
             # (overlapped chunk copies over this GPU's own link); the all-gather of counts
@@ -288,20 +309,48 @@ def main():
     pairs_step = total_scored / args.steps
     value = pairs_step / (ms_step / 1e3)
 
+    # PCIe-inclusive line (N=1): the same step with the match list copied to pinned host
+    # memory, as the C-ABI hands it to the MatchListener replay; never `value`
+    pcie = None
+    if world == 1 and args.pcie_steps > 0:
+        step(host=True)                      # sizes the pinned pool
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        sc_p = 0
+        for _ in range(args.pcie_steps):
+            last, sc = step(host=True)
+            sc_p += sc
+        torch.cuda.synchronize()
+        elp = time.perf_counter() - tp
+        pcie = {"value": sc_p / elp, "unit": "pairs/s", "steps": args.pcie_steps,
+                "ms_per_step": elp / args.pcie_steps * 1e3,
+                "note": "match list copied to pinned host memory inside the step (the "
+                        "boundary's host buffers); not `value`"}
+
     if rank == 0:
         launches = max(1, prof["score_launches"])
         score_s = prof["ms_score"] / 1e3
         achieved = prof["score_bytes"] / score_s if score_s > 0 else 0.0
         traffic = None
+        valu = None
         pmc = os.path.join(ROOT, "profiles", "pmc_k_score.json")
-        if w["name"] == "dedup" and os.path.exists(pmc):
+        if os.path.exists(pmc):
             with open(pmc) as f:
                 pj = json.load(f)
-            # the PMC run's HBM bytes per scored pair, at this run's pairs per launch
-            if pj.get("hbm_bytes_per_pair"):
-                traffic = pj["hbm_bytes_per_pair"] * prof["pairs_scored"] / launches
-            else:
-                traffic = pj.get("hbm_bytes_per_launch")
+            if pj.get("workload", "dedup") == w["name"]:
+                # the PMC run's HBM bytes per scored pair, at this run's pairs per launch
+                if pj.get("hbm_bytes_per_pair"):
+                    traffic = pj["hbm_bytes_per_pair"] * prof["pairs_scored"] / launches
+                else:
+                    traffic = pj.get("hbm_bytes_per_launch")
+                # VALU issue: wave-instructions per scored pair (SQ_INSTS_VALU of the PMC run)
+                # at this run's pairs and k_score time, against the chip's issue rate
+                # (1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction)
+                ipp = pj["counters"]["SQ_INSTS_VALU"] / pj["pairs_profiled"]
+                rate = ipp * prof["pairs_scored"] / score_s if score_s > 0 else 0.0
+                valu = {"insts_per_pair": ipp, "achieved": rate / 1e9, "peak": VALU_PEAK / 1e9,
+                        "unit": "G wave-instructions/s", "frac": rate / VALU_PEAK,
+                        "source": "profiles/pmc_k_score.json (" + pj.get("commit", "?") + ")"}
         out = {
             "metric": METRIC,
             "value": value,
@@ -329,6 +378,7 @@ def main():
             "host_pack_s": t_pack,
             "upsert_s": t_upsert,
             "matches_per_step": (sum(c[0] for c in shared.counts) if shared is not None
+                                 else sum(c[0] for c in holder["counts"]) if "counts" in holder
                                  else int(last.n) if last is not None else 0),
             "index_build_s": t_index,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
@@ -336,12 +386,16 @@ def main():
                          "traffic": traffic,
                          "kernel": "k_score", "launches": prof["score_launches"],
                          "avg_launch_ms": prof["ms_score"] / launches,
-                         "bytes_per_launch": prof["score_bytes"] / launches},
+                         "bytes_per_launch": prof["score_bytes"] / launches,
+                         "limiter": "valu" if valu else None, "valu": valu},
+            "pcie_inclusive": pcie,
             "phases_ms_per_step": {k: prof[k] / args.steps for k in
                                    ("ms_index", "ms_generate", "ms_score", "ms_gather", "ms_copy",
                                     "ms_total")},
         }
         if world == 1 and args.cpu_seconds > 0:
+            if last is None or last.on_device:
+                last, _ = step(host=True)    # the check needs the list on the host
             out["cpu_baseline"] = cpu_baseline(w, last, args)
         if world == 1 and not args.no_warm_batch:
             old = holder.pop("res", None)
@@ -392,14 +446,27 @@ def cpu_baseline(w, gpu_res, args):
     props = [{k: v for k, v in p.items() if k != "name"} for p in w["props"]]
     ot = O.OracleTable(props, [w["values"][p["name"]] for p in w["props"]], keys=w["keys"],
                        group=w["group"], threshold=w["threshold"], maybe=w["maybe"], mode=mode)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    nproc = os.cpu_count() or 1
+    threads = args.cpu_threads or nproc
     allq = w["queries"]
-    probe = min(len(allq), 2000 if mode != "allpairs" else 64)
-    r = ot.match(allq[:probe], nthreads=threads)
-    rate = r["pairs_scored"] / max(r["ms_score"] / 1e3, 1e-9)
-    per_q = r["pairs_scored"] / probe
-    s = int(min(len(allq), max(probe, args.cpu_seconds * rate / max(per_q, 1e-9))))
-    r = ot.match(allq[:s], nthreads=threads)
+
+    def sample(nthreads, seconds):
+        probe = min(len(allq), 2000 if mode != "allpairs" else 64)
+        if nthreads == 1:
+            probe = max(1, probe // 16)
+        r = ot.match(allq[:probe], nthreads=nthreads)
+        rate = r["pairs_scored"] / max(r["ms_score"] / 1e3, 1e-9)
+        per_q = r["pairs_scored"] / probe
+        s = int(min(len(allq), max(probe, seconds * rate / max(per_q, 1e-9))))
+        return s, ot.match(allq[:s], nthreads=nthreads)
+
+    single = None
+    if args.cpu_single_seconds > 0:
+        s1, r1 = sample(1, args.cpu_single_seconds)
+        single = {"value": r1["pairs_scored"] / (r1["ms_score"] / 1e3), "cores": 1,
+                  "sample": f"first {s1} query records ({r1['pairs_scored']} pairs)",
+                  "seconds": r1["ms_score"] / 1e3}
+    s, r = sample(threads, args.cpu_seconds)
     e = int(gpu_res.first[s])
     gq = np.repeat(allq[:s], np.diff(gpu_res.first[: s + 1]).astype(np.int64))
     ok = (np.array_equal(r["query"], gq) and np.array_equal(r["candidate"], gpu_res.candidate[:e])
@@ -410,12 +477,29 @@ def cpu_baseline(w, gpu_res, args):
             cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except OSError:
         pass
-    return {"value": r["pairs_scored"] / (r["ms_score"] / 1e3), "unit": "pairs/s", "cores": threads,
-            "kind": "port",
-            "sample": f"first {s} of {len(allq)} query records ({r['pairs_scored']} pairs), "
-                      f"scoring loop timed, blocking-index build excluded ({r['ms_index']:.0f} ms)",
-            "seconds": r["ms_score"] / 1e3, "cpu_model": cpu, "host_nproc": os.cpu_count(),
-            "matches_identical_to_gpu": bool(ok)}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except OSError:
+        affinity = None
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    out = {"value": r["pairs_scored"] / (r["ms_score"] / 1e3), "unit": "pairs/s", "cores": threads,
+           "kind": "port",
+           "sample": f"first {s} of {len(allq)} query records ({r['pairs_scored']} pairs), "
+                     f"scoring loop timed, blocking-index build excluded ({r['ms_index']:.0f} ms)",
+           "seconds": r["ms_score"] / 1e3, "cpu_model": cpu, "host_nproc": nproc,
+           "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+           "matches_identical_to_gpu": bool(ok), "single_core": single}
+    if single:
+        # what nproc cores would reach at the single-core rate (linear scaling: an upper
+        # bound of the host's all-core rate, the conservative denominator for GPU/CPU)
+        out["all_core_linear_bound"] = single["value"] * nproc
+    return out
 
 
 if __name__ == "__main__":

@@ -22,7 +22,11 @@
  *   dk_result        <- the MatchListener callbacks (BaseLinkDatabaseMatchListener.java:53-109):
  *                       entries grouped per query in batch order, candidate order inside;
  *                       result memory is pooled per ctx and recycled by dk_free_result.
- *   dk_compare_rows  <- `Processor.compare(Record, Record)` for one pair.
+ *   dk_compare_rows  <- `Processor.compare(Record, Record)` for one pair of indexed rows.
+ *   dk_compare_values<- `Processor.compare(Record, Record)` for two records that need not be
+ *                       indexed (SURVEY §8b dk_compare_pair): a dk_batch of 2.
+ *   dk_set_overwrite <- `Database.setOverwrite` (IncrementalLuceneDatabase.java:99, 515):
+ *                       with overwrite on, index() adds without the delete-by-ID.
  *   dk_set_profiling <- `Processor.setPerformanceProfiling` (App.java:345, 466).
  *   dk_last_error    <- DukeException / RuntimeException text (App.java:1007-1009).
  *
@@ -43,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DK_ABI_VERSION 2
+#define DK_ABI_VERSION 3
 
 /* status codes */
 #define DK_OK 0
@@ -155,6 +159,9 @@ typedef struct dk_ctx dk_ctx;
 
 int dk_create(const dk_schema* schema, int device, dk_ctx** out);
 void dk_destroy(dk_ctx* ctx);
+/* Failure-atomic: a batch that is rejected (DK_E_INVALID / DK_E_UNSUPPORTED / DK_E_NOMEM)
+ * leaves the index as it was -- no row added, no older version tombstoned -- so the caller
+ * may run that batch on stock Duke and keep the ctx.  LINKAGE batches need group[i] in {1,2}. */
 int dk_upsert(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
 /* IncrementalLuceneDatabase.setIndexingIsDisabled(true) (IncrementalLuceneDatabase.java:95,
  * 498-512) as the httptransform endpoint uses it (App.java:1130-1132): appends the batch as
@@ -188,7 +195,20 @@ typedef struct dk_region_layout {
 } dk_region_layout;
 int dk_result_region_layout(uint64_t bytes, uint64_t max_queries, dk_region_layout* out);
 int dk_set_result_region(dk_ctx* ctx, void* base, uint64_t bytes, uint64_t max_queries);
+/* Processor.compare(r1, r2) for two indexed rows; a record is compared with itself too
+ * (no isSameAs).  Leaves the blocking tables and result pools of the ctx untouched. */
 int dk_compare_rows(dk_ctx* ctx, uint32_t r1, uint32_t r2, double* prob);
+/* Processor.compare(r1, r2) for records given as a dk_batch with n == 2 (records 0 and 1
+ * are r1 and r2; ident / group / deleted / keys are ignored).  The ctx's index is not
+ * changed. */
+int dk_compare_values(dk_ctx* ctx, const dk_batch* pair, double* prob);
+/* Comparator.compare(v1, v2) of schema property `prop` for two indexed rows (the raw
+ * similarity PropertyImpl.compare maps to a probability), computed by the production
+ * scoring kernel.  NaN when either row has no (or an empty) value: Processor.compare never
+ * calls a comparator then.  Levenshtein: when Duke's early-exit cutoff fires the GPU
+ * returns a similarity below 0.5 (maxdist+1, not the column minimum); both map to <low>. */
+int dk_property_similarity(dk_ctx* ctx, int prop, uint32_t r1, uint32_t r2, double* sim);
+int dk_set_overwrite(dk_ctx* ctx, int on);
 uint64_t dk_num_rows(const dk_ctx* ctx);
 int dk_set_profiling(dk_ctx* ctx, int on);
 int dk_get_profile(const dk_ctx* ctx, dk_profile* out);

@@ -229,7 +229,12 @@ struct PropState {
   int maxlen = 0;
   int maxgrams = 0;        // longest code list of a value
   DevBuf off, len, units, num, numok, goff, gcnt, grams;
-  // candidate replica of the current dk_match (see dk_internal.h)
+};
+
+// One property's candidate replica (see dk_internal.h): values in replica-position order.
+// The blocking tables own one set (index state); dk_compare_rows builds its own one-position
+// set, so a single-pair compare never disturbs the cached tables.
+struct Replica {
   int rlmax = 0;
   int rgmax = 0;
   DevBuf rlen, runits, rnum, rnumok, rgoff, rgcnt, rgrams;
@@ -285,6 +290,11 @@ struct dk_ctx {
   uint64_t transient_row0 = 0;
   struct ArenaMark { uint64_t units, grams; int maxlen, maxgrams; };
   std::vector<ArenaMark> transient_mark;
+  bool overwrite = false;  // Database.setOverwrite(true): no delete-by-ID on upsert
+  std::vector<Replica> rep;       // candidate replica of the blocking tables, per property
+  std::vector<Replica> pair_rep;  // dk_compare_rows' one-position replica, per property
+  DevBuf pair_buf;                // dk_compare_rows' query row / rowof / staging
+  dk_ctx* pair_ctx = nullptr;     // dk_compare_values: a 2-row ALLPAIRS index of the schema
   // match scratch
   DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], rowof, sgroup[kMaxKeys];
   // The blocking tables + candidate replica are index state: built by the first dk_match
@@ -445,6 +455,7 @@ void dk_destroy(dk_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->copy_stream);
   if (c->region.base) (void)hipHostUnregister(c->region.base);
+  if (c->pair_ctx) dk_destroy(c->pair_ctx);
   hipStream_t s = c->stream, cs = c->copy_stream;
   hipEvent_t ev = c->chunk_done;
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
@@ -480,47 +491,55 @@ int dk_reset_profile(dk_ctx* c) {
 
 // ----------------------------------------------------------------------------------------
 // dk_upsert: Database.index(Record) for each record of the batch + Database.commit()
+//
+// Failure atomicity: a batch is validated and packed on the host first (stage_column,
+// stage_keys), then the device buffers are grown, and only then is anything committed —
+// the ID map, the tombstones of older versions and the arenas.  A rejected batch (bad
+// offsets, a value the GPU path does not hold, a bad group) leaves the index exactly as
+// it was, so a caller may hand that batch to stock Duke and keep using the ctx.  This is
+// Lucene's per-record delete-then-add made batch-atomic (IncrementalLuceneDatabase.java:
+// 516-517, 578-590: the deletes and adds become visible together at commit, :146-165).
 // ----------------------------------------------------------------------------------------
-static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, uint64_t row0) {
+struct ColStage {
+  int width = 0;                    // arena width after this batch
+  bool widen = false;               // the arena goes from u8 to u16 units
+  int maxlen = 0, maxgrams = 0;
+  std::vector<uint32_t> off;        // relative to the arena's current fill
+  std::vector<uint16_t> len;
+  std::vector<uint8_t> bytes;       // the batch's units at the arena width
+  std::vector<double> num;
+  std::vector<uint8_t> numok;
+  std::vector<uint32_t> goff;       // relative to the code list's current fill
+  std::vector<uint16_t> gcnt;
+  std::vector<uint64_t> grams;
+  uint64_t units = 0;               // code units appended (padded)
+};
+
+static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, ColStage& S) {
   PropState& P = c->P[pidx];
-  hipStream_t s = c->stream;
   if (!col->offsets || (n && !col->units && col->offsets[n] != col->offsets[0]))
     return fail(DK_E_INVALID, "property %d: offsets/units missing", pidx);
   if (col->width != 1 && col->width != 2)
     return fail(DK_E_INVALID, "property %d: width %d (1 or 2)", pidx, col->width);
-  int want = col->width;
-  if (P.width == 0) P.width = want;
-  if (want == 2 && P.width == 1) {
-    // widen the arena in place: strings keep their unit offsets (4-byte alignment holds)
-    DevBuf wide;
-    const uint64_t tot = P.units_used + 512;
-    HIPCHK(wide.reserve(P.units.bytes * 2 + 1024, 0, s));
-    HIPCHK(launch_widen_u8(P.units.as<uint8_t>(), wide.as<uint16_t>(), std::min<uint64_t>(tot, P.units.bytes), s));
-    HIPCHK(hipStreamSynchronize(s));
-    std::swap(P.units.p, wide.p);
-    std::swap(P.units.bytes, wide.bytes);
-    P.width = 2;
-  }
-  const int W = P.width;
+  const int W = std::max(P.width, col->width);
+  S.width = W;
+  S.widen = P.width == 1 && W == 2;
   const uint64_t align = 4 / W;  // units per 4 bytes
-  std::vector<uint32_t> off(n);
-  std::vector<uint16_t> len(n);
-  std::vector<uint8_t> bytes;
-  uint64_t cur = P.units_used;
+  S.off.resize(n);
+  S.len.resize(n);
+  S.maxlen = P.maxlen;
+  S.maxgrams = P.maxgrams;
+  uint64_t cur = 0;
   // values on the DP comparators are bounded by the long-value DP (query rows <= 256)
   const bool is_dp = P.cfg.comparator == DK_CMP_LEVENSHTEIN ||
                      P.cfg.comparator == DK_CMP_WEIGHTED_LEVENSHTEIN;
   std::vector<uint16_t> u16;
-  std::vector<double> num;
-  std::vector<uint8_t> numok;
-  std::vector<uint32_t> goff;
-  std::vector<uint16_t> gcnt;
-  std::vector<uint64_t> grams, g;
+  std::vector<uint64_t> g;
   const bool is_num = P.cfg.comparator == DK_CMP_NUMERIC;
   const bool is_qg = uses_codes(P.cfg.comparator);
   const bool is_tok = P.cfg.comparator != DK_CMP_QGRAM;
-  if (is_num) { num.assign(n, 0.0); numok.assign(n, 0); }
-  if (is_qg) { goff.assign(n, 0); gcnt.assign(n, 0); }
+  if (is_num) { S.num.assign(n, 0.0); S.numok.assign(n, 0); }
+  if (is_qg) { S.goff.assign(n, 0); S.gcnt.assign(n, 0); }
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t a = col->offsets[i], b = col->offsets[i + 1];
     if (b < a) return fail(DK_E_INVALID, "property %d: offsets not monotone at %llu", pidx,
@@ -534,58 +553,131 @@ static int upload_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, 
       return fail(DK_E_UNSUPPORTED,
                   "property %d: (Weighted)Levenshtein value of %llu units (GPU limit %d)", pidx,
                   (unsigned long long)L, kMaxLongUnits);
-    off[i] = (uint32_t)cur;
-    len[i] = present ? (uint16_t)L : kMissing;
+    S.off[i] = (uint32_t)cur;
+    S.len[i] = present ? (uint16_t)L : kMissing;
     if (!present) continue;
-    P.maxlen = std::max<int>(P.maxlen, (int)L);
+    S.maxlen = std::max<int>(S.maxlen, (int)L);
     u16.resize(L);
     for (uint64_t k = 0; k < L; ++k)
       u16[k] = col->width == 1 ? ((const uint8_t*)col->units)[a + k] : ((const uint16_t*)col->units)[a + k];
     const uint64_t padded = (L + align - 1) / align * align;
-    const size_t at = bytes.size();
-    bytes.resize(at + padded * W, 0);
-    if (W == 1) for (uint64_t k = 0; k < L; ++k) bytes[at + k] = (uint8_t)u16[k];
-    else memcpy(bytes.data() + at, u16.data(), L * 2);
+    const size_t at = S.bytes.size();
+    S.bytes.resize(at + padded * W, 0);
+    if (W == 1) for (uint64_t k = 0; k < L; ++k) S.bytes[at + k] = (uint8_t)u16[k];
+    else memcpy(S.bytes.data() + at, u16.data(), L * 2);
     cur += padded;
     if (is_num) {
       double v = 0.0;
-      numok[i] = java_parse_double(u16.data(), L, &v) ? 1 : 0;
-      num[i] = v;
+      S.numok[i] = java_parse_double(u16.data(), L, &v) ? 1 : 0;
+      S.num[i] = v;
     }
     if (is_qg) {
+      // token ids are interned per property; an id handed out by a batch that is then
+      // rejected is merely unused (ids only need to be equal <=> tokens equal)
       if (is_tok) token_codes(u16.data(), (int)L, P.tokens, g);
       else qgram_codes(u16.data(), (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, g);
       if (g.size() >= kMissing)
         return fail(DK_E_UNSUPPORTED, "property %d: %zu q-grams / tokens", pidx, g.size());
-      goff[i] = (uint32_t)(P.grams_used + grams.size());
-      gcnt[i] = (uint16_t)g.size();
-      P.maxgrams = std::max<int>(P.maxgrams, (int)g.size());
-      grams.insert(grams.end(), g.begin(), g.end());
+      S.goff[i] = (uint32_t)S.grams.size();
+      S.gcnt[i] = (uint16_t)g.size();
+      S.maxgrams = std::max<int>(S.maxgrams, (int)g.size());
+      S.grams.insert(S.grams.end(), g.begin(), g.end());
     }
   }
-  if (cur >= (1ull << 32)) return fail(DK_E_UNSUPPORTED, "property %d: arena over 4G units", pidx);
+  if (P.units_used + cur >= (1ull << 32))
+    return fail(DK_E_UNSUPPORTED, "property %d: arena over 4G units", pidx);
+  if (P.grams_used + S.grams.size() >= (1ull << 32))
+    return fail(DK_E_UNSUPPORTED, "property %d: over 4G q-gram / token codes", pidx);
+  S.units = cur;
+  return DK_OK;
+}
+
+// Grows the property's device buffers for the staged batch (contents preserved; a failed
+// allocation leaves the arena as it was).
+static int reserve_column(dk_ctx* c, int pidx, const ColStage& S) {
+  PropState& P = c->P[pidx];
+  hipStream_t s = c->stream;
+  const size_t used_b = P.units_used * S.width;
+  if (S.widen) {
+    // widen the arena: strings keep their unit offsets (4-byte alignment holds)
+    DevBuf wide;
+    const uint64_t tot = P.units_used + 512;
+    HIPCHK(wide.reserve(std::max<size_t>(P.units.bytes * 2 + 1024, used_b + S.bytes.size() + 512), 0, s));
+    HIPCHK(launch_widen_u8(P.units.as<uint8_t>(), wide.as<uint16_t>(), std::min<uint64_t>(tot, P.units.bytes), s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::swap(P.units.p, wide.p);
+    std::swap(P.units.bytes, wide.bytes);
+    P.width = 2;  // same strings, wider units: the index content is unchanged
+  }
+  HIPCHK(P.units.reserve(used_b + S.bytes.size() + 512, used_b, s));
+  if (!S.grams.empty() || uses_codes(P.cfg.comparator))
+    HIPCHK(P.grams.reserve((P.grams_used + S.grams.size() + 64) * 8, P.grams_used * 8, s));
+  return DK_OK;
+}
+
+static int commit_column(dk_ctx* c, int pidx, ColStage& S, uint64_t n, uint64_t row0) {
+  PropState& P = c->P[pidx];
+  hipStream_t s = c->stream;
+  const int W = S.width;
+  P.width = W;
+  for (auto& o : S.off) o += (uint32_t)P.units_used;
+  for (auto& o : S.goff) o += (uint32_t)P.grams_used;
   // units arena: keep 512 bytes of zeroed tail for the kernels' fixed-width over-reads
-  const size_t used_b = P.units_used * W, add_b = bytes.size();
-  HIPCHK(P.units.reserve(used_b + add_b + 512, used_b, s));
-  if (add_b) HIPCHK(hipMemcpyAsync(P.units.as<uint8_t>() + used_b, bytes.data(), add_b, hipMemcpyHostToDevice, s));
+  const size_t used_b = P.units_used * W, add_b = S.bytes.size();
+  if (add_b) HIPCHK(hipMemcpyAsync(P.units.as<uint8_t>() + used_b, S.bytes.data(), add_b, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(P.units.as<uint8_t>() + used_b + add_b, 0, 512, s));
-  P.units_used = cur;
-  HIPCHK(hipMemcpyAsync(P.off.as<uint32_t>() + row0, off.data(), n * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(P.len.as<uint16_t>() + row0, len.data(), n * 2, hipMemcpyHostToDevice, s));
-  if (is_num) {
-    HIPCHK(hipMemcpyAsync(P.num.as<double>() + row0, num.data(), n * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(P.numok.as<uint8_t>() + row0, numok.data(), n, hipMemcpyHostToDevice, s));
+  P.units_used += S.units;
+  P.maxlen = S.maxlen;
+  P.maxgrams = S.maxgrams;
+  HIPCHK(hipMemcpyAsync(P.off.as<uint32_t>() + row0, S.off.data(), n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P.len.as<uint16_t>() + row0, S.len.data(), n * 2, hipMemcpyHostToDevice, s));
+  if (!S.num.empty()) {
+    HIPCHK(hipMemcpyAsync(P.num.as<double>() + row0, S.num.data(), n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(P.numok.as<uint8_t>() + row0, S.numok.data(), n, hipMemcpyHostToDevice, s));
   }
-  if (is_qg) {
-    HIPCHK(hipMemcpyAsync(P.goff.as<uint32_t>() + row0, goff.data(), n * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(P.gcnt.as<uint16_t>() + row0, gcnt.data(), n * 2, hipMemcpyHostToDevice, s));
-    HIPCHK(P.grams.reserve((P.grams_used + grams.size() + 64) * 8, P.grams_used * 8, s));
-    if (!grams.empty())
-      HIPCHK(hipMemcpyAsync(P.grams.as<uint64_t>() + P.grams_used, grams.data(), grams.size() * 8,
+  if (!S.gcnt.empty()) {
+    HIPCHK(hipMemcpyAsync(P.goff.as<uint32_t>() + row0, S.goff.data(), n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(P.gcnt.as<uint16_t>() + row0, S.gcnt.data(), n * 2, hipMemcpyHostToDevice, s));
+    if (!S.grams.empty())
+      HIPCHK(hipMemcpyAsync(P.grams.as<uint64_t>() + P.grams_used, S.grams.data(), S.grams.size() * 8,
                             hipMemcpyHostToDevice, s));
-    P.grams_used += grams.size();
+    P.grams_used += S.grams.size();
   }
-  HIPCHK(hipStreamSynchronize(s));  // host staging vectors go out of scope
+  return DK_OK;
+}
+
+// Key ids of the batch per key function (u64 keys as given, or key strings interned
+// exactly).  Interning a key of a batch that is later rejected only adds an unused id.
+static int stage_keys(dk_ctx* c, const dk_batch* b, int style, std::vector<uint64_t>& kv) {
+  const int nk = c->schema.nkeys;
+  const uint64_t n = b->n;
+  kv.resize((uint64_t)nk * n);
+  for (int k = 0; k < nk; ++k) {
+    uint64_t* dst = kv.data() + (uint64_t)k * n;
+    if (style == 1) {
+      memcpy(dst, b->keys + (uint64_t)k * n, n * 8);
+      continue;
+    }
+    const dk_column& kc = b->key_columns[k];
+    if (!kc.offsets || (kc.width != 1 && kc.width != 2) ||
+        (n && !kc.units && kc.offsets[n] != kc.offsets[0]))
+      return fail(DK_E_INVALID, "key function %d: bad key column", k);
+    for (uint64_t i = 0; i < n; ++i)
+      if (kc.offsets[i + 1] < kc.offsets[i])
+        return fail(DK_E_INVALID, "key function %d: offsets not monotone at %llu", k,
+                    (unsigned long long)i);
+    auto& tab = c->intern[k];
+    std::u16string str;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t a = kc.offsets[i], e = kc.offsets[i + 1];
+      str.resize(e - a);
+      for (uint64_t j = a; j < e; ++j)
+        str[j - a] = kc.width == 1 ? ((const uint8_t*)kc.units)[j] : ((const uint16_t*)kc.units)[j];
+      auto it = tab.find(str);
+      if (it == tab.end()) it = tab.emplace(str, (uint64_t)tab.size()).first;
+      dst[i] = it->second;
+    }
+  }
   return DK_OK;
 }
 
@@ -594,47 +686,78 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   if (!transient && c->transient)
     return fail(DK_E_STATE, "transient rows present: dk_drop_transient before indexing");
   if (b->n == 0) return DK_OK;
-  c->index_gen++;  // also when the upsert fails part-way (tombstones may already be written)
   if (!b->ident) return fail(DK_E_INVALID, "batch.ident is NULL");
   if (c->schema.nprops > 0 && !b->columns) return fail(DK_E_INVALID, "batch.columns is NULL");
-  if (c->schema.mode == DK_MODE_LINKAGE && !b->group)
-    return fail(DK_E_INVALID, "LINKAGE mode needs batch.group (dukeGroupNo)");
+  const uint64_t n = b->n, row0 = c->nrows;
+  if (c->schema.mode == DK_MODE_LINKAGE) {
+    // dukeGroupNo is 1 or 2 (IncrementalDataSource.java:80-84); a record without it makes
+    // findCandidateMatches throw (IncrementalLuceneDatabase.java:469-471)
+    if (!b->group) return fail(DK_E_INVALID, "LINKAGE mode needs batch.group (dukeGroupNo)");
+    for (uint64_t i = 0; i < n; ++i)
+      if (b->group[i] != 1 && b->group[i] != 2)
+        return fail(DK_E_INVALID, "record %llu: dukeGroupNo %u (1 or 2 in LINKAGE mode)",
+                    (unsigned long long)i, (unsigned)b->group[i]);
+  }
   const int nk = c->schema.nkeys;
+  int style = 0;
   if (nk > 0) {
-    const int style = b->keys ? 1 : (b->key_columns ? 2 : 0);
+    style = b->keys ? 1 : (b->key_columns ? 2 : 0);
     if (!style) return fail(DK_E_INVALID, "batch has neither keys nor key_columns");
     if (c->key_style && c->key_style != style)
       return fail(DK_E_STATE, "key style changed between batches (u64 keys vs key strings)");
-    c->key_style = style;
   }
   // rows < 2^29: K (<= 8) sorted tables of replica positions stay below the u32 sentinel
-  if (c->nrows + b->n >= (1ull << 29))
+  if (row0 + n >= (1ull << 29))
     return fail(DK_E_UNSUPPORTED, "index would exceed %u rows", 1u << 29);
+
+  // 1. validate + pack on the host (no index state changes)
+  std::vector<ColStage> cols(c->schema.nprops);
+  for (int p = 0; p < c->schema.nprops; ++p) {
+    int rc = stage_column(c, p, &b->columns[p], n, cols[p]);
+    if (rc) return rc;
+  }
+  std::vector<uint64_t> kv;
+  if (nk > 0) {
+    int rc = stage_keys(c, b, style, kv);
+    if (rc) return rc;
+  }
+  // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517;
+  // skipped with overwrite, :515); transient rows are neither alive (never candidates) nor
+  // entered in the ID map.  Staged: the ID map changes are applied at commit.
+  std::vector<uint8_t> flags(n, 0);
+  std::vector<uint32_t> dead;
+  std::unordered_map<uint64_t, uint32_t> batch_row;  // ID -> newest row of this batch
+  for (uint64_t i = 0; i < n && !transient; ++i) {
+    flags[i] = kAlive | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
+    if (c->overwrite) continue;
+    auto bt = batch_row.find(b->ident[i]);
+    if (bt != batch_row.end()) {
+      flags[bt->second - row0] &= (uint8_t)~kAlive;
+      bt->second = (uint32_t)(row0 + i);
+      continue;
+    }
+    batch_row.emplace(b->ident[i], (uint32_t)(row0 + i));
+    auto it = c->ident_row.find(b->ident[i]);
+    if (it != c->ident_row.end()) dead.push_back(it->second);
+  }
+
+  // 2. device space (contents preserved; nothing logical changes on failure)
   HIPCHK(hipSetDevice(c->device));
-  const uint64_t n = b->n, row0 = c->nrows;
-  HIPCHK(grow_rows(c, row0 + n));
   hipStream_t s = c->stream;
+  HIPCHK(grow_rows(c, row0 + n));
+  for (int p = 0; p < c->schema.nprops; ++p) {
+    int rc = reserve_column(c, p, cols[p]);
+    if (rc) return rc;
+  }
+  DevBuf d_dead;
+  if (!dead.empty()) HIPCHK(d_dead.reserve(dead.size() * 4, 0, s));
+
+  // 3. commit
+  c->index_gen++;
   if (transient && !c->transient) {
     c->transient_row0 = row0;
     c->transient_mark.clear();
     for (auto& p : c->P) c->transient_mark.push_back({p.units_used, p.grams_used, p.maxlen, p.maxgrams});
-  }
-
-  // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517);
-  // transient rows are neither alive (never candidates) nor entered in the ID map
-  std::vector<uint8_t> flags(n, 0);
-  std::vector<uint32_t> dead;
-  for (uint64_t i = 0; i < n && !transient; ++i) {
-    flags[i] = kAlive | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
-    auto it = c->ident_row.find(b->ident[i]);
-    if (it != c->ident_row.end()) {
-      const uint32_t old = it->second;
-      if (old >= row0) flags[old - row0] &= (uint8_t)~kAlive;
-      else dead.push_back(old);
-      it->second = (uint32_t)(row0 + i);
-    } else {
-      c->ident_row.emplace(b->ident[i], (uint32_t)(row0 + i));
-    }
   }
   HIPCHK(hipMemcpyAsync(c->ident.as<uint64_t>() + row0, b->ident, n * 8, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(c->flags.as<uint8_t>() + row0, flags.data(), n, hipMemcpyHostToDevice, s));
@@ -642,43 +765,20 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     HIPCHK(hipMemcpyAsync(c->group.as<uint8_t>() + row0, b->group, n, hipMemcpyHostToDevice, s));
   else
     HIPCHK(hipMemsetAsync(c->group.as<uint8_t>() + row0, 0, n, s));
-  DevBuf d_dead;
   if (!dead.empty()) {
-    HIPCHK(d_dead.reserve(dead.size() * 4, 0, s));
     HIPCHK(hipMemcpyAsync(d_dead.p, dead.data(), dead.size() * 4, hipMemcpyHostToDevice, s));
     HIPCHK(launch_clear_flag(c->flags.as<uint8_t>(), d_dead.as<uint32_t>(), dead.size(), kAlive, s));
   }
   for (int p = 0; p < c->schema.nprops; ++p) {
-    int rc = upload_column(c, p, &b->columns[p], n, row0);
+    int rc = commit_column(c, p, cols[p], n, row0);
     if (rc) return rc;
   }
-  // key functions
-  std::vector<uint64_t> kv(n);
-  for (int k = 0; k < nk; ++k) {
-    const uint64_t* src;
-    if (c->key_style == 1) {
-      src = b->keys + (uint64_t)k * n;
-    } else {
-      const dk_column& kc = b->key_columns[k];
-      if (!kc.offsets || (kc.width != 1 && kc.width != 2))
-        return fail(DK_E_INVALID, "key function %d: bad key column", k);
-      auto& tab = c->intern[k];
-      std::u16string str;
-      for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t a = kc.offsets[i], e = kc.offsets[i + 1];
-        str.resize(e - a);
-        for (uint64_t j = a; j < e; ++j)
-          str[j - a] = kc.width == 1 ? ((const uint8_t*)kc.units)[j] : ((const uint16_t*)kc.units)[j];
-        auto it = tab.find(str);
-        if (it == tab.end()) it = tab.emplace(str, (uint64_t)tab.size()).first;
-        kv[i] = it->second;
-      }
-      src = kv.data();
-    }
-    HIPCHK(hipMemcpyAsync(c->keys[k].as<uint64_t>() + row0, src, n * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
-  }
-  HIPCHK(hipStreamSynchronize(s));
+  for (int k = 0; k < nk; ++k)
+    HIPCHK(hipMemcpyAsync(c->keys[k].as<uint64_t>() + row0, kv.data() + (uint64_t)k * n, n * 8,
+                          hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // host staging goes out of scope
+  for (const auto& br : batch_row) c->ident_row[br.first] = br.second;
+  if (nk > 0) c->key_style = style;
   c->nrows += n;
   c->index_gen++;
   if (transient) c->transient = true;
@@ -771,17 +871,21 @@ uint64_t chunk_slots() {
 }
 }  // namespace
 
-static ScoreParams make_params(const dk_ctx* c) {
+// Score parameters over a candidate replica set (`rep`, one per property) whose position g
+// holds row rowof[g], npos positions.
+static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
+                               const uint32_t* rowof, uint64_t npos) {
   ScoreParams P{};
   P.nprops = c->schema.nprops;
   P.mode = c->schema.mode;
   P.threshold = c->schema.threshold;
   P.maybe = c->schema.maybe_threshold;
   P.ident = c->ident.as<uint64_t>();
-  P.rowof = c->rowof_p;
-  P.rstride = c->rstride;
+  P.rowof = rowof;
+  P.rstride = npos;
   P.lev_rows = 0;
   P.long_rows = 0;
+  P.raw_prop = -1;
   for (const auto& S : c->P) {
     if (S.cfg.comparator == DK_CMP_LEVENSHTEIN) {
       P.lev_rows = std::max(P.lev_rows, std::min(S.maxlen, kMaxUnits));
@@ -792,6 +896,7 @@ static ScoreParams make_params(const dk_ctx* c) {
   }
   for (int i = 0; i < P.nprops; ++i) {
     const PropState& S = c->P[i];
+    const Replica& R = rep[i];
     DevProp& D = P.props[i];
     D.op = S.cfg.comparator;
     D.width = S.width ? S.width : 1;
@@ -809,15 +914,15 @@ static ScoreParams make_params(const dk_ctx* c) {
     D.goff = S.goff.as<uint32_t>();
     D.gcnt = S.gcnt.as<uint16_t>();
     D.grams = S.grams.as<uint64_t>();
-    D.rlmax = S.rlmax;
-    D.rlen = S.rlen.as<uint16_t>();
-    D.runits = S.runits.p;
-    D.rnum = S.rnum.as<double>();
-    D.rnumok = S.rnumok.as<uint8_t>();
-    D.rgoff = S.rgoff.as<uint32_t>();
-    D.rgcnt = S.rgcnt.as<uint16_t>();
-    D.rgrams = S.rgrams.p;
-    D.rgmax = S.rgmax;
+    D.rlmax = R.rlmax;
+    D.rlen = R.rlen.as<uint16_t>();
+    D.runits = R.runits.p;
+    D.rnum = R.rnum.as<double>();
+    D.rnumok = R.rnumok.as<uint8_t>();
+    D.rgoff = R.rgoff.as<uint32_t>();
+    D.rgcnt = R.rgcnt.as<uint16_t>();
+    D.rgrams = R.rgrams.p;
+    D.rgmax = R.rgmax;
     D.rg32 = 16 * S.cfg.qgram_q + (S.cfg.qgram_tokenizer == DK_QGRAM_POSITIONAL ? 16 : 0) <= 32;
   }
   return P;
@@ -825,36 +930,37 @@ static ScoreParams make_params(const dk_ctx* c) {
 
 // Candidate replica: every property's candidate-side values in replica order, units
 // transposed ([unit][position]) for values of at most kMaxReplicaUnits units.
-static int build_replica(dk_ctx* c, const uint32_t* rowof, uint64_t npos) {
+static int build_replica(dk_ctx* c, std::vector<Replica>& rep, const uint32_t* rowof, uint64_t npos) {
   hipStream_t s = c->stream;
-  c->rowof_p = rowof;
-  c->rstride = npos;
-  for (auto& S : c->P) {
+  rep.resize(c->P.size());
+  for (size_t i = 0; i < c->P.size(); ++i) {
+    const PropState& S = c->P[i];
+    Replica& R = rep[i];
     const int op = S.cfg.comparator;
     const bool strcmp_ = op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER ||
                          op == DK_CMP_EXACT || uses_codes(op) ||
                          op == DK_CMP_WEIGHTED_LEVENSHTEIN;
     const int W = S.width ? S.width : 1;
-    S.rlmax = strcmp_ && S.maxlen <= kMaxReplicaUnits ? ((std::max(S.maxlen, 1) + 3) & ~3) : 0;
-    HIPCHK(S.rlen.reserve(npos * 2 + 8, 0, s));
-    if (S.rlmax) HIPCHK(S.runits.reserve(npos * (uint64_t)S.rlmax * W + 64, 0, s));
+    R.rlmax = strcmp_ && S.maxlen <= kMaxReplicaUnits ? ((std::max(S.maxlen, 1) + 3) & ~3) : 0;
+    HIPCHK(R.rlen.reserve(npos * 2 + 8, 0, s));
+    if (R.rlmax) HIPCHK(R.runits.reserve(npos * (uint64_t)R.rlmax * W + 64, 0, s));
     const bool num = op == DK_CMP_NUMERIC, qg = uses_codes(op);
     if (num) {
-      HIPCHK(S.rnum.reserve(npos * 8 + 8, 0, s));
-      HIPCHK(S.rnumok.reserve(npos + 8, 0, s));
+      HIPCHK(R.rnum.reserve(npos * 8 + 8, 0, s));
+      HIPCHK(R.rnumok.reserve(npos + 8, 0, s));
     }
     if (qg) {
-      HIPCHK(S.rgoff.reserve(npos * 4 + 8, 0, s));
-      HIPCHK(S.rgcnt.reserve(npos * 2 + 8, 0, s));
+      HIPCHK(R.rgoff.reserve(npos * 4 + 8, 0, s));
+      HIPCHK(R.rgcnt.reserve(npos * 2 + 8, 0, s));
     }
-    S.rgmax = op == DK_CMP_QGRAM && S.maxgrams <= kMaxReplicaGrams ? std::max(S.maxgrams, 1) : 0;
+    R.rgmax = op == DK_CMP_QGRAM && S.maxgrams <= kMaxReplicaGrams ? std::max(S.maxgrams, 1) : 0;
     // codes pack 16 bits per unit (+16 for the POSITIONAL index): q <= 2 fits in a u32
     const int gram_bits = 16 * S.cfg.qgram_q + (S.cfg.qgram_tokenizer == DK_QGRAM_POSITIONAL ? 16 : 0);
     const int rgw = gram_bits <= 32 ? 4 : 8;
-    if (S.rgmax) HIPCHK(S.rgrams.reserve(npos * (uint64_t)S.rgmax * rgw + 64, 0, s));
+    if (R.rgmax) HIPCHK(R.rgrams.reserve(npos * (uint64_t)R.rgmax * rgw + 64, 0, s));
     ReplicaJob J{};
     J.width = W;
-    J.rlmax = S.rlmax;
+    J.rlmax = R.rlmax;
     J.has_num = num;
     J.has_qgram = qg;
     J.stride = npos;
@@ -865,16 +971,16 @@ static int build_replica(dk_ctx* c, const uint32_t* rowof, uint64_t npos) {
     J.numok = S.numok.as<uint8_t>();
     J.goff = S.goff.as<uint32_t>();
     J.gcnt = S.gcnt.as<uint16_t>();
-    J.rlen = S.rlen.as<uint16_t>();
-    J.runits = S.runits.p;
-    J.rnum = S.rnum.as<double>();
-    J.rnumok = S.rnumok.as<uint8_t>();
-    J.rgoff = S.rgoff.as<uint32_t>();
-    J.rgcnt = S.rgcnt.as<uint16_t>();
-    J.rgmax = S.rgmax;
+    J.rlen = R.rlen.as<uint16_t>();
+    J.runits = R.runits.p;
+    J.rnum = R.rnum.as<double>();
+    J.rnumok = R.rnumok.as<uint8_t>();
+    J.rgoff = R.rgoff.as<uint32_t>();
+    J.rgcnt = R.rgcnt.as<uint16_t>();
+    J.rgmax = R.rgmax;
     J.rg32 = rgw == 4;
     J.grams = S.grams.as<uint64_t>();
-    J.rgrams = S.rgrams.p;
+    J.rgrams = R.rgrams.p;
     HIPCHK(launch_replicate(J, rowof, npos, s));
   }
   return DK_OK;
@@ -966,8 +1072,9 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   }
   T.rowof = c->rowof.as<uint32_t>();
   // candidate replica in slot-position order: the K sorted tables, or the usable rows
-  rc = allpairs ? build_replica(c, c->usable.as<uint32_t>(), M)
-                : build_replica(c, c->rowof.as<uint32_t>(), (uint64_t)nk * M);
+  c->rowof_p = allpairs ? c->usable.as<uint32_t>() : c->rowof.as<uint32_t>();
+  c->rstride = allpairs ? M : (uint64_t)nk * M;
+  rc = build_replica(c, c->rep, c->rowof_p, c->rstride);
   if (rc) return rc;
   if (!allpairs) {  // replica-ordered identity / keys for the candidate filters
     const uint64_t npos = (uint64_t)nk * M;
@@ -1016,7 +1123,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   }
   t_gen.stop();
 
-  const ScoreParams P = make_params(c);
+  const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
   const uint64_t CH = (chunk_slots() + kScoreBlock - 1) / kScoreBlock * kScoreBlock;
   const uint64_t chunk = std::min(CH, std::max<uint64_t>(total, 1));
   const uint64_t nblk_max = (chunk + kScoreBlock - 1) / kScoreBlock;
@@ -1307,28 +1414,48 @@ void dk_free_result(dk_result* r) {
   delete R;
 }
 
+// Processor.compare(r1, r2) of two indexed rows.  The candidate side is a private
+// one-position replica (pair_rep) and staging (pair_buf): the blocking tables, their
+// replica and the result pools are untouched, so dk_match after a compare reuses them.
+static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double* prob);
+
 int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
+  return compare_one(c, r1, r2, -1, prob);
+}
+
+// Comparator.compare(v1, v2) of property `prop` (the raw similarity PropertyImpl maps to a
+// probability) for two indexed rows, through the production scoring kernel.
+int dk_property_similarity(dk_ctx* c, int prop, uint32_t r1, uint32_t r2, double* sim) {
+  if (!c || !sim) return fail(DK_E_INVALID, "NULL argument");
+  if (prop < 0 || prop >= c->schema.nprops)
+    return fail(DK_E_INVALID, "property %d out of range [0, %d)", prop, c->schema.nprops);
+  return compare_one(c, r1, r2, prop, sim);
+}
+
+static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double* prob) {
   if (!c || !prob) return fail(DK_E_INVALID, "NULL argument");
   if (r1 >= c->nrows || r2 >= c->nrows) return fail(DK_E_INVALID, "row out of range");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  DevBuf buf;  // [0] query row, [3] rowof[0] (the one replica position); then staging
-  HIPCHK(buf.reserve(8192, 0, s));
+  // pair_buf: [0] query row, [3] rowof[0] (the one replica position); then staging
+  HIPCHK(c->pair_buf.reserve(8192, 0, s));
   uint32_t host[4] = {r1, 0u, 0u, r2};
-  HIPCHK(hipMemsetAsync(buf.p, 0, 8192, s));
-  HIPCHK(hipMemcpyAsync(buf.p, host, sizeof host, hipMemcpyHostToDevice, s));
-  uint8_t* base = buf.as<uint8_t>();
+  HIPCHK(hipMemsetAsync(c->pair_buf.p, 0, 8192, s));
+  HIPCHK(hipMemcpyAsync(c->pair_buf.p, host, sizeof host, hipMemcpyHostToDevice, s));
+  uint8_t* base = c->pair_buf.as<uint8_t>();
   StageOut st{reinterpret_cast<uint64_t*>(base + 64), reinterpret_cast<uint32_t*>(base + 96),
               reinterpret_cast<uint32_t*>(base + 100), reinterpret_cast<uint32_t*>(base + 104),
               reinterpret_cast<double*>(base + 128), reinterpret_cast<uint32_t*>(base + 2176),
               reinterpret_cast<uint32_t*>(base + 3200)};
-  int rc = build_replica(c, buf.as<uint32_t>() + 3, 1);  // one-position candidate replica
+  const uint32_t* rowof = c->pair_buf.as<uint32_t>() + 3;
+  int rc = build_replica(c, c->pair_rep, rowof, 1);
   if (rc) return rc;
-  ScoreParams P = make_params(c);
+  ScoreParams P = make_params(c, c->pair_rep, rowof, 1);
+  P.raw_prop = raw_prop;
   P.threshold = -INFINITY;  // every non-NaN probability is emitted
   P.maybe = 0.0;
   PairSource src{};  // one all-pairs slot: query r1 against replica position 0 (row r2)
-  src.queries = buf.as<uint32_t>();
+  src.queries = c->pair_buf.as<uint32_t>();
   src.allpairs = 1;
   src.m = 1;
   src.mpad = 64;
@@ -1340,5 +1467,55 @@ int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
   HIPCHK(hipMemcpyAsync(&p, base + 128, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   *prob = n ? p : NAN;
+  return DK_OK;
+}
+
+// Processor.compare(Record, Record) for two records that need not be indexed (SURVEY §8b
+// dk_compare_pair): the pair is packed into a private 2-row ALLPAIRS index with the same
+// properties (created on first use, emptied per call) and scored there.
+static void clear_index(dk_ctx* c) {
+  c->nrows = 0;
+  c->index_gen++;
+  c->ident_row.clear();
+  for (auto& t : c->intern) t.clear();
+  c->key_style = 0;
+  c->transient = false;
+  for (auto& p : c->P) {
+    p.units_used = p.grams_used = 0;
+    p.maxlen = p.maxgrams = 0;
+    p.tokens.clear();
+  }
+}
+
+int dk_compare_values(dk_ctx* c, const dk_batch* pair, double* prob) {
+  if (!c || !pair || !prob) return fail(DK_E_INVALID, "NULL argument");
+  if (pair->n != 2) return fail(DK_E_INVALID, "dk_compare_values takes a batch of 2 records (r1, r2)");
+  if (!c->pair_ctx) {
+    std::vector<dk_property> props(c->P.size());
+    for (size_t i = 0; i < c->P.size(); ++i) props[i] = c->P[i].cfg;
+    dk_schema sc = c->schema;
+    sc.props = props.data();
+    sc.mode = DK_MODE_ALLPAIRS;
+    sc.nkeys = 0;
+    int rc = dk_create(&sc, c->device, &c->pair_ctx);
+    if (rc) return rc;
+  }
+  dk_ctx* pc = c->pair_ctx;
+  clear_index(pc);
+  dk_batch b = *pair;
+  const uint64_t ident[2] = {0, 1};  // Processor.compare does not apply isSameAs
+  b.ident = ident;
+  b.group = nullptr;
+  b.deleted = nullptr;
+  b.keys = nullptr;
+  b.key_columns = nullptr;
+  int rc = upsert_rows(pc, &b, nullptr, false);
+  if (rc) return rc;
+  return dk_compare_rows(pc, 0, 1, prob);
+}
+
+int dk_set_overwrite(dk_ctx* c, int on) {
+  if (!c) return fail(DK_E_INVALID, "ctx is NULL");
+  c->overwrite = on != 0;
   return DK_OK;
 }

@@ -77,6 +77,9 @@ struct ScoreParams {
   int32_t mode;
   int32_t lev_rows;       // longest Levenshtein value in the index (selects the variant)
   int32_t long_rows;      // longest value on the long-value DP (0 = none; selects the variant)
+  int32_t raw_prop;       // >= 0: emit property raw_prop's comparator similarity instead of
+                          // the probability (dk_property_similarity); -1 = normal scoring
+  int32_t pad_;
   double threshold;
   double maybe;
   const uint64_t* ident;

@@ -1039,7 +1039,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   if (S.allpairs && !S.same_ok) valid = valid && P.ident[crow] != P.ident[q];  // Processor.isSameAs
   wave_lds_sync();
 
-  double prob = 0.5;
+  double prob = P.raw_prop < 0 ? 0.5 : __builtin_nan("");
   uint32_t bytes = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
   for (int p = 0; p < P.nprops; ++p) {
     const DevProp& D = P.props[p];
@@ -1049,16 +1049,27 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     const bool present = lc != (int)kMissing;
     const bool cmp = present && lq > 0 && lc > 0;
     double sim = 0.0;
+    // algorithmic bytes: the CANDIDATE's operands at their stored
+    // width -- the query's value is read once per wave (LDS tables), not per pair
+    if (present) bytes += 2u;  // rlen
     if (D.op == DK_CMP_NUMERIC) {
       if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
-      if (cmp) bytes += 16;
+      if (cmp) bytes += 9u;   // rnum + rnumok
     } else if (D.op != DK_CMP_NONE) {
       sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp)
                          : string_sim<RMAX, LR, uint16_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp);
       if (cmp) {
-        bytes += 8u + (uint32_t)(lq + lc) * (uint32_t)D.width;
-        if (uses_codes(D.op)) bytes += 8u + 8u * (uint32_t)(D.gcnt[q] + D.rgcnt[g]);
+        if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2)
+          bytes += 6u + (D.rg32 && D.rgmax ? 4u : 8u) * (uint32_t)D.rgcnt[g];
+        else if (uses_codes(D.op))  // token ids
+          bytes += 6u + 8u * (uint32_t)D.rgcnt[g];
+        else
+          bytes += (uint32_t)lc * (uint32_t)D.width;
       }
+    }
+    if (p == P.raw_prop) {  // Comparator.compare(v1, v2) itself (wave-uniform branch)
+      if (cmp) prob = sim;
+      break;
     }
     if (present) {
       double high = 0.0;

@@ -28,7 +28,7 @@ MATCH_HOST, MATCH_DEVICE = 0, 1
 EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
            "dk_match", "dk_result_copy_to_device",
            "dk_free_result", "dk_result_region_layout", "dk_set_result_region",
-           "dk_compare_rows", "dk_num_rows", "dk_set_profiling", "dk_get_profile",
+           "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite", "dk_num_rows", "dk_set_profiling", "dk_get_profile",
            "dk_reset_profile", "dk_last_error", "dk_abi_version")
 
 
@@ -113,6 +113,9 @@ def load():
     L.dk_result_region_layout.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(dk_region_layout)]
     L.dk_set_result_region.argtypes = [vp, vp, C.c_uint64, C.c_uint64]
     L.dk_compare_rows.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
+    L.dk_compare_values.argtypes = [vp, C.POINTER(dk_batch), C.POINTER(C.c_double)]
+    L.dk_set_overwrite.argtypes = [vp, C.c_int]
+    L.dk_property_similarity.argtypes = [vp, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
     L.dk_num_rows.argtypes = [vp]
     L.dk_num_rows.restype = C.c_uint64
     L.dk_set_profiling.argtypes = [vp, C.c_int]
@@ -120,7 +123,9 @@ def load():
     L.dk_reset_profile.argtypes = [vp]
     L.dk_last_error.restype = C.c_char_p
     L.dk_abi_version.restype = C.c_int
-    for f in ("dk_create", "dk_upsert", "dk_match", "dk_compare_rows", "dk_set_profiling",
+    for f in ("dk_create", "dk_upsert", "dk_upsert_transient", "dk_drop_transient", "dk_match",
+              "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite",
+              "dk_set_profiling",
               "dk_result_region_layout", "dk_set_result_region",
               "dk_get_profile", "dk_reset_profile"):
         getattr(L, f).restype = C.c_int

@@ -117,6 +117,39 @@ class DukeConfig:
     def scored_properties(self):
         return [p for p in self.properties if p.scored()]
 
+    def to_dict(self):
+        """JSON-able form (committed fixtures; the Java shim passes the same fields)."""
+        def comp(c):
+            if c is None:
+                return None
+            return {"class": c.klass, "params": {k: (comp(v) if isinstance(v, Comparator) else v)
+                                                 for k, v in c.params.items()}}
+        return {"threshold": self.threshold, "maybe_threshold": self.maybe_threshold,
+                "linkage": self.linkage,
+                "properties": [{"name": p.name, "comparator": comp(p.comparator), "low": p.low,
+                                "high": p.high, "is_id": p.is_id, "ignore": p.ignore}
+                               for p in self.properties],
+                "data_sources": [{"dataset_id": d.dataset_id, "group_no": d.group_no,
+                                  "columns": [{"name": c.name, "property": c.property,
+                                               "cleaner": c.cleaner} for c in d.columns]}
+                                 for d in self.data_sources]}
+
+    @classmethod
+    def from_dict(cls, d):
+        def comp(c):
+            if c is None:
+                return None
+            return Comparator(c["class"], {k: (comp(v) if isinstance(v, dict) else v)
+                                           for k, v in c.get("params", {}).items()})
+        props = [Property(p["name"], comp(p["comparator"]), p["low"], p["high"],
+                          p.get("is_id", False), p.get("ignore", False)) for p in d["properties"]]
+        sources = [DataSource(s["dataset_id"], [DataSourceColumn(c["name"], c["property"],
+                                                                 c.get("cleaner"))
+                                                for c in s["columns"]], s.get("group_no"))
+                   for s in d["data_sources"]]
+        return cls(props, d["threshold"], d.get("maybe_threshold", 0.0), sources,
+                   d.get("linkage", False))
+
     def comparison_order(self):
         """Scored properties in Processor.compare's visiting order: the key order of the
         record's java.util.HashMap (RecordImpl), whose keys are the data source's column
@@ -132,9 +165,30 @@ class DukeConfig:
                 names.append(p.name)
         synth = ([GROUP_NO_PROPERTY_NAME] if self.linkage else []) + [
             ID_PROPERTY, ORIGINAL_ENTITY_ID_PROPERTY_NAME, DATASET_ID_PROPERTY_NAME]
+        # A HashMap keeps capacity 16 up to 12 keys; past that its capacity (and so its
+        # iteration order) depends on how many values a record holds, and computeBayes is
+        # not associative: the GPU path runs one fixed order, so such schemas are not
+        # eligible.  (+1: dukeDeleted is added for deleted entities.)
+        if len(names + synth) + 1 > 12:
+            raise UnsupportedComparator(
+                f"{len(names + synth) + 1} record properties: past 12 a record's HashMap "
+                "order depends on its value count (not GPU-eligible)")
         order = java_hashmap_order(names + synth)
         scored = {p.name: p for p in self.scored_properties()}
-        return [scored[n] for n in order if n in scored]
+        out = [scored[n] for n in order if n in scored]
+        # every data source must give its records the same visiting order (a different
+        # column order only matters for keys sharing a HashMap bucket)
+        for ds in self.data_sources[1:]:
+            alt = []
+            for c in ds.columns:
+                if c.property not in alt:
+                    alt.append(c.property)
+            alt += [p.name for p in self.scored_properties() if p.name not in alt]
+            if [n for n in java_hashmap_order(alt + synth) if n in scored] != [p.name for p in out]:
+                raise UnsupportedComparator(
+                    f"data source {ds.dataset_id!r} orders the record's properties differently "
+                    "(HashMap bucket collision): one fixed comparison order does not hold")
+        return out
 
     def to_schema(self, mode, nkeys):
         props = self.comparison_order()

@@ -185,6 +185,26 @@ class GpuEngine:
         A.check(self.lib.dk_compare_rows(self.ctx, int(r1), int(r2), C.byref(out)))
         return out.value
 
+    def compare_values(self, columns):
+        """dk_compare_values: Processor.compare(r1, r2) of two records given as columns of
+        two values each (schema order; None = no value).  The index is not touched."""
+        cols = (A.dk_column * max(1, len(columns)))(*[c.c() for c in columns])
+        ident = np.zeros(2, np.uint64)
+        b = A.dk_batch(2, ident.ctypes.data, None, None, cols, None, None)
+        out = C.c_double()
+        A.check(self.lib.dk_compare_values(self.ctx, C.byref(b), C.byref(out)))
+        return out.value
+
+    def set_overwrite(self, on):
+        A.check(self.lib.dk_set_overwrite(self.ctx, 1 if on else 0))
+
+    def property_similarity(self, prop, r1, r2):
+        """dk_property_similarity: Comparator.compare of schema property `prop` (index into
+        the schema order) for two indexed rows; NaN when either value is missing/empty."""
+        out = C.c_double()
+        A.check(self.lib.dk_property_similarity(self.ctx, int(prop), int(r1), int(r2), C.byref(out)))
+        return out.value
+
     def set_profiling(self, on):
         A.check(self.lib.dk_set_profiling(self.ctx, 1 if on else 0))
 
@@ -231,7 +251,10 @@ class GpuBlockingDatabase:
             self.drop_transient()
 
     def set_overwrite(self, overwrite):
+        """Database.setOverwrite (IncrementalLuceneDatabase.java:99): with overwrite on,
+        index() adds a record without first deleting the previous version by ID (:515)."""
         self.overwrite = bool(overwrite)
+        self.engine.set_overwrite(self.overwrite)
 
     def is_in_memory(self):
         return True
@@ -284,8 +307,14 @@ class GpuBlockingDatabase:
             cols.append(A.Column.from_strings(vals))
         group = None
         if self.mode == A.MODE_LINKAGE:
-            group = np.array([int(r.get_value(GROUP_NO_PROPERTY_NAME) or 0) for r in records],
-                             dtype=np.uint8)
+            # dukeGroupNo is "1" or "2" (IncrementalDataSource.java:80-84); a record without
+            # it makes findCandidateMatches throw (IncrementalLuceneDatabase.java:469-471)
+            gs = [r.get_value(GROUP_NO_PROPERTY_NAME) for r in records]
+            bad = [g for g in gs if g not in ("1", "2")]
+            if bad:
+                raise ValueError(f"The '{GROUP_NO_PROPERTY_NAME}' property was missing or not "
+                                 f"1/2: {bad[0]!r}")
+            group = np.array([int(g) for g in gs], dtype=np.uint8)
         deleted = np.array([r.get_value(DELETED_PROPERTY_NAME) == "true" for r in records],
                            dtype=np.uint8)
         key_cols = None
@@ -335,8 +364,13 @@ class GpuProcessor:
         records = list(records)
         for l in self.listeners:
             l.batch_ready(len(records))
-        rows = self.database.index_batch(records)
-        res = self.database.engine.match(rows)
+        # index every record, then commit (IncrementalLuceneDatabase.java:498-575, 146-165):
+        # records handed to database.index() beforehand -- the deleted records of
+        # App.java:988-1001, 1121-1137 -- become visible in the same commit
+        db = self.database
+        pending, db.pending = db.pending, []
+        rows = db.index_batch(pending + records)[len(pending):]
+        res = db.engine.match(rows)
         self._replay(records, res)
         for l in self.listeners:
             l.batch_done()
@@ -362,9 +396,15 @@ class GpuProcessor:
                         l.matches_perhaps(r, cand, p)
 
     def compare(self, r1: Record, r2: Record):
-        """[Duke 1.2] Processor.compare for two indexed records."""
-        a = self.database.by_id.get(r1.get_value(ID_PROPERTY))
-        b = self.database.by_id.get(r2.get_value(ID_PROPERTY))
-        if a is None or b is None:
-            raise ValueError("GpuProcessor.compare needs both records indexed")
-        return self.database.engine.compare_rows(a, b)
+        """[Duke 1.2] Processor.compare(r1, r2) for any two records (indexed or not):
+        dk_compare_values on their values; the index is not changed."""
+        cols = []
+        for p in self.database.props:
+            vals = []
+            for r in (r1, r2):
+                vs = r.get_values(p.name)
+                if len(vs) > 1:
+                    raise ValueError(f"property {p.name}: {len(vs)} values (GPU path holds one)")
+                vals.append(vs[0] if vs else None)
+            cols.append(A.Column.from_strings(vals))
+        return self.database.engine.compare_values(cols)

@@ -1,0 +1,443 @@
+"""GPU parity on BASELINE.json's configurations and the reference's own schema, the
+committed golden fixtures pushed through the production kernel, and the C-ABI boundary
+contracts (failure-atomic upsert, single-pair compares that leave the index alone).
+
+Oracle: oracle/duke_oracle.c (PARITY UNPINNED against Duke 1.2 itself, see its header);
+fixtures: tests/golden/*.jsonl (tests/gen_golden.py) and testdukeconfig_schema.json
+(tests/gen_reference_schema.py, the reference's src/main/resources/testdukeconfig.xml).
+"""
+import json
+import math
+import os
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import oracle as O
+import dukehip as dh
+from dukehip import _abi as A
+from dukehip import dist as dshard
+from dukehip import synth
+from dukehip.config import DukeConfig, DUKE_CMP
+from test_gpu_parity import schema_of, run_both, assert_same, persons_case
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+LEV, JW, QG, EX, NUM = A.CMP_LEVENSHTEIN, A.CMP_JAROWINKLER, A.CMP_QGRAM, A.CMP_EXACT, A.CMP_NUMERIC
+WL, DICE_T, JACC_T = A.CMP_WEIGHTED_LEVENSHTEIN, A.CMP_DICE_TOKENS, A.CMP_JACCARD_TOKENS
+
+
+def oracle_props(props):
+    """dukehip.config.Property list (schema order) -> oracle property dicts."""
+    out = []
+    for p in props:
+        c = p.comparator.to_c(p.low, p.high)
+        out.append({"comparator": c.comparator, "low": c.low, "high": c.high, "q": c.qgram_q,
+                    "formula": c.qgram_formula, "tokenizer": c.qgram_tokenizer,
+                    "min_ratio": c.min_ratio})
+    return out
+
+
+def alive_after(ident, upto):
+    alive = np.ones(upto, np.uint8)
+    last = {}
+    for r in range(upto):
+        if ident[r] in last:
+            alive[last[ident[r]]] = 0
+        last[ident[r]] = r
+    return alive
+
+
+# ---------------------------------------------------------------------------------------
+# configs[0]: the reference's Deduplication pipeline (testdukeconfig.xml) over the stress
+# test's shape (sesam_node_deduplication_stresstest_config.conf.json:18-71: 2 x 10,000
+# fake entities, country = first name, capital = last name, area in 1..10, ids drawn from
+# a 1..1,000,000 pool), posted in HTTP batches through GpuProcessor.deduplicate.
+# Blocking contract (stated; the reference itself uses Lucene): key = NAME[0:3].
+# ---------------------------------------------------------------------------------------
+def stress_entities(n, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    first = synth._vocab(rng, 3000, 1, 3)
+    last = synth._vocab(rng, 8000, 2, 3)
+    fi = synth._zipf_choice(rng, len(first), 1.1, n)
+    li = synth._zipf_choice(rng, len(last), 1.07, n)
+    ids = rng.integers(1, 1_000_001, n)
+    area = rng.integers(1, 11, n)
+    ents = []
+    for i in range(n):
+        e = {"_id": str(int(ids[i])), "country": first[fi[i]], "capital": last[li[i]],
+             "area": dh.records.JsonNumber(str(int(area[i]))), "id": str(int(ids[i]))}
+        if i % 97 == 5:
+            e["_deleted"] = True
+        ents.append(e)
+    return ents
+
+
+def test_reference_schema_dedup_gpu():
+    with open(os.path.join(GOLDEN, "testdukeconfig_schema.json")) as f:
+        cfg = DukeConfig.from_dict(json.load(f)["pipelines"]["Deduplication/countries-dbpedia-mondial"])
+    dbpedia, mondial = cfg.data_sources
+    kf = dh.PartsKey(("NAME", None, 0, 3))
+    db = dh.GpuBlockingDatabase(cfg, [kf])
+    proc = dh.GpuProcessor(cfg, db)
+    assert [p.name for p in db.props] == ["AREA", "CAPITAL", "NAME"]
+    batches = []
+    for src, seed in ((dbpedia, 1234), (mondial, 4321)):
+        ents = stress_entities(10_000, seed)
+        for a in range(0, len(ents), 2500):
+            batches.append(dh.records_from_entities(ents[a:a + 2500], src))
+    allrecs, ids, results = [], {}, []
+    for recs in batches:
+        res = proc.deduplicate(recs)
+        results.append((len(allrecs), len(allrecs) + len(recs), res))
+        allrecs += recs
+    props = oracle_props(db.props)
+    vals = [[r.get_value(p.name) for r in allrecs] for p in db.props]
+    ident = np.array([ids.setdefault(r.get_value("ID"), len(ids)) for r in allrecs], np.uint64)
+    deleted = np.array([r.get_value("dukeDeleted") == "true" for r in allrecs], np.uint8)
+    keys = [kf.make_key(r) for r in allrecs]
+    assert sum(r.get_value("CAPITAL") is None for r in allrecs) == 10_000   # "capical"
+    total = 0
+    for a, e, res in results:
+        ot = O.OracleTable(props, [v[:e] for v in vals], keys=[keys[:e]], ident=ident[:e],
+                           deleted=deleted[:e], alive=alive_after(list(ident), e),
+                           threshold=cfg.threshold, maybe=cfg.maybe_threshold)
+        assert_same(res, ot.match(np.arange(a, e, dtype=np.uint32)))
+        total += res.n
+    assert total > 1000
+    db.close()
+
+
+# ---------------------------------------------------------------------------------------
+# configs[2] (QGram DICE/JACCARD + Numeric min-ratio 0.9, cross-group key blocking) and
+# configs[4] (WeightedLevenshtein + QGram q=3 JACCARD, key = first two tokens) in linkage
+# ---------------------------------------------------------------------------------------
+def test_config2_linkage_qgram_numeric():
+    p, group = synth.linkage_persons(2500)
+    props = [{"comparator": QG, "low": 0.1, "high": 0.95, "q": 2, "formula": A.QGRAM_DICE},
+             {"comparator": QG, "low": 0.2, "high": 0.8, "q": 2, "formula": A.QGRAM_JACCARD},
+             {"comparator": NUM, "low": 0.3, "high": 0.7, "min_ratio": 0.9},
+             {"comparator": NUM, "low": 0.4, "high": 0.75, "min_ratio": 0.9}]
+    vals = [p["name"], p["address"], p["birthyear"], p["zip"]]
+    res, ref = run_both(props, vals, synth.keys_config2(p), mode="linkage", group=group,
+                        threshold=0.9, maybe=0.7, queries=np.arange(2500, len(group)))
+    assert res.n > 100
+    assert_same(res, ref)
+
+
+def test_config4_linkage_long_text():
+    texts, group = synth.long_texts(1000)
+    props = [{"comparator": WL, "low": 0.2, "high": 0.9},
+             {"comparator": QG, "low": 0.3, "high": 0.8, "q": 3, "formula": A.QGRAM_JACCARD}]
+    res, ref = run_both(props, [texts, texts], synth.keys_first_two_tokens(texts), mode="linkage",
+                        group=group, threshold=0.9, maybe=0.7, queries=np.arange(1000, len(group)))
+    assert res.n > 10
+    assert_same(res, ref)
+
+
+# ---------------------------------------------------------------------------------------
+# golden fixtures through the production kernel (dk_property_similarity)
+# ---------------------------------------------------------------------------------------
+def fx(v):
+    if v is None:
+        return None
+    return float.fromhex(v["hex"])
+
+
+GOLDEN_PROPS = {
+    "levenshtein": {"comparator": LEV},
+    "jarowinkler": {"comparator": JW},
+    "exact": {"comparator": EX},
+    "weighted_levenshtein": {"comparator": WL},
+    "dice_tokens": {"comparator": DICE_T},
+    "jaccard_tokens": {"comparator": JACC_T},
+    "qgram_q2_f1_ends": {"comparator": QG, "q": 2, "formula": 1, "tokenizer": A.QGRAM_ENDS},
+    "qgram_q3_f2_ends": {"comparator": QG, "q": 3, "formula": 2, "tokenizer": A.QGRAM_ENDS},
+    "qgram_q2_f1_positional": {"comparator": QG, "q": 2, "formula": 1, "tokenizer": A.QGRAM_POSITIONAL},
+}
+for _q in (1, 2, 3):
+    for _f in (0, 1, 2):
+        GOLDEN_PROPS[f"qgram_q{_q}_f{_f}"] = {"comparator": QG, "q": _q, "formula": _f}
+
+
+def load_jsonl(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return [json.loads(l) for l in f]
+
+
+def units_str(u):
+    return struct.pack(f"<{len(u)}H", *u).decode("utf-16-le", "surrogatepass")
+
+
+@pytest.mark.parametrize("fixture", ["comparators.jsonl", "long_values.jsonl"])
+def test_golden_fixtures_through_kernel(fixture):
+    rows = load_jsonl(fixture)
+    strs = []
+    for r in rows:
+        strs += [units_str(r["s1"]), units_str(r["s2"])]
+    keys = [k for k in GOLDEN_PROPS if k in rows[0]]
+    assert keys
+    checked = 0
+    for key in keys:
+        prop = dict(GOLDEN_PROPS[key], low=0.1, high=0.9)
+        eng = dh.GpuEngine(schema_of([prop], 0.9, 0.0, "allpairs", 0))
+        eng.upsert(len(strs), np.arange(len(strs)), [dh.Column.from_strings(strs)])
+        for i, r in enumerate(rows):
+            want = fx(r[key])
+            got = eng.property_similarity(0, 2 * i, 2 * i + 1)
+            if not r["s1"] or not r["s2"]:
+                assert math.isnan(got), (key, i)   # Processor never compares empty values
+                continue
+            if key == "levenshtein":
+                n1, n2 = len(r["s1"]), len(r["s2"])
+                cut = r["compact_distance"] > min(n1, n2) // 2
+                if cut and 2 * min(n1, n2) > max(n1, n2):
+                    # Duke's cutoff fired: the GPU reports maxdist+1; both similarities map
+                    # to <low> (PropertyImpl), the integer distance differs by design
+                    assert got < 0.5 and want < 0.5, (key, i, got, want)
+                    checked += 1
+                    continue
+                if want >= 0.5 and 2 * min(n1, n2) > max(n1, n2) and got != 1.0:
+                    # integer distance bit-exact: dist = len * (1 - sim)
+                    ln = min(n1, n2)
+                    assert round((1.0 - got) * ln) == min(r["compact_distance"], ln)
+            assert got == want or (math.isnan(got) and want is not None and math.isnan(want)), \
+                (key, i, got, want)
+            checked += 1
+        eng.close()
+    assert checked > len(rows)
+
+
+def java_numeric(d1, ok1, d2, ok2, min_ratio):
+    if not ok1 or not ok2:
+        return 0.5
+    if d1 == 0.0 and d2 == 0.0:
+        return 1.0
+    if d2 < d1:
+        d1, d2 = d2, d1
+    ratio = d1 / d2
+    return 0.0 if ratio < min_ratio else ratio
+
+
+def test_golden_numeric_through_kernel():
+    allrows = load_jsonl("numeric.jsonl")
+    # fixture pairs: NumericComparator.compare(s1, s2) at the row's min-ratio
+    pairs = [r for r in allrows if "s1" in r]
+    assert pairs
+    for mr in sorted({r["min_ratio"] for r in pairs}):
+        sel = [r for r in pairs if r["min_ratio"] == mr]
+        strs = []
+        for r in sel:
+            strs += [units_str(r["s1"]), units_str(r["s2"])]
+        eng = dh.GpuEngine(schema_of([{"comparator": NUM, "low": 0.1, "high": 0.9, "min_ratio": mr}],
+                                     0.9, 0.0, "allpairs", 0))
+        eng.upsert(len(strs), np.arange(len(strs)), [dh.Column.from_strings(strs)])
+        for i, r in enumerate(sel):
+            got = eng.property_similarity(0, 2 * i, 2 * i + 1)
+            if not r["s1"] or not r["s2"]:
+                assert math.isnan(got)
+                continue
+            want = fx(r["numeric"])
+            assert got == want or (math.isnan(got) and math.isnan(want)), (r, got)
+            assert math.copysign(1.0, got) == math.copysign(1.0, want) or math.isnan(got)
+        eng.close()
+    # parsed values (Double.parseDouble fixture) crossed at random
+    rows = [r for r in allrows if "parse" in r]
+    strs = [units_str(r["parse"]) for r in rows]
+    parsed = [(fx(r["value"]) if r["value"] is not None else 0.0, r["value"] is not None) for r in rows]
+    eng = dh.GpuEngine(schema_of([{"comparator": NUM, "low": 0.1, "high": 0.9, "min_ratio": 0.7}],
+                                 0.9, 0.0, "allpairs", 0))
+    eng.upsert(len(strs), np.arange(len(strs)), [dh.Column.from_strings(strs)])
+    rng = random.Random(3)
+    pairs = [(i, i + 1) for i in range(len(rows) - 1)] + [
+        (rng.randrange(len(rows)), rng.randrange(len(rows))) for _ in range(2000)]
+    for a, b in pairs:
+        got = eng.property_similarity(0, a, b)
+        if not strs[a] or not strs[b]:
+            assert math.isnan(got)
+            continue
+        want = java_numeric(parsed[a][0], parsed[a][1], parsed[b][0], parsed[b][1], 0.7)
+        assert got == want or (math.isnan(got) and math.isnan(want)), (strs[a], strs[b], got, want)
+    eng.close()
+
+
+# ---------------------------------------------------------------------------------------
+# boundary contracts
+# ---------------------------------------------------------------------------------------
+def upsert_slice(eng, vals, keys, ident, a, b, deleted=None):
+    return eng.upsert(b - a, ident[a:b], [dh.Column.from_strings(v[a:b]) for v in vals],
+                      deleted=None if deleted is None else deleted[a:b],
+                      key_columns=[dh.Column.from_strings(k[a:b]) for k in keys])
+
+
+def test_failed_upsert_leaves_index_unchanged():
+    """A batch rejected by dk_upsert (a Levenshtein value over 256 units) that re-posts
+    already indexed IDs must not tombstone them; a valid re-post of those IDs in shuffled
+    positions afterwards supersedes them exactly once (Lucene delete-then-add)."""
+    p, props, vals, keys = persons_case(600, 200, 31)
+    n = len(vals[0])
+    eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", 2))
+    ident = np.arange(n, dtype=np.uint64)
+    upsert_slice(eng, vals, keys, ident, 0, 500)
+    # batch 2: IDs 0..59 again + new ones, and one over-long ADDRESS value
+    perm = np.random.default_rng(1).permutation(60)
+    b_ident = np.r_[perm, np.arange(500, n)].astype(np.uint64)
+    b_vals = [[v[i] for i in perm] + v[500:] for v in vals]
+    b_keys = [[k[i] for i in perm] + k[500:] for k in keys]
+    bad = [list(col) for col in b_vals]
+    bad[1][7] = "x" * 300
+    with pytest.raises(dh.DukeHipError) as e:
+        eng.upsert(len(b_ident), b_ident, [dh.Column.from_strings(v) for v in bad],
+                   key_columns=[dh.Column.from_strings(k) for k in b_keys])
+    assert e.value.code == A.DK_E_UNSUPPORTED
+    assert eng.num_rows == 500
+    # the index is as before: compare with the oracle over the first batch
+    q = np.arange(500, dtype=np.uint32)
+    ot = O.OracleTable(props, [v[:500] for v in vals], keys=[k[:500] for k in keys],
+                       threshold=0.9, maybe=0.7)
+    assert_same(eng.match(q), ot.match(q))
+    # the valid batch: rows 500.. hold IDs perm + 500..n-1
+    eng.upsert(len(b_ident), b_ident, [dh.Column.from_strings(v) for v in b_vals],
+               key_columns=[dh.Column.from_strings(k) for k in b_keys])
+    full_vals = [v[:500] + bv for v, bv in zip(vals, b_vals)]
+    full_keys = [k[:500] + bk for k, bk in zip(keys, b_keys)]
+    full_ident = np.r_[ident[:500], b_ident].astype(np.uint64)
+    m = len(full_ident)
+    ot = O.OracleTable(props, full_vals, keys=full_keys, ident=full_ident,
+                       alive=alive_after(list(full_ident), m), threshold=0.9, maybe=0.7)
+    q = np.arange(m, dtype=np.uint32)
+    assert_same(eng.match(q), ot.match(q))
+    eng.close()
+
+
+def test_compare_rows_then_match_then_compare_rows():
+    """dk_compare_rows uses private scratch: the cached blocking tables stay valid."""
+    p, props, vals, keys = persons_case(700, 300, 32)
+    n = len(vals[0])
+    eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", 2))
+    ident = np.arange(n, dtype=np.uint64)
+    upsert_slice(eng, vals, keys, ident, 0, n)
+    ot = O.OracleTable(props, vals, keys=keys, threshold=0.9, maybe=0.7)
+    q = np.arange(n, dtype=np.uint32)
+    ref = ot.match(q)
+    assert_same(eng.match(q), ref)             # builds the tables
+    pairs = [(0, 1), (5, 9), (17, 17), (n - 1, 3), (42, 400)]
+    for a, b in pairs:
+        assert eng.compare_rows(a, b) == ot.compare_rows(a, b)
+    assert_same(eng.match(q), ref)             # reuses the tables
+    for a, b in pairs:
+        assert eng.compare_rows(b, a) == ot.compare_rows(b, a)
+    assert_same(eng.match(q[::3]), ot.match(q[::3]))
+    eng.close()
+
+
+def test_compare_values_unindexed_records():
+    rng = random.Random(33)
+    props = [{"comparator": JW, "low": 0.1, "high": 0.95},
+             {"comparator": LEV, "low": 0.2, "high": 0.8},
+             {"comparator": WL, "low": 0.1, "high": 0.9},
+             {"comparator": QG, "low": 0.2, "high": 0.8, "q": 3, "formula": 1},
+             {"comparator": NUM, "low": 0.3, "high": 0.7, "min_ratio": 0.5}]
+    eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", 1))
+    eng.upsert(2, [0, 1], [dh.Column.from_strings(["zz", "zy"]) for _ in props],
+               key_columns=[dh.Column.from_strings(["k", "k"])])
+    alpha = "abcdeł\U0001F600 "
+    for t in range(60):
+        def val(i):
+            if rng.random() < 0.1:
+                return None
+            if i == 4:
+                return str(rng.randint(0, 30))
+            return "".join(rng.choice(alpha) for _ in range(rng.randint(1, 90 if i == 2 else 20)))
+        r1 = [val(i) for i in range(len(props))]
+        r2 = [v if (v is not None and rng.random() < 0.4) else val(i) for i, v in enumerate(r1)]
+        got = eng.compare_values([dh.Column.from_strings([a, b]) for a, b in zip(r1, r2)])
+        ot = O.OracleTable(props, [[a, b] for a, b in zip(r1, r2)], keys=[["k", "k"]])
+        want = ot.compare_rows(0, 1)
+        assert got == want or (math.isnan(got) and math.isnan(want)), (t, r1, r2, got, want)
+    assert eng.num_rows == 2                      # the ctx's index is untouched
+    eng.close()
+
+
+def test_processor_compare_and_deduplicate_flush_pending():
+    """GpuProcessor.compare on unindexed records; records handed to Database.index()
+    before deduplicate (App.java:988-1001) are committed with the batch."""
+    cfg = dh.DukeConfig([dh.Property("NAME", dh.Comparator(DUKE_CMP + "Levenshtein"), 0.1, 0.9)],
+                        threshold=0.6, maybe_threshold=0.5)
+    db = dh.GpuBlockingDatabase(cfg, [dh.PartsKey(("NAME", None, 0, 1))])
+    proc = dh.GpuProcessor(cfg, db)
+    a = dh.Record({"ID": "d__1", "NAME": "anna"})
+    b = dh.Record({"ID": "d__2", "NAME": "anne"})
+    ot = O.OracleTable([{"comparator": LEV, "low": 0.1, "high": 0.9}], [["anna", "anne"]],
+                       keys=[["a", "a"]])
+    assert proc.compare(a, b) == ot.compare_rows(0, 1)
+    proc.deduplicate([a, b])
+    lis = dh.CollectingListener()
+    proc.add_match_listener(lis)
+    gone = dh.Record({"ID": "d__2", "NAME": "anne", "dukeDeleted": "true"})
+    db.index(gone)                                # deleted version of d__2
+    proc.deduplicate([dh.Record({"ID": "d__3", "NAME": "annu"})])
+    assert db.pending == []
+    hits = [e for e in lis.events if e[0] in ("matches", "matchesPerhaps")]
+    assert hits and all(e[2] != "d__2" for e in hits)   # d__2 is deleted: not a candidate
+    assert any(e[2] == "d__1" for e in hits)
+    db.close()
+
+
+def test_overwrite_keeps_older_versions():
+    p, props, vals, keys = persons_case(300, 100, 34)
+    n = len(vals[0])
+    ident = np.arange(n, dtype=np.uint64)
+    ident[350:] = ident[:50]
+    eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", 2))
+    eng.set_overwrite(True)
+    upsert_slice(eng, vals, keys, ident, 0, 300)
+    upsert_slice(eng, vals, keys, ident, 300, n)
+    ot = O.OracleTable(props, vals, keys=keys, ident=ident, threshold=0.9, maybe=0.7)
+    q = np.arange(n, dtype=np.uint32)
+    assert_same(eng.match(q), ot.match(q))
+    eng.close()
+
+
+def test_linkage_group_validated():
+    cfg = dh.DukeConfig([dh.Property("NAME", dh.Comparator(DUKE_CMP + "Levenshtein"), 0.1, 0.9)],
+                        threshold=0.6, linkage=True)
+    db = dh.GpuBlockingDatabase(cfg, [dh.PartsKey(("NAME", None, 0, 1))])
+    with pytest.raises(ValueError):
+        db.index_batch([dh.Record({"ID": "1__a__1", "NAME": "x"})])
+    eng = db.engine
+    with pytest.raises(dh.DukeHipError) as e:
+        eng.upsert(2, [0, 1], [dh.Column.from_strings(["a", "b"])], group=[1, 3],
+                   key_columns=[dh.Column.from_strings(["a", "b"])])
+    assert e.value.code == A.DK_E_INVALID and eng.num_rows == 0
+    db.close()
+
+
+def test_two_engines_tiles_equal_single_engine():
+    """Two dk_ctx on one device, each matching its query tile of a replicated index:
+    concat_ranks of their lists equals the single-engine list bit for bit."""
+    p, props, vals, keys = persons_case(1500, 500, 35)
+    n = len(vals[0])
+    ident = np.arange(n, dtype=np.uint64)
+    engs = [dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", 2)) for _ in range(3)]
+    for e in engs:
+        upsert_slice(e, vals, keys, ident, 0, n)
+    q = np.arange(n, dtype=np.uint32)
+    full = engs[0].match(q)
+    lists = []
+    for r, e in enumerate(engs[1:]):
+        a, b = dshard.tile(n, r, 2)
+        res = e.match(q[a:b])
+        lists.append({"first": res.first.copy(), "candidate": res.candidate.copy(),
+                      "prob": res.prob.copy(), "kind": res.kind.copy()})
+        res.close()
+    cat = dshard.concat_ranks(lists)
+    assert np.array_equal(cat["first"], full.first.astype(np.int64))
+    for k in ("candidate", "prob", "kind"):
+        assert np.array_equal(cat[k], getattr(full, k))
+    for e in engs:
+        e.close()
