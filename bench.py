@@ -451,9 +451,9 @@ def cpu_baseline(w, gpu_res, args):
     allq = w["queries"]
 
     def sample(nthreads, seconds):
-        probe = min(len(allq), 2000 if mode != "allpairs" else 64)
+        probe = min(len(allq), max(2000, 64 * nthreads) if mode != "allpairs" else max(64, 2 * nthreads))
         if nthreads == 1:
-            probe = max(1, probe // 16)
+            probe = max(1, min(probe, 2000) // 16)
         r = ot.match(allq[:probe], nthreads=nthreads)
         rate = r["pairs_scored"] / max(r["ms_score"] / 1e3, 1e-9)
         per_q = r["pairs_scored"] / probe

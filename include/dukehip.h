@@ -153,6 +153,8 @@ typedef struct dk_profile {
   uint64_t pairs_generated;
   uint64_t score_bytes;   /* algorithmic operand bytes of the scored pairs */
   double ms_copy;         /* device->host copies of the match list (copy stream, overlapped) */
+  double ms_emit;         /* symmetric dedup schedule: the emission pass (k_emit) */
+  uint64_t sym_matches;   /* dk_match calls that ran the symmetric dedup schedule */
 } dk_profile;
 
 typedef struct dk_ctx dk_ctx;

@@ -306,6 +306,10 @@ struct dk_ctx {
   const uint32_t* rowof_p = nullptr;  // replica position -> row (rowof, or usable in ALLPAIRS)
   uint64_t rstride = 0;               // replica positions
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
+  // symmetric dedup schedule: owner slot counts / offsets / wave map,
+  // per-(key, query) bucket positions, owner results, chunk boundaries
+  DevBuf ocounts, oqoff, owq, obase, ores, bidx, bval;
+  PinnedBuf h_bounds;
   DevBuf counters;
   struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx; };
   StageBufs stage[2];                          // double-buffered per-chunk staging
@@ -1025,8 +1029,28 @@ static int build_usable(dk_ctx* c, uint64_t* m_out) {
   return DK_OK;
 }
 
+static bool sym_enabled() {
+  const char* e = getenv("DK_SYM");
+  return !(e && e[0] == '0');
+}
+
+// The symmetric schedule holds when every comparator gives compare(a, b) and compare(b, a)
+// the same PropertyImpl probability, or (JaroWinkler) the kernel computes both directions:
+// Levenshtein (the cutoff only moves a < 0.5 similarity), QGram, Exact, Numeric, none.
+// WeightedLevenshtein's stride aliasing and the token comparators' "shorter list first"
+// are orientation dependent; the long-value kernels are not instantiated for it.
+static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
+  if (c->schema.mode != DK_MODE_DEDUP || P.long_rows > 0) return false;
+  for (const auto& S : c->P) {
+    const int op = S.cfg.comparator;
+    if (op == DK_CMP_WEIGHTED_LEVENSHTEIN || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS)
+      return false;
+  }
+  return true;
+}
+
 static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
-                     ResultHolder* R) {
+                     ResultHolder* R, bool contiguous) {
   hipStream_t s = c->stream;
   c->spans.clear();   // left over by a failed call
   c->ev_next = 0;
@@ -1095,8 +1119,53 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
 
   // ---- candidate counts per query -> slot offsets ----
   Timer t_gen(c, &c->prof.ms_generate, s);
-  uint64_t total = 0, generated = 0, mpad = 0;
-  if (!allpairs) {
+  uint64_t total = 0, generated = 0, mpad = 0, otot = 0;
+  const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
+  bool sym = contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
+  const uint32_t r0 = nq ? query_rows[0] : 0;
+  uint64_t* hs = c->h_small.as<uint64_t>();
+  if (sym) {
+    HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 16 + 16, 0, s));
+    HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
+    HIPCHK(c->ocounts.reserve((nq + 1) * 8, 0, s));
+    HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
+    HIPCHK(c->oqoff.reserve((nq + 1) * 8, 0, s));
+    HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
+    HIPCHK(launch_count_sym(c->d_queries.as<uint32_t>(), nq, T, r0, c->ranges.as<uint4>(),
+                            c->counts.as<uint64_t>(), c->ocounts.as<uint64_t>(),
+                            c->counters.as<uint64_t>() + 2, s));
+    HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
+    HIPCHK(hipMemsetAsync(c->ocounts.as<uint64_t>() + nq, 0, 8, s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
+    }));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return exclusive_scan_u64(t, b, c->ocounts.as<uint64_t>(), c->oqoff.as<uint64_t>(), nq + 1, s);
+    }));
+    HIPCHK(hipMemcpyAsync(&hs[3], c->qoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&hs[2], c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&hs[1], c->oqoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    total = hs[3];
+    generated = hs[2];
+    otot = hs[1];
+    // the owner results live for the whole call (a pair is read back by a later query's
+    // emission): 16 B per owner slot, within a third of the free HBM, else no symmetry
+    size_t fr = 0, tot_mem = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot_mem));
+    const size_t need = otot * 16 + 64;
+    if (need > c->ores.bytes && need - c->ores.bytes > fr / 3) sym = false;
+  }
+  if (sym) {
+    HIPCHK(c->ores.reserve(otot * 16 + 64, 0, s));
+    HIPCHK(c->wq.reserve(total / 64 * 4 + 4, 0, s));
+    HIPCHK(c->owq.reserve(otot / 64 * 4 + 4, 0, s));
+    HIPCHK(c->obase.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
+    HIPCHK(launch_wavemap(c->qoff.as<uint64_t>(), nq, c->wq.as<uint32_t>(), s));
+    HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s));
+    HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), nq, nk,
+                        c->obase.as<uint64_t>(), s));
+  } else if (!allpairs) {
     HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
     HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
@@ -1107,7 +1176,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
     }));
-    uint64_t* hs = c->h_small.as<uint64_t>();
     HIPCHK(hipMemcpyAsync(&hs[3], c->qoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&hs[2], c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -1121,11 +1189,54 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     total = nq * mpad;
     generated = nq * M;
   }
+  const uint64_t CH = (chunk_slots() + kScoreBlock - 1) / kScoreBlock * kScoreBlock;
+  // chunk boundaries in slots: full chunks, then (host modes) the last two chunks' worth
+  // halved down to CH/16, so the copy of the final chunk's entries (not overlapped with
+  // scoring) is short.  The symmetric schedule cuts by queries instead (an emission chunk
+  // reads the owner results of its own and earlier queries): bounds = full slots and
+  // obounds = owner slots at the same query boundaries.
+  std::vector<uint64_t> bounds{0}, obounds;
+  if (sym) {
+    std::vector<uint64_t> qb{0};
+    const uint64_t nch = std::max<uint64_t>(1, (total + CH - 1) / CH);
+    for (uint64_t i = 1; i < nch; ++i) qb.push_back(nq * i / nch);
+    qb.push_back(nq);
+    if (!(flags & DK_MATCH_DEVICE)) {  // halve the last chunk twice
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t a = qb[qb.size() - 2], e = qb.back();
+        if (e - a >= 2) qb.insert(qb.end() - 1, a + (e - a) / 2);
+      }
+    }
+    const uint64_t nb = qb.size();
+    HIPCHK(c->bidx.reserve(nb * 8 + 8, 0, s));
+    HIPCHK(c->bval.reserve(2 * nb * 8 + 8, 0, s));
+    HIPCHK(c->h_bounds.reserve(2 * nb * 8 + 8));
+    uint64_t* hb = c->h_bounds.as<uint64_t>();
+    memcpy(hb, qb.data(), nb * 8);
+    HIPCHK(hipMemcpyAsync(c->bidx.p, hb, nb * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_gather_u64(c->qoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb, c->bval.as<uint64_t>(), s));
+    HIPCHK(launch_gather_u64(c->oqoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb,
+                             c->bval.as<uint64_t>() + nb, s));
+    HIPCHK(hipMemcpyAsync(hb, c->bval.p, 2 * nb * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    bounds.assign(hb, hb + nb);
+    obounds.assign(hb + nb, hb + 2 * nb);
+  } else {
+    const uint64_t min_chunk = std::max<uint64_t>(kScoreBlock, CH / 16 / kScoreBlock * kScoreBlock);
+    uint64_t at = 0;
+    while (at < total) {
+      const uint64_t rem = total - at;
+      uint64_t len = rem > CH ? CH : rem;
+      if (rem <= 2 * CH && rem > min_chunk && !(flags & DK_MATCH_DEVICE))
+        len = std::max(min_chunk, (rem / 2 + kScoreBlock - 1) / kScoreBlock * kScoreBlock);
+      at = std::min(total, at + len);
+      bounds.push_back(at);
+    }
+  }
   t_gen.stop();
 
-  const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
-  const uint64_t CH = (chunk_slots() + kScoreBlock - 1) / kScoreBlock * kScoreBlock;
-  const uint64_t chunk = std::min(CH, std::max<uint64_t>(total, 1));
+  uint64_t chunk = 1;
+  for (size_t i = 0; i + 1 < bounds.size(); ++i) chunk = std::max(chunk, bounds[i + 1] - bounds[i]);
   const uint64_t nblk_max = (chunk + kScoreBlock - 1) / kScoreBlock;
   // two staging sets: chunk i+1 scores into one while chunk i's entries are compacted
   // out of the other, so the host never waits between score launches
@@ -1146,21 +1257,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * sizeof(uint64_t), s));
   ResultBufs& B = *R->bufs;
   uint64_t nm = 0;  // entries so far
-  // chunk boundaries: full chunks, then the last two chunks' worth halved down to CH/16, so
-  // the copy of the final chunk's entries (not overlapped with scoring) is short
-  std::vector<uint64_t> bounds{0};
-  {
-    const uint64_t min_chunk = std::max<uint64_t>(kScoreBlock, CH / 16 / kScoreBlock * kScoreBlock);
-    uint64_t at = 0;
-    while (at < total) {
-      const uint64_t rem = total - at;
-      uint64_t len = rem > CH ? CH : rem;
-      if (rem <= 2 * CH && rem > min_chunk && !(flags & DK_MATCH_DEVICE))
-        len = std::max(min_chunk, (rem / 2 + kScoreBlock - 1) / kScoreBlock * kScoreBlock);
-      at = std::min(total, at + len);
-      bounds.push_back(at);
-    }
-  }
   PairSource src{};
   src.queries = c->d_queries.as<uint32_t>();
   src.m = M;
@@ -1179,7 +1275,29 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       src.rkeys[k] = c->rkeys[k].as<uint64_t>();
     }
   }
-  uint64_t* hs = c->h_small.as<uint64_t>();
+  EmitSource esrc{};
+  if (sym) {
+    // owner slots: phase 1 scores them into ores; the emission pass walks the full slots
+    src.sym = 1;
+    src.wq = c->owq.as<uint32_t>();
+    src.qoff = c->oqoff.as<uint64_t>();
+    src.sranges = c->ranges.as<uint4>();
+    src.ores = c->ores.as<double>();
+    src.r0 = r0;
+    src.r1 = r0 + (uint32_t)nq;
+    esrc.wq = c->wq.as<uint32_t>();
+    esrc.qoff = c->qoff.as<uint64_t>();
+    esrc.sranges = c->ranges.as<uint4>();
+    esrc.obase = c->obase.as<uint64_t>();
+    esrc.ores = c->ores.as<double>();
+    esrc.rowof = c->rowof.as<uint32_t>();
+    esrc.nq = nq;
+    esrc.m = M;
+    esrc.nkeys = nk;
+    esrc.r0 = r0;
+    esrc.threshold = P.threshold;
+    esrc.maybe = P.maybe;
+  }
   hipStream_t cs = c->copy_stream;
   // Chunk ci scores on the main stream; its block-ordered compaction onto the match list and
   // (host modes) the copy of its entries run on the copy stream, beside the next chunk's
@@ -1245,12 +1363,27 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     const uint64_t s0 = bounds[ci], s1 = bounds[ci + 1];
     const uint64_t nblk = (s1 - s0 + kScoreBlock - 1) / kScoreBlock;
     if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging b drained
-    {
-      Timer t_score(c, &c->prof.ms_score, s);
-      HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
-      t_score.stop();
+    if (sym) {
+      // phase 1: the chunk's owner slots, both directions of every owned pair -> ores
+      const uint64_t o0 = obounds[ci], o1 = obounds[ci + 1];
+      {
+        Timer t_score(c, &c->prof.ms_score, s);
+        HIPCHK(launch_score(P, src, o0, o1 - o0, st[b], s));
+        t_score.stop();
+      }
+      HIPCHK(launch_reduce_blocks(st[b], (o1 - o0 + kScoreBlock - 1) / kScoreBlock, s));
+      // phase 2: the chunk's full slots in Duke's candidate order -> staged entries
+      Timer t_emit(c, &c->prof.ms_emit, s);
+      HIPCHK(launch_emit(esrc, s0, s1 - s0, st[b], s));
+      t_emit.stop();
+    } else {
+      {
+        Timer t_score(c, &c->prof.ms_score, s);
+        HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
+        t_score.stop();
+      }
+      HIPCHK(launch_reduce_blocks(st[b], nblk, s));
     }
-    HIPCHK(launch_reduce_blocks(st[b], nblk, s));
     c->prof.score_launches += 1;
     {
       Timer t_gather(c, &c->prof.ms_gather, s);
@@ -1279,6 +1412,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   HIPCHK(hipStreamSynchronize(s));
   const uint64_t scored = c->h_small.as<uint64_t>()[0];
   const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
+  if (sym) c->prof.sym_matches += 1;
   R->r.pairs_scored = scored;
   R->r.pairs_generated = generated;
   c->prof.pairs_scored += scored;
@@ -1323,10 +1457,13 @@ int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_r
   *out = nullptr;
   if (nq && !query_rows) return fail(DK_E_INVALID, "query_rows is NULL");
   if (flags & ~DK_MATCH_DEVICE) return fail(DK_E_INVALID, "unknown flags 0x%x", flags);
-  for (uint64_t i = 0; i < nq; ++i)
+  bool contiguous = true;  // query rows r0, r0+1, ... (Processor.deduplicate's batch)
+  for (uint64_t i = 0; i < nq; ++i) {
     if (query_rows[i] >= c->nrows)
       return fail(DK_E_INVALID, "query row %u not in the index (%llu rows)", query_rows[i],
                   (unsigned long long)c->nrows);
+    contiguous = contiguous && query_rows[i] == query_rows[0] + i;
+  }
   if (nq >= (1ull << 32)) return fail(DK_E_UNSUPPORTED, "too many queries");
   if (c->region.base && !(flags & DK_MATCH_DEVICE) && nq > c->region.max_queries)
     return fail(DK_E_INVALID, "%llu queries; the result region was laid out for %llu",
@@ -1338,7 +1475,7 @@ int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_r
   R->bufs = c->pool->take();
   R->device = c->device;
   R->stream = c->stream;
-  int rc = run_match(c, query_rows, nq, flags, R);
+  int rc = run_match(c, query_rows, nq, flags, R, contiguous);
   if (rc) {
     R->pool->give(std::move(R->bufs));
     delete R;

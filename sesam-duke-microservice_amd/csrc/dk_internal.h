@@ -107,7 +107,36 @@ struct PairSource {
   uint64_t m;               // usable rows (= replica positions per key function)
   uint64_t mpad;            // m rounded up to a wave (64)
   int32_t same_ok;          // score pairs of one identity too (dk_compare_rows)
-  int32_t pad;
+  int32_t sym;              // 1: owner slots of the symmetric dedup schedule (below)
+  // Symmetric dedup schedule: queries are the contiguous rows [r0, r1);
+  // per (key function k, query qi) sranges[k * nq + qi] = {lo, hi, qa, pq}: the bucket
+  // [lo, hi) of the query's key in sorted table k, qa = first position with row >= r0,
+  // pq = the query's own position (kNoPos when it is not in the table: then qa = hi).
+  // The query OWNS candidates [lo, qa) and (pq, hi): it scores them and, for those that
+  // are queries themselves, also the reverse direction; candidates in [qa, pq) are owned
+  // by those (earlier) queries.  Owner slot t of a query is its t-th owned candidate over
+  // k; qoff / wq then describe owner slots.  Results: ores[2 s] = compare(query, cand),
+  // ores[2 s + 1] = compare(cand, query) (NaN = filtered / no entry).
+  const uint4* sranges;
+  double* ores;
+  uint32_t r0, r1;
+};
+
+constexpr uint32_t kNoPos = 0xFFFFFFFFu;
+
+// The emission pass of the symmetric schedule: slots of the full candidate order (qoff /
+// wq / ranges as in PairSource) read their probability from the owner results.
+struct EmitSource {
+  const uint32_t* wq;
+  const uint64_t* qoff;
+  const uint4* sranges;
+  const uint64_t* obase;    // [k * nq + qi]: owner slot of candidate position qa of (k, qi)
+  const double* ores;
+  const uint32_t* rowof;
+  uint64_t nq, m;
+  int32_t nkeys;
+  uint32_t r0;
+  double threshold, maybe;
 };
 
 // Per-chunk staging of the score kernel.  Block b (256 slots) writes its emitted entries,
@@ -199,6 +228,17 @@ hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t npos, const uin
                                  hipStream_t s);
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                         uint64_t nslots, const StageOut& out, hipStream_t s);
+// symmetric dedup schedule: per query its bucket positions (sranges), full and owner slot
+// counts (each padded to 64), real[0] += the unpadded full total
+hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
+                            uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* real,
+                            hipStream_t s);
+hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, uint64_t nq, int nkeys,
+                        uint64_t* obase, hipStream_t s);
+hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, const StageOut& out,
+                       hipStream_t s);
+hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
+                             hipStream_t s);
 hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s);
 hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nblocks,
                           uint64_t base, const MatchList& out, hipStream_t s);

@@ -706,16 +706,22 @@ __device__ __forceinline__ int popc_t(MT m) {
   return sizeof(MT) == 8 ? __popcll((uint64_t)m) : __popc((uint32_t)m);
 }
 
-template <typename MT, typename CT>
+// DUAL (symmetric dedup schedule): also the similarity with the roles swapped, *rev =
+// JaroWinkler(r1 = candidate, r2 = query).  Only equal-length pairs differ (Duke keeps r1
+// as s1 on a tie); for them the same sweep runs the candidate-rows form over the query
+// window [j - md, j + md) beside the query-rows form.
+template <typename MT, typename CT, bool DUAL>
 __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str<CT>& qs, int nq,
-                                                  const Str<CT>& cs, int nc, bool act) {
+                                                  const Str<CT>& cs, int nc, bool act, double* rev) {
   if (act && str_equal(qs, nq, cs, nc)) act = false;  // 1.0 below
   const bool rows_cand = act && nc < nq;
   const bool rows_query = act && !rows_cand;
+  const bool eqlen = DUAL && act && nc == nq;  // the reversed orientation, candidate rows
   // window over the query: [j - md, j + md) for candidate row j (md = |query| / 2), or the
   // rows i with j in [i - md, i + md) (md = |candidate| / 2) — both as [lo_off + j, hi_off + j)
   const int md = rows_cand ? (nq >> 1) : (nc >> 1);
   const int lo_off = rows_cand ? -md : 1 - md, hi_off = rows_cand ? md : md + 1;
+  const int md2 = nq >> 1;
   int c = 0, t = 0, prev = -1;
   MT found = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
   const int maxn = act ? nc : 0;
@@ -727,12 +733,12 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
 #pragma unroll
     for (int u = 0; u < UPW; ++u) {
       const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
-      MT e = 0;
-      if (j < maxn)
-        e = peq_eq_t<MT, CT>(peq, Str<CT>::unit(w, u)) &
-            range_mask_t<MT>(max(0, j + lo_off), min(nq, j + hi_off));
+      MT pv = 0;
+      if (j < maxn) pv = peq_eq_t<MT, CT>(peq, Str<CT>::unit(w, u));
+      const MT e = pv & range_mask_t<MT>(max(0, j + lo_off), min(nq, j + hi_off));
       // candidate rows: first match of row j
-      const MT ec = rows_cand ? e : (MT)0;
+      MT ec = rows_cand ? e : (MT)0;
+      if (DUAL && eqlen) ec = pv & range_mask_t<MT>(max(0, j - md2), min(nq, j + md2));
       const int jj = ffs64((uint64_t)ec | (1ull << 63));
       const bool has = ec != 0;
       c += has ? 1 : 0;
@@ -749,6 +755,7 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
       if (j & 32) p5 |= m;
     }
   }
+  const int cc = c, tc = t;  // candidate-rows counts (rows_cand lanes, or the reversed pair)
   if (rows_query) {
     c = popc_t(found);
     // descents p(i) < p(previous matched row), MSB-first bit-sliced compare
@@ -762,14 +769,30 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
     }
     t = popc_t<MT>(lt & found);
   }
-  if (!act) return 1.0;  // equal values (inactive lanes discard the result)
-  if (c == 0) return 0.0;
+  if (!act) {  // equal values (inactive lanes discard the result)
+    if (DUAL) *rev = 1.0;
+    return 1.0;
+  }
+  double score = 0.0;
   const Str<CT>& s1 = rows_cand ? cs : qs;
   const Str<CT>& s2 = rows_cand ? qs : cs;
   const int n1 = rows_cand ? nc : nq, n2 = rows_cand ? nq : nc;
-  double score = ((c / (double)n1) + (c / (double)n2) + ((c - t) / (double)c)) / 3.0;
-  const int p = common_prefix4(s1, s2, min(4, n1));
-  score += ((p * (1 - score)) / 10);
+  const int p = common_prefix4(s1, s2, min(4, n1));  // symmetric in s1 / s2
+  if (c != 0) {
+    score = ((c / (double)n1) + (c / (double)n2) + ((c - t) / (double)c)) / 3.0;
+    score += ((p * (1 - score)) / 10);
+  }
+  if (DUAL) {
+    double r = score;
+    if (eqlen) {  // r1 = candidate = s1 (n1 == n2)
+      r = 0.0;
+      if (cc != 0) {
+        r = ((cc / (double)nc) + (cc / (double)nq) + ((cc - tc) / (double)cc)) / 3.0;
+        r += ((p * (1 - r)) / 10);
+      }
+    }
+    *rev = r;
+  }
   return score;
 }
 
@@ -886,10 +909,12 @@ __device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool o
 // ------------------------------------------------------------------------------------
 // The fused scoring kernel.  One lane per slot, one query per wave.
 // ------------------------------------------------------------------------------------
-template <int RMAX, int LR, typename CT>
+// SYM: `rev` receives Comparator.compare(candidate, query) where it can differ from
+// compare(query, candidate) (JaroWinkler on equal lengths); it is left alone otherwise.
+template <int RMAX, int LR, typename CT, bool SYM>
 __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
-                                             int lc, bool cmp) {
+                                             int lc, bool cmp, double& rev) {
   const CT* base = reinterpret_cast<const CT*>(D.units);
   const Str<CT> s1{reinterpret_cast<const uint32_t*>(base + D.off[q]), 1, 1 << 30};
   const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + g, rstride,
@@ -921,12 +946,18 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
       const bool table = lq <= 64 && (D.op == DK_CMP_LEVENSHTEIN || __ballot(cmp && lc > 64) == 0);
       if (table) {
         peq_set(peq, base + D.off[q], lq, true);
-        sim = D.op == DK_CMP_LEVENSHTEIN ? levenshtein_peq<RMAX>(peq, s1, lq, s2, lc, cmp)
-                 : (lq <= DK_JW_NARROW ? jarowinkler_peq<uint32_t>(peq, s1, lq, s2, lc, cmp)
-                             : jarowinkler_peq<uint64_t>(peq, s1, lq, s2, lc, cmp));
+        if (D.op == DK_CMP_LEVENSHTEIN) {
+          sim = levenshtein_peq<RMAX>(peq, s1, lq, s2, lc, cmp);
+        } else {
+          double r = 0.0;
+          sim = lq <= DK_JW_NARROW ? jarowinkler_peq<uint32_t, CT, SYM>(peq, s1, lq, s2, lc, cmp, &r)
+                                   : jarowinkler_peq<uint64_t, CT, SYM>(peq, s1, lq, s2, lc, cmp, &r);
+          if (SYM) rev = r;
+        }
         peq_set(peq, base + D.off[q], lq, false);
       } else if (cmp) {
         sim = jarowinkler(s1, lq, s2, lc);
+        if (SYM) rev = lq == lc ? jarowinkler(s2, lc, s1, lq) : sim;
       }
       break;
     }
@@ -985,120 +1016,23 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
   return sim;
 }
 
-template <int RMAX, int LR>
-__device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
-                                           uint64_t nslots, const StageOut& out) {
-  __shared__ uint64_t peq_all[kScoreBlock / 64][kPeqEntries];
+// Block-ordered compaction of a 256-slot block's decisions: wave ballots -> per-wave
+// counts in LDS -> slot-ordered entries at the block's staging region (no atomics on
+// entries), plus the block's scored-pair and operand-byte sums.
+__device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, double prob,
+                                           uint32_t crow, uint32_t qi, uint32_t scored,
+                                           uint32_t bytes) {
   __shared__ uint32_t wcount[kScoreBlock / 64], wscored[kScoreBlock / 64], wbytes[kScoreBlock / 64];
   const uint32_t wave = threadIdx.x >> 6;
-  uint64_t* peq = peq_all[wave];
-  for (int e = (int)lane_id(); e < kPeqEntries; e += 64) peq[e] = 0;
-
-  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool valid = idx < nslots;
-  const uint64_t s = slot0 + min(idx, nslots - 1);
-  uint32_t qi = 0, g = 0;
-  if (S.allpairs) {
-    // slots of a query: [qi * mpad, qi * mpad + m), mpad = m rounded up to 64
-    qi = (uint32_t)(s / S.mpad);
-    const uint64_t t = s - (uint64_t)qi * S.mpad;
-    valid = valid && t < S.m;
-    g = valid ? (uint32_t)t : 0u;
-  } else {
-    qi = S.wq[s >> 6];  // one query per wave by construction (padded slot layout)
-  }
-  qi = __builtin_amdgcn_readfirstlane(qi);
-  const uint32_t q = __builtin_amdgcn_readfirstlane(S.queries[qi]);
-  if (!S.allpairs) {
-    // Candidate t of the query: key function k's range first, then (group, row) order
-    // inside it.  Filters: isSameAs (identity), and "already a candidate under an
-    // earlier key function" (Duke returns candidates as a set).  The ranges and the
-    // query's keys are wave-uniform.
-    uint64_t t = s - S.qoff[qi];
-    int k = -1;
-    for (int kk = 0; kk < S.nkeys; ++kk) {
-      const uint2 r = S.ranges[(uint64_t)kk * S.nq + qi];
-      const uint64_t len = (uint64_t)(r.y - r.x);
-      if (k < 0) {
-        if (t < len) {
-          k = kk;
-          g = (uint32_t)((uint64_t)kk * S.m + r.x + t);
-        } else {
-          t -= len;
-        }
-      }
-    }
-    valid = valid && k >= 0;
-    if (!valid) g = 0u;  // lanes without a pair read replica position 0 (always in range)
-    bool ok = S.rident[g] != P.ident[q];
-    for (int j = 0; j < S.nkeys - 1; ++j)
-      if (j < k) ok = ok && S.rkeys[j][g] != S.qkeys[j][q];
-    valid = valid && ok;
-  }
-  const uint32_t crow = P.rowof[g];
-  if (S.allpairs && !S.same_ok) valid = valid && P.ident[crow] != P.ident[q];  // Processor.isSameAs
-  wave_lds_sync();
-
-  double prob = P.raw_prop < 0 ? 0.5 : __builtin_nan("");
-  uint32_t bytes = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
-  for (int p = 0; p < P.nprops; ++p) {
-    const DevProp& D = P.props[p];
-    const int lq = (int)__builtin_amdgcn_readfirstlane((uint32_t)D.len[q]);
-    if (lq == (int)kMissing) continue;  // r1 has no value: property skipped for the wave
-    const int lc = valid ? (int)D.rlen[g] : (int)kMissing;
-    const bool present = lc != (int)kMissing;
-    const bool cmp = present && lq > 0 && lc > 0;
-    double sim = 0.0;
-    // algorithmic bytes (SURVEY §8d, DESIGN.md §5): the CANDIDATE's operands at their stored
-    // width -- the query's value is read once per wave (LDS tables), not per pair
-    if (present) bytes += 2u;  // rlen
-    if (D.op == DK_CMP_NUMERIC) {
-      if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
-      if (cmp) bytes += 9u;   // rnum + rnumok
-    } else if (D.op != DK_CMP_NONE) {
-      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp)
-                         : string_sim<RMAX, LR, uint16_t>(D, P.rstride, peq, q, g, crow, lq, lc, cmp);
-      if (cmp) {
-        if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2)
-          bytes += 6u + (D.rg32 && D.rgmax ? 4u : 8u) * (uint32_t)D.rgcnt[g];
-        else if (uses_codes(D.op))  // token ids
-          bytes += 6u + 8u * (uint32_t)D.rgcnt[g];
-        else
-          bytes += (uint32_t)lc * (uint32_t)D.width;
-      }
-    }
-    if (p == P.raw_prop) {  // Comparator.compare(v1, v2) itself (wave-uniform branch)
-      if (cmp) prob = sim;
-      break;
-    }
-    if (present) {
-      double high = 0.0;
-      if (cmp) {
-        // [Duke 1.2] PropertyImpl.compare
-        const double v = D.op == DK_CMP_NONE ? 0.5
-                         : (sim < 0.5 ? D.low : ((D.high - 0.5) * (sim * sim)) + 0.5);
-        high = java_max(high, v);
-      }
-      prob = compute_bayes(prob, high);
-    }
-  }
-
-  // [Duke 1.2] Processor.compareCandidatesSimple: strict thresholds
-  uint32_t kind = 0;
-  if (valid) {
-    if (prob > P.threshold) kind = DK_KIND_MATCH;
-    else if (P.maybe != 0.0 && prob > P.maybe) kind = DK_KIND_MAYBE;
-  }
-
-  // block-ordered compaction: wave ballots -> per-wave counts in LDS -> slot-ordered
-  // entries at the block's staging region; no atomics on entries
   const uint64_t em = __ballot(kind != 0);
-  const uint64_t vm = __ballot(valid);
-  uint32_t sb = bytes;
-  for (int o = 32; o > 0; o >>= 1) sb += __shfl_xor(sb, o);
+  uint32_t sb = bytes, ss = scored;
+  for (int o = 32; o > 0; o >>= 1) {
+    sb += __shfl_xor(sb, o);
+    ss += __shfl_xor(ss, o);
+  }
   if (lane_id() == 0) {
     wcount[wave] = (uint32_t)__popcll(em);
-    wscored[wave] = (uint32_t)__popcll(vm);
+    wscored[wave] = ss;
     wbytes[wave] = sb;
   }
   __syncthreads();
@@ -1128,20 +1062,220 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   }
 }
 
+// [Duke 1.2] Processor.compareCandidatesSimple: strict thresholds
+__device__ __forceinline__ uint32_t decide(double prob, double threshold, double maybe) {
+  if (prob > threshold) return DK_KIND_MATCH;
+  if (maybe != 0.0 && prob > maybe) return DK_KIND_MAYBE;
+  return 0;
+}
+
+// [Duke 1.2] PropertyImpl.compare then the start of Processor.compare's java_max
+__device__ __forceinline__ double property_prob(const DevProp& D, double sim) {
+  const double v = D.op == DK_CMP_NONE ? 0.5
+                   : (sim < 0.5 ? D.low : ((D.high - 0.5) * (sim * sim)) + 0.5);
+  return java_max(0.0, v);
+}
+
+// SYM: the owner slots of the symmetric dedup schedule (PairSource::sym): every owned pair
+// is scored in both directions in one pass and the two probabilities go to S.ores; the
+// emission pass (k_emit) turns them into the match list.
+template <int RMAX, int LR, bool SYM>
+__device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
+                                           uint64_t nslots, const StageOut& out) {
+  __shared__ uint64_t peq_all[kScoreBlock / 64][kPeqEntries];
+  const uint32_t wave = threadIdx.x >> 6;
+  uint64_t* peq = peq_all[wave];
+  for (int e = (int)lane_id(); e < kPeqEntries; e += 64) peq[e] = 0;
+
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in_launch = idx < nslots;
+  bool valid = in_launch;
+  const uint64_t s = slot0 + min(idx, nslots - 1);
+  uint32_t qi = 0, g = 0;
+  bool mirror = false;  // SYM: the candidate is a query too (the reverse pair is owned here)
+  if (S.allpairs) {
+    // slots of a query: [qi * mpad, qi * mpad + m), mpad = m rounded up to 64
+    qi = (uint32_t)(s / S.mpad);
+    const uint64_t t = s - (uint64_t)qi * S.mpad;
+    valid = valid && t < S.m;
+    g = valid ? (uint32_t)t : 0u;
+  } else {
+    qi = S.wq[s >> 6];  // one query per wave by construction (padded slot layout)
+  }
+  qi = __builtin_amdgcn_readfirstlane(qi);
+  const uint32_t q = __builtin_amdgcn_readfirstlane(S.queries[qi]);
+  if (!S.allpairs) {
+    // Candidate t of the query: key function k's range first, then (group, row) order
+    // inside it.  Filters: isSameAs (identity), and "already a candidate under an
+    // earlier key function" (Duke returns candidates as a set).  The ranges and the
+    // query's keys are wave-uniform.
+    uint64_t t = s - S.qoff[qi];
+    int k = -1;
+    for (int kk = 0; kk < S.nkeys; ++kk) {
+      if (SYM) {  // owned candidates: [lo, qa) then (pq, hi)
+        const uint4 r = S.sranges[(uint64_t)kk * S.nq + qi];
+        const bool in_t = r.w != kNoPos;
+        const uint64_t nlow = r.z - r.x;
+        const uint64_t len = nlow + (in_t ? (uint64_t)(r.y - r.w - 1) : 0);
+        if (k < 0) {
+          if (t < len) {
+            k = kk;
+            const uint64_t x = t < nlow ? r.x + t : r.w + 1 + (t - nlow);
+            g = (uint32_t)((uint64_t)kk * S.m + x);
+            mirror = in_t;
+          } else {
+            t -= len;
+          }
+        }
+      } else {
+        const uint2 r = S.ranges[(uint64_t)kk * S.nq + qi];
+        const uint64_t len = (uint64_t)(r.y - r.x);
+        if (k < 0) {
+          if (t < len) {
+            k = kk;
+            g = (uint32_t)((uint64_t)kk * S.m + r.x + t);
+          } else {
+            t -= len;
+          }
+        }
+      }
+    }
+    valid = valid && k >= 0;
+    if (!valid) g = 0u;  // lanes without a pair read replica position 0 (always in range)
+    bool ok = S.rident[g] != P.ident[q];
+    for (int j = 0; j < S.nkeys - 1; ++j)
+      if (j < k) ok = ok && S.rkeys[j][g] != S.qkeys[j][q];
+    valid = valid && ok;
+  }
+  const uint32_t crow = P.rowof[g];
+  if (S.allpairs && !S.same_ok) valid = valid && P.ident[crow] != P.ident[q];  // Processor.isSameAs
+  // the high segment (pq, hi) holds rows above the query's own; those below r1 are queries
+  if (SYM) mirror = mirror && valid && crow >= S.r0 && crow < S.r1;
+  wave_lds_sync();
+
+  double prob = P.raw_prop < 0 ? 0.5 : __builtin_nan("");
+  double prob2 = 0.5;  // SYM: Processor.compare(candidate, query)
+  uint32_t bytes = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
+  for (int p = 0; p < P.nprops; ++p) {
+    const DevProp& D = P.props[p];
+    const int lq = (int)__builtin_amdgcn_readfirstlane((uint32_t)D.len[q]);
+    if (lq == (int)kMissing) continue;  // r1 has no value: property skipped for the wave
+    const int lc = valid ? (int)D.rlen[g] : (int)kMissing;
+    const bool present = lc != (int)kMissing;
+    const bool cmp = present && lq > 0 && lc > 0;
+    double sim = 0.0, rev = 0.0;
+    // algorithmic bytes (SURVEY §8d, DESIGN.md §5): the CANDIDATE's operands at their stored
+    // width -- the query's value is read once per wave (LDS tables), not per pair
+    if (present) bytes += 2u;  // rlen
+    if (D.op == DK_CMP_NUMERIC) {
+      if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
+      if (cmp) bytes += 9u;   // rnum + rnumok
+      rev = sim;
+    } else if (D.op != DK_CMP_NONE) {
+      rev = __builtin_nan("");  // marks "same as sim" unless the comparator sets it
+      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev)
+                         : string_sim<RMAX, LR, uint16_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev);
+      if (!SYM || rev != rev) rev = sim;
+      if (cmp) {
+        if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2)
+          bytes += 6u + (D.rg32 && D.rgmax ? 4u : 8u) * (uint32_t)D.rgcnt[g];
+        else if (uses_codes(D.op))  // token ids
+          bytes += 6u + 8u * (uint32_t)D.rgcnt[g];
+        else
+          bytes += (uint32_t)lc * (uint32_t)D.width;
+      }
+    }
+    if (p == P.raw_prop) {  // Comparator.compare(v1, v2) itself (wave-uniform branch)
+      if (cmp) prob = sim;
+      break;
+    }
+    if (present) {
+      // [Duke 1.2] Processor.compare: high = max(0.0, PropertyImpl.compare) over the value
+      // pairs (one each here), then computeBayes
+      prob = compute_bayes(prob, cmp ? property_prob(D, sim) : 0.0);
+      if (SYM) prob2 = compute_bayes(prob2, cmp ? property_prob(D, rev) : 0.0);
+    }
+  }
+
+  if (SYM) {
+    // owner results; the emission pass reads them for this query and (mirror) for the
+    // candidate's own list
+    if (in_launch)
+      reinterpret_cast<double2*>(S.ores)[s] =
+          make_double2(valid ? prob : __builtin_nan(""), mirror ? prob2 : __builtin_nan(""));
+    block_emit(out, 0u, 0.0, 0u, qi, valid ? (mirror ? 2u : 1u) : 0u, bytes);  // operands read once
+  } else {
+    const uint32_t kind = valid ? decide(prob, P.threshold, P.maybe) : 0u;
+    block_emit(out, kind, prob, crow, qi, valid ? 1u : 0u, bytes);
+  }
+}
+
 // The fused scoring kernel.  Short-value variants pin the occupancy (the DP is
 // latency-bound: 5 waves/SIMD up to 40 rows, 4 above); the long-value variants (LR > 0)
 // carry the systolic DP's f64 rows and take what the register allocator needs.
-template <int RMAX>
+template <int RMAX, bool SYM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? DK_WAVES_SHORT : 4, 8)))
 void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
-  score_body<RMAX, 0>(P, S, slot0, nslots, out);
+  score_body<RMAX, 0, SYM>(P, S, slot0, nslots, out);
 }
 
 template <int RMAX, int LR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LR <= 8 ? DK_WAVES_LONG8 : DK_WAVES_LONG16, 8)))
 void k_score_long(const ScoreParams P, const PairSource S,
                                                     uint64_t slot0, uint64_t nslots, StageOut out) {
-  score_body<RMAX, LR>(P, S, slot0, nslots, out);
+  score_body<RMAX, LR, false>(P, S, slot0, nslots, out);
+}
+
+// Emission pass of the symmetric dedup schedule: the query's slots in Duke's candidate
+// order (key function, then bucket position); each reads its probability from the owner
+// results -- its own (owned candidates) or the candidate's (candidates in [qa, pq), which
+// own the pair) -- and goes through the same thresholds and block-ordered compaction as
+// k_score.  HBM-bound: a 4-byte row and an 8-byte probability per slot.
+__global__ __launch_bounds__(256) void k_emit(const EmitSource S, uint64_t slot0, uint64_t nslots,
+                                              StageOut out) {
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool valid = idx < nslots;
+  const uint64_t s = slot0 + min(idx, nslots - 1);
+  const uint32_t qi = __builtin_amdgcn_readfirstlane(S.wq[s >> 6]);
+  uint64_t t = s - S.qoff[qi];
+  int k = -1;
+  uint4 r = make_uint4(0, 0, 0, 0);
+  for (int kk = 0; kk < S.nkeys; ++kk) {
+    const uint4 rr = S.sranges[(uint64_t)kk * S.nq + qi];
+    const uint64_t len = (uint64_t)(rr.y - rr.x);
+    if (k < 0) {
+      if (t < len) {
+        k = kk;
+        r = rr;
+      } else {
+        t -= len;
+      }
+    }
+  }
+  valid = valid && k >= 0;
+  double prob = __builtin_nan("");
+  uint32_t crow = 0;
+  if (valid) {
+    const uint32_t x = r.x + (uint32_t)t;
+    crow = S.rowof[(uint64_t)k * S.m + x];
+    const bool in_t = r.w != kNoPos;
+    uint64_t slot;
+    bool rev = false;
+    if (in_t && x == r.w) {
+      valid = false;  // the query itself (Processor.isSameAs)
+      slot = 0;
+    } else if (in_t && x >= r.z && x < r.w) {
+      // candidate owns the pair: its owner slot for this query's position
+      slot = S.obase[(uint64_t)k * S.nq + (crow - S.r0)] + (r.w - x - 1);
+      rev = true;
+    } else {
+      const uint64_t base = S.obase[(uint64_t)k * S.nq + qi];
+      slot = x < r.z ? base - (r.z - x) : base + (x - r.w - 1);
+    }
+    if (valid) prob = S.ores[2 * slot + (rev ? 1 : 0)];
+  }
+  const uint32_t kind = valid ? decide(prob, S.threshold, S.maybe) : 0u;
+  block_emit(out, kind, prob, crow, qi, 0u, 0u);
 }
 
 // Sum the per-block counters of a chunk into counters[0..1]: one atomic pair per block
@@ -1301,6 +1435,68 @@ __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const
   if (lane_id() == 0 && w) atomicAdd((unsigned long long*)real, (unsigned long long)w);
 }
 
+// Symmetric dedup schedule (PairSource::sym): per query and key function its bucket
+// [lo, hi), the first position qa of a query row (rows >= r0; the bucket is sorted by row)
+// and its own position pq, by binary search; full and owner slot counts padded to 64.
+__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* a, uint64_t lo, uint64_t hi,
+                                                    uint32_t v) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, const BlockTables T,
+                            uint32_t r0, uint4* __restrict__ sranges, uint64_t* __restrict__ counts,
+                            uint64_t* __restrict__ ocounts, uint64_t* __restrict__ real) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t total = 0, own = 0;
+  if (i < nq) {
+    const uint32_t q = queries[i];
+    for (int k = 0; k < T.nkeys; ++k) {
+      const uint64_t key = T.keys[k][q];
+      const uint64_t lo = lower_bound_u64(T.skeys[k], T.m, key);
+      const uint64_t hi = upper_bound_u64(T.skeys[k], lo, T.m, key);
+      const uint32_t* rows = T.rowof + (uint64_t)k * T.m;
+      const uint64_t qa = lower_bound_u32(rows, lo, hi, r0);
+      const uint64_t p = lower_bound_u32(rows, qa, hi, q);
+      const bool in_t = p < hi && rows[p] == q;
+      const uint32_t qa_eff = in_t ? (uint32_t)qa : (uint32_t)hi;
+      sranges[(uint64_t)k * nq + i] =
+          make_uint4((uint32_t)lo, (uint32_t)hi, qa_eff, in_t ? (uint32_t)p : kNoPos);
+      total += hi - lo;
+      own += (qa_eff - lo) + (in_t ? hi - p - 1 : 0);
+    }
+    counts[i] = (total + 63) & ~(uint64_t)63;
+    ocounts[i] = (own + 63) & ~(uint64_t)63;
+  }
+  uint64_t w = total;
+  for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
+  if (lane_id() == 0 && w) atomicAdd((unsigned long long*)real, (unsigned long long)w);
+}
+
+// obase[k][qi] = owner slot of bucket position qa for (k, qi): the query's owner slots
+// start at oqoff[qi] and hold its owned candidates key function by key function
+__global__ void k_obase(const uint4* __restrict__ sranges, const uint64_t* __restrict__ oqoff,
+                        uint64_t nq, int nkeys, uint64_t* __restrict__ obase) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  uint64_t cum = oqoff[i];
+  for (int k = 0; k < nkeys; ++k) {
+    const uint4 r = sranges[(uint64_t)k * nq + i];
+    const uint64_t nlow = r.z - r.x;
+    obase[(uint64_t)k * nq + i] = cum + nlow;
+    cum += nlow + (r.w != kNoPos ? (uint64_t)(r.y - r.w - 1) : 0);
+  }
+}
+
+__global__ void k_gather_u64(const uint64_t* __restrict__ src, const uint64_t* __restrict__ idx,
+                             uint64_t n, uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[idx[i]];
+}
+
 // wq[w] = qi for every wave w of query qi's slots (one thread per query, its waves in a
 // short loop: a query spans a few waves on average)
 __global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32_t* __restrict__ wq) {
@@ -1454,6 +1650,35 @@ hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t npos, const uin
   return hipGetLastError();
 }
 
+hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
+                            uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* real,
+                            hipStream_t s) {
+  DK_LAUNCH_GUARD(nq);
+  k_count_sym<<<grid1d(nq), 256, 0, s>>>(queries, nq, T, r0, sranges, counts, ocounts, real);
+  return hipGetLastError();
+}
+
+hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, uint64_t nq, int nkeys,
+                        uint64_t* obase, hipStream_t s) {
+  DK_LAUNCH_GUARD(nq);
+  k_obase<<<grid1d(nq), 256, 0, s>>>(sranges, oqoff, nq, nkeys, obase);
+  return hipGetLastError();
+}
+
+hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, const StageOut& out,
+                       hipStream_t s) {
+  DK_LAUNCH_GUARD(nslots);
+  k_emit<<<grid1d(nslots, kScoreBlock), kScoreBlock, 0, s>>>(src, slot0, nslots, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
+                             hipStream_t s) {
+  DK_LAUNCH_GUARD(n);
+  k_gather_u64<<<grid1d(n), 256, 0, s>>>(src, idx, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                         uint64_t nslots, const StageOut& out, hipStream_t s) {
   DK_LAUNCH_GUARD(nslots);
@@ -1461,8 +1686,13 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
   // kernel variant by the longest Levenshtein query value (rows of the lane-per-pair DP
   // column) and the longest value of the long-value DP (WeightedLevenshtein, or a
   // Levenshtein value over 64 units): both bound the VGPRs of the fused kernel
-#define DK_SHORT(RM) k_score<RM><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
+#define DK_SHORT(RM)                                                               \
+  do {                                                                             \
+    if (src.sym) k_score<RM, true><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out); \
+    else k_score<RM, false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);        \
+  } while (0)
 #define DK_LONG(RM, L) k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
+  if (src.sym && P.long_rows > 0) return hipErrorInvalidValue;  // the host never schedules it
   if (P.long_rows > 0) {
     const bool lev64 = P.lev_rows > 16;
     if (P.long_rows <= 64) { if (lev64) DK_LONG(64, 4); else DK_LONG(16, 4); }

@@ -79,7 +79,7 @@ class dk_profile(C.Structure):
                 ("ms_gather", C.c_double), ("ms_total", C.c_double),
                 ("score_launches", C.c_uint64), ("pairs_scored", C.c_uint64),
                 ("pairs_generated", C.c_uint64), ("score_bytes", C.c_uint64),
-                ("ms_copy", C.c_double)]
+                ("ms_copy", C.c_double), ("ms_emit", C.c_double), ("sym_matches", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

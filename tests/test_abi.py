@@ -59,7 +59,7 @@ int main(void) {
   S(dk_profile) F(dk_profile, ms_index) F(dk_profile, ms_generate) F(dk_profile, ms_score)
   F(dk_profile, ms_gather) F(dk_profile, ms_total) F(dk_profile, score_launches)
   F(dk_profile, pairs_scored) F(dk_profile, pairs_generated) F(dk_profile, score_bytes)
-  F(dk_profile, ms_copy)
+  F(dk_profile, ms_copy) F(dk_profile, ms_emit) F(dk_profile, sym_matches)
   S(dk_region_layout) F(dk_region_layout, capacity) F(dk_region_layout, first_offset)
   F(dk_region_layout, prob_offset) F(dk_region_layout, candidate_offset)
   F(dk_region_layout, kind_offset)

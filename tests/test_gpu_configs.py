@@ -212,6 +212,15 @@ def test_golden_fixtures_through_kernel(fixture):
     assert checked > len(rows)
 
 
+def java_div(a, b):
+    """Java's double division (IEEE: x/0 is +-Infinity, 0/0 and NaN operands give NaN)."""
+    if b == 0.0:
+        if a == 0.0 or math.isnan(a):
+            return math.nan
+        return math.copysign(math.inf, a) * math.copysign(1.0, b)
+    return a / b
+
+
 def java_numeric(d1, ok1, d2, ok2, min_ratio):
     if not ok1 or not ok2:
         return 0.5
@@ -219,7 +228,7 @@ def java_numeric(d1, ok1, d2, ok2, min_ratio):
         return 1.0
     if d2 < d1:
         d1, d2 = d2, d1
-    ratio = d1 / d2
+    ratio = java_div(d1, d2)
     return 0.0 if ratio < min_ratio else ratio
 
 
