@@ -450,3 +450,81 @@ def test_two_engines_tiles_equal_single_engine():
         assert np.array_equal(cat[k], getattr(full, k))
     for e in engs:
         e.close()
+
+
+# ---------------------------------------------------------------------------------------
+# the symmetric dedup schedule (owner slots + emission pass) against the direct schedule
+# (DK_SYM=0) and the oracle
+# ---------------------------------------------------------------------------------------
+def sym_case(seed, n=2400):
+    rng = random.Random(seed)
+    alpha = "abcdeł"
+    fixed = ["".join(rng.choice("abc") for _ in range(6)) for _ in range(n)]   # equal-length JW
+    name = [("".join(rng.choice(alpha) for _ in range(rng.randint(3, 9))) if rng.random() > 0.05 else None)
+            for _ in range(n)]
+    num = [str(rng.randint(1, 9)) if rng.random() > 0.1 else None for _ in range(n)]
+    props = [{"comparator": JW, "low": 0.2, "high": 0.9},
+             {"comparator": LEV, "low": 0.1, "high": 0.8},
+             {"comparator": QG, "low": 0.3, "high": 0.7, "q": 2, "formula": A.QGRAM_DICE},
+             {"comparator": NUM, "low": 0.3, "high": 0.7, "min_ratio": 0.5},
+             {"comparator": EX, "low": 0.4, "high": 0.6}]
+    vals = [fixed, name, name, num, fixed]
+    keys = [[f[:1] for f in fixed], [(v or "")[:1] for v in name]]
+    return props, vals, keys
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_symmetric_schedule_equals_direct(seed, monkeypatch):
+    props, vals, keys = sym_case(seed)
+    n = len(vals[0])
+    rng = np.random.default_rng(seed)
+    ident = np.arange(n, dtype=np.uint64)
+    ident[2000:2100] = ident[100:200]                # superseded rows (not in the tables)
+    ident[2100:2110] = ident[2110:2120]              # superseded inside the query range
+    deleted = (rng.random(n) < 0.03).astype(np.uint8)
+    eng = dh.GpuEngine(schema_of(props, 0.75, 0.55, "dedup", 2))
+    upsert_slice(eng, vals, keys, ident, 0, 1500, deleted)
+    upsert_slice(eng, vals, keys, ident, 1500, n, deleted)
+    ot = O.OracleTable(props, vals, keys=keys, ident=ident, deleted=deleted,
+                       alive=alive_after(list(ident), n), threshold=0.75, maybe=0.55)
+    for q in (np.arange(n, dtype=np.uint32), np.arange(700, 1900, dtype=np.uint32),
+              np.arange(1500, n, dtype=np.uint32)):
+        for chunk in (None, "3000"):
+            if chunk:
+                monkeypatch.setenv("DK_CHUNK_SLOTS", chunk)
+            else:
+                monkeypatch.delenv("DK_CHUNK_SLOTS", raising=False)
+            eng.reset_profile()
+            eng.set_profiling(True)
+            res = eng.match(q)
+            assert eng.profile()["sym_matches"] == 1
+            ref = ot.match(q)
+            assert res.n > 0
+            assert_same(res, ref)
+            res_dev = eng.match(q, on_device=True)
+            assert res_dev.n == res.n and res_dev.pairs_scored == res.pairs_scored
+            res_dev.close()
+            monkeypatch.setenv("DK_SYM", "0")
+            direct = eng.match(q)
+            monkeypatch.delenv("DK_SYM")
+            assert_same(direct, ref)
+            eng.set_profiling(False)
+            res.close()
+            direct.close()
+    eng.close()
+
+
+def test_symmetric_schedule_overwrite_duplicates():
+    """overwrite: several alive rows of one ID; isSameAs filters them from each other."""
+    props, vals, keys = sym_case(43, n=900)
+    n = len(vals[0])
+    ident = np.arange(n, dtype=np.uint64) % 700
+    eng = dh.GpuEngine(schema_of(props, 0.75, 0.55, "dedup", 2))
+    eng.set_overwrite(True)
+    upsert_slice(eng, vals, keys, ident, 0, n)
+    ot = O.OracleTable(props, vals, keys=keys, ident=ident, threshold=0.75, maybe=0.55)
+    q = np.arange(n, dtype=np.uint32)
+    eng.set_profiling(True)
+    assert_same(eng.match(q), ot.match(q))
+    assert eng.profile()["sym_matches"] == 1
+    eng.close()
