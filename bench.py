@@ -390,7 +390,7 @@ def main():
                          "limiter": "valu" if valu else None, "valu": valu},
             "pcie_inclusive": pcie,
             "phases_ms_per_step": {k: prof[k] / args.steps for k in
-                                   ("ms_index", "ms_generate", "ms_score", "ms_gather", "ms_copy",
+                                   ("ms_index", "ms_generate", "ms_score", "ms_emit", "ms_gather", "ms_copy",
                                     "ms_total")},
         }
         if world == 1 and args.cpu_seconds > 0:

@@ -4,7 +4,7 @@
 # usage: scripts/pmc_profile.sh OUTDIR [bench args...]
 set -e
 OUT=$1; shift
-ARGS=${@:---steps 1 --warmup 0 --cpu-seconds 0 --no-warm-batch}
+ARGS=${@:---steps 1 --warmup 0 --cpu-seconds 0 --no-warm-batch --pcie-steps 0}
 export TMPDIR=/tmp
 mkdir -p $OUT
 run() {  # name counters...

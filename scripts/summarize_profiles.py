@@ -47,16 +47,21 @@ def main():
     per_launch = (2.0 * fetch_kb + write_kb) * 1024.0 / n
     # pairs scored by the profiled command (its bench.py JSON line), for a per-pair figure
     # that bench.py scales to its own launch mix
-    pairs = None
+    pairs, workload = None, None
     try:
         for line in open(os.path.join(pmcdir, "fetch.log")):
             if line.startswith("{"):
                 d = json.loads(line)
                 pairs = d["config"]["pairs_per_step"] * d["steps"] + d["config"]["pairs_per_step"] * d["warmup"]
+                workload = d["config"]["workload"].split(":")[0]
     except (OSError, ValueError, KeyError):
         pass
+    names = {"BASELINE configs[1]": "dedup", "BASELINE configs[2]": "linkage",
+             "BASELINE configs[3]": "allpairs", "BASELINE configs[4]": "longtext"}
     summary = {
         "kernel": "k_score",
+        "workload": names.get(workload, workload),
+        "commit": os.environ.get("DK_COMMIT", "?"),
         "launches_profiled": n,
         "fetch_size_kib_total": fetch_kb,
         "write_size_kib_total": write_kb,
@@ -77,7 +82,8 @@ def main():
         for k, val in summary.items():
             f.write(f"{k}: {val}\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with open(os.path.join(root, "profiles", "pmc_k_score.json"), "w") as f:
+    dest = os.environ.get("PMC_JSON", os.path.join(root, "profiles", "pmc_k_score.json"))
+    with open(dest, "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps({k: summary[k] for k in list(summary)[:12]}, indent=1))
 
