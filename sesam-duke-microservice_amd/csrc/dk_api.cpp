@@ -308,7 +308,7 @@ struct dk_ctx {
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
-  DevBuf ocounts, oqoff, owq, obase, ores, bidx, bval;
+  DevBuf ocounts, oqoff, owq, obase, ores, mcounts, mqoff, mbase, mres, bidx, bval;
   PinnedBuf h_bounds;
   DevBuf counters;
   struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx; };
@@ -1119,7 +1119,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
 
   // ---- candidate counts per query -> slot offsets ----
   Timer t_gen(c, &c->prof.ms_generate, s);
-  uint64_t total = 0, generated = 0, mpad = 0, otot = 0;
+  uint64_t total = 0, generated = 0, mpad = 0, otot = 0, mtot = 0;
   const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
   bool sym = contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
   const uint32_t r0 = nq ? query_rows[0] : 0;
@@ -1130,12 +1130,18 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(c->ocounts.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->oqoff.reserve((nq + 1) * 8, 0, s));
+    HIPCHK(c->mcounts.reserve((nq + 1) * 8, 0, s));
+    HIPCHK(c->mqoff.reserve((nq + 1) * 8, 0, s));
     HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
     HIPCHK(launch_count_sym(c->d_queries.as<uint32_t>(), nq, T, r0, c->ranges.as<uint4>(),
                             c->counts.as<uint64_t>(), c->ocounts.as<uint64_t>(),
-                            c->counters.as<uint64_t>() + 2, s));
+                            c->mcounts.as<uint64_t>(), c->counters.as<uint64_t>() + 2, s));
     HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->ocounts.as<uint64_t>() + nq, 0, 8, s));
+    HIPCHK(hipMemsetAsync(c->mcounts.as<uint64_t>() + nq, 0, 8, s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return exclusive_scan_u64(t, b, c->mcounts.as<uint64_t>(), c->mqoff.as<uint64_t>(), nq + 1, s);
+    }));
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
     }));
@@ -1145,26 +1151,33 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(hipMemcpyAsync(&hs[3], c->qoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&hs[2], c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&hs[1], c->oqoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&hs[0], c->mqoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     total = hs[3];
     generated = hs[2];
     otot = hs[1];
-    // the owner results live for the whole call (a pair is read back by a later query's
-    // emission): 16 B per owner slot, within a third of the free HBM, else no symmetry
+    mtot = hs[0];
+    // owner and mirror results live for the whole call (a query's emission reads what
+    // earlier queries pushed): 8 B per owner and per mirror slot, within a third of the
+    // free HBM, else the direct schedule
     size_t fr = 0, tot_mem = 0;
     HIPCHK(hipMemGetInfo(&fr, &tot_mem));
-    const size_t need = otot * 16 + 64;
-    if (need > c->ores.bytes && need - c->ores.bytes > fr / 3) sym = false;
+    const size_t need = (otot * 8 + 64 > c->ores.bytes ? otot * 8 + 64 - c->ores.bytes : 0) +
+                        (mtot * 8 + 64 > c->mres.bytes ? mtot * 8 + 64 - c->mres.bytes : 0);
+    if (need > fr / 3) sym = false;
   }
   if (sym) {
-    HIPCHK(c->ores.reserve(otot * 16 + 64, 0, s));
+    HIPCHK(c->ores.reserve(otot * 8 + 64, 0, s));
+    HIPCHK(c->mres.reserve(mtot * 8 + 64, 0, s));
+    HIPCHK(c->mbase.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
+    HIPCHK(hipMemsetAsync(c->mres.p, 0xFF, mtot * 8, s));  // all-ones: a NaN (no entry)
     HIPCHK(c->wq.reserve(total / 64 * 4 + 4, 0, s));
     HIPCHK(c->owq.reserve(otot / 64 * 4 + 4, 0, s));
     HIPCHK(c->obase.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
     HIPCHK(launch_wavemap(c->qoff.as<uint64_t>(), nq, c->wq.as<uint32_t>(), s));
     HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s));
-    HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), nq, nk,
-                        c->obase.as<uint64_t>(), s));
+    HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), c->mqoff.as<uint64_t>(),
+                        nq, nk, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
   } else if (!allpairs) {
     HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
     HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
@@ -1283,6 +1296,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     src.qoff = c->oqoff.as<uint64_t>();
     src.sranges = c->ranges.as<uint4>();
     src.ores = c->ores.as<double>();
+    src.mres = c->mres.as<double>();
+    src.mbase = c->mbase.as<uint64_t>();
     src.r0 = r0;
     src.r1 = r0 + (uint32_t)nq;
     esrc.wq = c->wq.as<uint32_t>();
@@ -1290,6 +1305,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     esrc.sranges = c->ranges.as<uint4>();
     esrc.obase = c->obase.as<uint64_t>();
     esrc.ores = c->ores.as<double>();
+    esrc.mres = c->mres.as<double>();
+    esrc.mbase = c->mbase.as<uint64_t>();
     esrc.rowof = c->rowof.as<uint32_t>();
     esrc.nq = nq;
     esrc.m = M;

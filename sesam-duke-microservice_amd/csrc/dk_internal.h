@@ -115,10 +115,16 @@ struct PairSource {
   // The query OWNS candidates [lo, qa) and (pq, hi): it scores them and, for those that
   // are queries themselves, also the reverse direction; candidates in [qa, pq) are owned
   // by those (earlier) queries.  Owner slot t of a query is its t-th owned candidate over
-  // k; qoff / wq then describe owner slots.  Results: ores[2 s] = compare(query, cand),
-  // ores[2 s + 1] = compare(cand, query) (NaN = filtered / no entry).
+  // k; qoff / wq then describe owner slots.  Results: ores[s] = compare(query, cand) of
+  // owner slot s (NaN = filtered); compare(cand, query) goes to the candidate's MIRROR
+  // segment for key k, mres[mbase[k * nq + cand] + (pq - qa)] -- the candidate's mirror
+  // candidates are the bucket positions [qa, pq_cand) in order -- and only when it is a
+  // match / maybe (mres is pre-filled with NaN), so the emission pass reads both kinds of
+  // slots as contiguous runs.
   const uint4* sranges;
   double* ores;
+  double* mres;
+  const uint64_t* mbase;
   uint32_t r0, r1;
 };
 
@@ -131,7 +137,9 @@ struct EmitSource {
   const uint64_t* qoff;
   const uint4* sranges;
   const uint64_t* obase;    // [k * nq + qi]: owner slot of candidate position qa of (k, qi)
+  const uint64_t* mbase;    // [k * nq + qi]: mirror slot of candidate position qa of (k, qi)
   const double* ores;
+  const double* mres;
   const uint32_t* rowof;
   uint64_t nq, m;
   int32_t nkeys;
@@ -231,10 +239,10 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
 // symmetric dedup schedule: per query its bucket positions (sranges), full and owner slot
 // counts (each padded to 64), real[0] += the unpadded full total
 hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
-                            uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* real,
-                            hipStream_t s);
-hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, uint64_t nq, int nkeys,
-                        uint64_t* obase, hipStream_t s);
+                            uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* mcounts,
+                            uint64_t* real, hipStream_t s);
+hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint64_t* mqoff,
+                        uint64_t nq, int nkeys, uint64_t* obase, uint64_t* mbase, hipStream_t s);
 hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, const StageOut& out,
                        hipStream_t s);
 hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,

@@ -1093,6 +1093,8 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   const uint64_t s = slot0 + min(idx, nslots - 1);
   uint32_t qi = 0, g = 0;
   bool mirror = false;  // SYM: the candidate is a query too (the reverse pair is owned here)
+  int ksel = 0;         // SYM: key function of the slot and its bucket record
+  uint4 rsel = make_uint4(0, 0, 0, 0);
   if (S.allpairs) {
     // slots of a query: [qi * mpad, qi * mpad + m), mpad = m rounded up to 64
     qi = (uint32_t)(s / S.mpad);
@@ -1123,6 +1125,8 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
             const uint64_t x = t < nlow ? r.x + t : r.w + 1 + (t - nlow);
             g = (uint32_t)((uint64_t)kk * S.m + x);
             mirror = in_t;
+            ksel = kk;
+            rsel = r;
           } else {
             t -= len;
           }
@@ -1198,11 +1202,12 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   }
 
   if (SYM) {
-    // owner results; the emission pass reads them for this query and (mirror) for the
-    // candidate's own list
-    if (in_launch)
-      reinterpret_cast<double2*>(S.ores)[s] =
-          make_double2(valid ? prob : __builtin_nan(""), mirror ? prob2 : __builtin_nan(""));
+    // owner result for this query's list; the reverse direction into the candidate's mirror
+    // segment (a scattered store while the VALU-bound wave keeps computing) when it will be
+    // an entry -- the rest of that segment keeps its NaN fill
+    if (in_launch) S.ores[s] = valid ? prob : __builtin_nan("");
+    if (mirror && decide(prob2, P.threshold, P.maybe) != 0u)
+      S.mres[S.mbase[(uint64_t)ksel * S.nq + (crow - S.r0)] + (rsel.w - rsel.z)] = prob2;
     block_emit(out, 0u, 0.0, 0u, qi, valid ? (mirror ? 2u : 1u) : 0u, bytes);  // operands read once
   } else {
     const uint32_t kind = valid ? decide(prob, P.threshold, P.maybe) : 0u;
@@ -1259,20 +1264,15 @@ __global__ __launch_bounds__(256) void k_emit(const EmitSource S, uint64_t slot0
     const uint32_t x = r.x + (uint32_t)t;
     crow = S.rowof[(uint64_t)k * S.m + x];
     const bool in_t = r.w != kNoPos;
-    uint64_t slot;
-    bool rev = false;
     if (in_t && x == r.w) {
       valid = false;  // the query itself (Processor.isSameAs)
-      slot = 0;
     } else if (in_t && x >= r.z && x < r.w) {
-      // candidate owns the pair: its owner slot for this query's position
-      slot = S.obase[(uint64_t)k * S.nq + (crow - S.r0)] + (r.w - x - 1);
-      rev = true;
+      // the candidate owns the pair and pushed compare(this query, it) to our mirror run
+      prob = S.mres[S.mbase[(uint64_t)k * S.nq + qi] + (x - r.z)];
     } else {
       const uint64_t base = S.obase[(uint64_t)k * S.nq + qi];
-      slot = x < r.z ? base - (r.z - x) : base + (x - r.w - 1);
+      prob = S.ores[x < r.z ? base - (r.z - x) : base + (x - r.w - 1)];
     }
-    if (valid) prob = S.ores[2 * slot + (rev ? 1 : 0)];
   }
   const uint32_t kind = valid ? decide(prob, S.threshold, S.maybe) : 0u;
   block_emit(out, kind, prob, crow, qi, 0u, 0u);
@@ -1449,9 +1449,10 @@ __device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* a, uint64_t 
 
 __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, const BlockTables T,
                             uint32_t r0, uint4* __restrict__ sranges, uint64_t* __restrict__ counts,
-                            uint64_t* __restrict__ ocounts, uint64_t* __restrict__ real) {
+                            uint64_t* __restrict__ ocounts, uint64_t* __restrict__ mcounts,
+                            uint64_t* __restrict__ real) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t total = 0, own = 0;
+  uint64_t total = 0, own = 0, mir = 0;
   if (i < nq) {
     const uint32_t q = queries[i];
     for (int k = 0; k < T.nkeys; ++k) {
@@ -1467,9 +1468,11 @@ __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, c
           make_uint4((uint32_t)lo, (uint32_t)hi, qa_eff, in_t ? (uint32_t)p : kNoPos);
       total += hi - lo;
       own += (qa_eff - lo) + (in_t ? hi - p - 1 : 0);
+      mir += in_t ? p - qa : 0;
     }
     counts[i] = (total + 63) & ~(uint64_t)63;
     ocounts[i] = (own + 63) & ~(uint64_t)63;
+    mcounts[i] = mir;
   }
   uint64_t w = total;
   for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
@@ -1478,16 +1481,22 @@ __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, c
 
 // obase[k][qi] = owner slot of bucket position qa for (k, qi): the query's owner slots
 // start at oqoff[qi] and hold its owned candidates key function by key function
+// and mbase[k][qi] = mirror slot of bucket position qa (the query's mirror runs [qa, pq)
+// start at mqoff[qi], key function by key function)
 __global__ void k_obase(const uint4* __restrict__ sranges, const uint64_t* __restrict__ oqoff,
-                        uint64_t nq, int nkeys, uint64_t* __restrict__ obase) {
+                        const uint64_t* __restrict__ mqoff, uint64_t nq, int nkeys,
+                        uint64_t* __restrict__ obase, uint64_t* __restrict__ mbase) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
-  uint64_t cum = oqoff[i];
+  uint64_t cum = oqoff[i], mcum = mqoff[i];
   for (int k = 0; k < nkeys; ++k) {
     const uint4 r = sranges[(uint64_t)k * nq + i];
     const uint64_t nlow = r.z - r.x;
+    const bool in_t = r.w != kNoPos;
     obase[(uint64_t)k * nq + i] = cum + nlow;
-    cum += nlow + (r.w != kNoPos ? (uint64_t)(r.y - r.w - 1) : 0);
+    mbase[(uint64_t)k * nq + i] = mcum;
+    cum += nlow + (in_t ? (uint64_t)(r.y - r.w - 1) : 0);
+    mcum += in_t ? (uint64_t)(r.w - r.z) : 0;
   }
 }
 
@@ -1651,17 +1660,17 @@ hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t npos, const uin
 }
 
 hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
-                            uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* real,
-                            hipStream_t s) {
+                            uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* mcounts,
+                            uint64_t* real, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_count_sym<<<grid1d(nq), 256, 0, s>>>(queries, nq, T, r0, sranges, counts, ocounts, real);
+  k_count_sym<<<grid1d(nq), 256, 0, s>>>(queries, nq, T, r0, sranges, counts, ocounts, mcounts, real);
   return hipGetLastError();
 }
 
-hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, uint64_t nq, int nkeys,
-                        uint64_t* obase, hipStream_t s) {
+hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint64_t* mqoff,
+                        uint64_t nq, int nkeys, uint64_t* obase, uint64_t* mbase, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_obase<<<grid1d(nq), 256, 0, s>>>(sranges, oqoff, nq, nkeys, obase);
+  k_obase<<<grid1d(nq), 256, 0, s>>>(sranges, oqoff, mqoff, nq, nkeys, obase, mbase);
   return hipGetLastError();
 }
 
