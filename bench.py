@@ -127,6 +127,7 @@ def build_workload(args):
                  keys=synth.keys_first_two_tokens(texts), group=group, mode=A.MODE_LINKAGE,
                  queries=np.arange(n, len(group)))
     w["n"] = len(next(iter(w["values"].values())))
+    w["nkeys"] = len(w["keys"])
     w["queries"] = np.asarray(w["queries"], dtype=np.uint32)
     # Processor.compare visits the record's HashMap order (data-source columns + ID and the
     # ignored synthetic properties, App.java:309-323; dukeGroupNo in linkage)
@@ -148,7 +149,7 @@ def make_schema(w):
         arr[i] = A.dk_property(p["comparator"], p.get("q", 2), p.get("formula", A.QGRAM_OVERLAP),
                                p.get("tokenizer", A.QGRAM_BASIC), p["low"], p["high"],
                                p.get("min_ratio", 0.0))
-    s = A.dk_schema(len(w["props"]), arr, w["threshold"], w["maybe"], w["mode"], len(w["keys"]))
+    s = A.dk_schema(len(w["props"]), arr, w["threshold"], w["maybe"], w["mode"], w["nkeys"])
     s._keep = arr
     return s
 
@@ -185,28 +186,60 @@ def main():
     import dukehip as dh
     from dukehip import synth
 
+    from dukehip import dist as dshard
     t0 = time.time()
-    w = build_workload(args)
+    shared_batch = None
+    if dist is None:
+        w = build_workload(args)
+        # records/sec deduped: the batch's host pack (strings -> SoA columns)
+        # and dk_upsert, plus one dk_match of the batch (the step below)
+        t_pack = time.perf_counter()
+        cols = [synth.column(w["values"][p["name"]]) for p in w["props"]]
+        kcols = [synth.column(k) for k in w["keys"]] or None
+        t_pack = time.perf_counter() - t_pack
+    else:
+        # pack once: rank 0 builds and packs the batch, every rank maps the same SoA arrays
+        # (one shared file under /dev/shm) and upserts them into its replica of the index
+        meta, arrays, t_pack = [None], None, 0.0
+        if rank == 0:
+            w = build_workload(args)
+            t_pack = time.perf_counter()
+            cols = [synth.column(w["values"][p["name"]]) for p in w["props"]]
+            kcols = [synth.column(k) for k in w["keys"]]
+            t_pack = time.perf_counter() - t_pack
+            arrays = dshard.columns_to_arrays("p", cols)
+            arrays.update(dshard.columns_to_arrays("k", kcols))
+            arrays["queries"] = w["queries"]
+            if w["group"] is not None:
+                arrays["group"] = w["group"]
+            meta = [{k: v for k, v in w.items() if k not in ("values", "keys", "queries", "group")}]
+        dist.broadcast_object_list(meta, src=0)
+        shared_batch = dshard.SharedBatch(dist, rank, arrays)
+        cols = dshard.arrays_to_columns("p", shared_batch.arrays)
+        kcols = dshard.arrays_to_columns("k", shared_batch.arrays) or None
+        if rank != 0:
+            w = dict(meta[0])
+            w["queries"] = shared_batch.arrays["queries"]
+            w["group"] = shared_batch.arrays.get("group")
     n = w["n"]
     eng = dh.GpuEngine(make_schema(w), device=local)
     torch.cuda.synchronize()
-    # records/sec deduped: the batch's host pack (strings -> SoA columns) and
-    # dk_upsert, plus one dk_match of the batch (the step below)
-    t_pack = time.perf_counter()
-    cols = [synth.column(w["values"][p["name"]]) for p in w["props"]]
-    kcols = [synth.column(k) for k in w["keys"]] or None
     t_up = time.perf_counter()
     eng.upsert(n, np.arange(n, dtype=np.uint64), cols, group=w["group"], key_columns=kcols)
     t_upsert = time.perf_counter() - t_up
-    t_pack = t_up - t_pack
     del cols, kcols
     t_index = time.time() - t0
-    # contiguous query tile of this rank
+    # this rank's contiguous query tile: equal estimated cost (blocking's candidate counts,
+    # identical on every rank's replica of the index), SURVEY §8e
     allq = w["queries"]
-    from dukehip import dist as dshard
-    q0, q1 = dshard.tile(len(allq), rank, world)
+    if world > 1:
+        counts = eng.candidate_counts(allq)
+        bounds = dshard.cost_bounds(counts, world)
+    else:
+        bounds = [0, len(allq)]
+    q0, q1 = bounds[rank], bounds[rank + 1]
     queries = allq[q0:q1]
-    nq_max = dshard.max_tile(len(allq), world)
+    nq_max = max(bounds[r + 1] - bounds[r] for r in range(world))
     holder = {}
     shared = None
     # the first dk_match after dk_upsert also builds the blocking tables + candidate replica
@@ -256,9 +289,9 @@ def main():
         if shared is not None:
             # N>1, shm gather: the list goes to this rank's slice of the shared host mapping
             # (overlapped chunk copies over this GPU's own link); the all-gather of counts
-            # completes the exchange, after which rank 0 holds the node list in place
-            res = eng.match(queries)
-            total = shared.exchange(len(queries), res.n, res.pairs_scored)
+            # completes the exchange, after which rank 0 holds the node list in place (a
+            # list that outgrows its region is handled collectively by shared.match)
+            res, total = shared.match(eng, queries)
             holder["res"] = res
             return res, total
         # N>1: entries stay in HBM; RCCL all-gathers the per-rank counts, then gathers
@@ -368,7 +401,7 @@ def main():
                        "pairs_per_step": pairs_step,
                        "comparators": {p["name"]: CMP_NAMES[p["comparator"]] for p in w["props"]},
                        "threshold": w["threshold"], "maybe_threshold": w["maybe"],
-                       "parallelism": f"query-tile sharding x{world}, replicated index"
+                       "parallelism": f"query-tile sharding x{world} (cost-weighted tiles), replicated index"
                                       + (f", {args.gather} result gather" if world > 1 else "")},
             "records_per_s": len(allq) / (ms_step / 1e3),
             # host pack + dk_upsert + the first dk_match after it (table build included)
@@ -389,6 +422,9 @@ def main():
                          "bytes_per_launch": prof["score_bytes"] / launches,
                          "limiter": "valu" if valu else None, "valu": valu},
             "pcie_inclusive": pcie,
+            # per-rank pairs scored of the last step (tile balance; N>1)
+            "rank_pairs": ([c[1] for c in holder["counts"]] if "counts" in holder else
+                           [c[1] for c in shared.counts] if shared is not None and shared.counts else None),
             "phases_ms_per_step": {k: prof[k] / args.steps for k in
                                    ("ms_index", "ms_generate", "ms_score", "ms_emit", "ms_gather", "ms_copy",
                                     "ms_total")},
@@ -409,6 +445,8 @@ def main():
     if shared is not None:
         dist.barrier()   # rank 0 is done with the lists
         shared.close()
+    if shared_batch is not None:
+        shared_batch.close()
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

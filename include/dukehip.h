@@ -173,6 +173,11 @@ int dk_upsert(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
 int dk_upsert_transient(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
 int dk_drop_transient(dk_ctx* ctx);
 int dk_match(dk_ctx* ctx, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out);
+/* counts[i] = the candidates blocking produces for query_rows[i] (its buckets' sizes over
+ * the key functions, before the isSameAs / already-a-candidate filters): the cost model for
+ * splitting queries into balanced multi-GPU tiles.  Builds the blocking tables if the index
+ * changed (as dk_match would). */
+int dk_candidate_counts(dk_ctx* ctx, const uint32_t* query_rows, uint64_t nq, uint64_t* counts);
 /* device-to-device copy of a result's entries (any of the pointers may be NULL); the
  * destination buffers live on the ctx's device */
 int dk_result_copy_to_device(const dk_result* result, uint64_t* first, uint32_t* candidate,

@@ -1029,47 +1029,20 @@ static int build_usable(dk_ctx* c, uint64_t* m_out) {
   return DK_OK;
 }
 
-static bool sym_enabled() {
-  const char* e = getenv("DK_SYM");
-  return !(e && e[0] == '0');
-}
-
-// The symmetric schedule holds when every comparator gives compare(a, b) and compare(b, a)
-// the same PropertyImpl probability, or (JaroWinkler) the kernel computes both directions:
-// Levenshtein (the cutoff only moves a < 0.5 similarity), QGram, Exact, Numeric, none.
-// WeightedLevenshtein's stride aliasing and the token comparators' "shorter list first"
-// are orientation dependent; the long-value kernels are not instantiated for it.
-static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
-  if (c->schema.mode != DK_MODE_DEDUP || P.long_rows > 0) return false;
-  for (const auto& S : c->P) {
-    const int op = S.cfg.comparator;
-    if (op == DK_CMP_WEIGHTED_LEVENSHTEIN || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS)
-      return false;
-  }
-  return true;
-}
-
-static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
-                     ResultHolder* R, bool contiguous) {
+// The blocking tables and the candidate replica (index state): built by the first call
+// after the index changed, reused until the next change.
+static int ensure_tables(dk_ctx* c, BlockTables* Tout, uint64_t* Mout) {
   hipStream_t s = c->stream;
-  c->spans.clear();   // left over by a failed call
-  c->ev_next = 0;
-  const auto t0 = std::chrono::steady_clock::now();
   const int nk = c->schema.nkeys;
   const bool allpairs = c->schema.mode == DK_MODE_ALLPAIRS;
-
-  HIPCHK(c->d_queries.reserve(nq * 4 + 4, 0, s));
-  HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
-
-  // ---- index: usable rows + per key function sort by (key, group, row) ----
-  Timer t_index(c, &c->prof.ms_index, s);
+  if (c->tables_gen == c->index_gen) {
+    *Tout = c->tables;
+    *Mout = c->tables_m;
+    return DK_OK;
+  }
   uint64_t M = 0;
   int rc = 0;
   BlockTables T{};
-  if (c->tables_gen == c->index_gen) {
-    T = c->tables;
-    M = c->tables_m;
-  } else {
   rc = build_usable(c, &M);
   if (rc) return rc;
   T.nkeys = nk;
@@ -1114,7 +1087,49 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   c->tables = T;
   c->tables_m = M;
   c->tables_gen = c->index_gen;
+  *Tout = T;
+  *Mout = M;
+  return DK_OK;
+}
+
+static bool sym_enabled() {
+  const char* e = getenv("DK_SYM");
+  return !(e && e[0] == '0');
+}
+
+// The symmetric schedule holds when every comparator gives compare(a, b) and compare(b, a)
+// the same PropertyImpl probability, or (JaroWinkler) the kernel computes both directions:
+// Levenshtein (the cutoff only moves a < 0.5 similarity), QGram, Exact, Numeric, none.
+// WeightedLevenshtein's stride aliasing and the token comparators' "shorter list first"
+// are orientation dependent; the long-value kernels are not instantiated for it.
+static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
+  if (c->schema.mode != DK_MODE_DEDUP || P.long_rows > 0) return false;
+  for (const auto& S : c->P) {
+    const int op = S.cfg.comparator;
+    if (op == DK_CMP_WEIGHTED_LEVENSHTEIN || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS)
+      return false;
   }
+  return true;
+}
+
+static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
+                     ResultHolder* R, bool contiguous) {
+  hipStream_t s = c->stream;
+  c->spans.clear();   // left over by a failed call
+  c->ev_next = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int nk = c->schema.nkeys;
+  const bool allpairs = c->schema.mode == DK_MODE_ALLPAIRS;
+
+  HIPCHK(c->d_queries.reserve(nq * 4 + 4, 0, s));
+  HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
+
+  // ---- index: usable rows + per key function sort by (key, group, row) ----
+  Timer t_index(c, &c->prof.ms_index, s);
+  uint64_t M = 0;
+  BlockTables T{};
+  int rc = ensure_tables(c, &T, &M);
+  if (rc) return rc;
   t_index.stop();
 
   // ---- candidate counts per query -> slot offsets ----
@@ -1499,6 +1514,37 @@ int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_r
     return rc;
   }
   *out = &R->r;
+  return DK_OK;
+}
+
+// Per-query candidate counts of the blocking contract (the sum of the query's bucket
+// sizes over the key functions, before the isSameAs / duplicate filters): the cost model
+// of the multi-GPU query tiles.  ALLPAIRS: every query gets the usable rows.
+int dk_candidate_counts(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, uint64_t* counts) {
+  if (!c || (nq && (!query_rows || !counts))) return fail(DK_E_INVALID, "NULL argument");
+  for (uint64_t i = 0; i < nq; ++i)
+    if (query_rows[i] >= c->nrows)
+      return fail(DK_E_INVALID, "query row %u not in the index (%llu rows)", query_rows[i],
+                  (unsigned long long)c->nrows);
+  if (nq == 0) return DK_OK;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  BlockTables T{};
+  uint64_t M = 0;
+  int rc = ensure_tables(c, &T, &M);
+  if (rc) return rc;
+  if (c->schema.mode == DK_MODE_ALLPAIRS) {
+    for (uint64_t i = 0; i < nq; ++i) counts[i] = M;
+    return DK_OK;
+  }
+  HIPCHK(c->d_queries.reserve(nq * 4 + 4, 0, s));
+  HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c->ranges.reserve((uint64_t)c->schema.nkeys * nq * 8 + 8, 0, s));
+  HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
+  HIPCHK(launch_count_exact(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(),
+                            c->counts.as<uint64_t>(), s));
+  HIPCHK(hipMemcpyAsync(counts, c->counts.p, nq * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
   return DK_OK;
 }
 

@@ -228,6 +228,9 @@ hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t
 // real[0] += the unpadded total
 hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint2* ranges,
                         uint64_t* counts, uint64_t* real, hipStream_t s);
+// counts[i] = candidate slots of query i, unpadded (dk_candidate_counts)
+hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockTables& T,
+                              uint2* ranges, uint64_t* counts, hipStream_t s);
 // wq[w] = qi for the waves of query qi's slots (qoff in slots, multiples of 64)
 hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s);
 // replica-ordered identity and keys 0..nkeys-2 of the rows at replica positions

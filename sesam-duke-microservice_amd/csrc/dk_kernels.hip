@@ -77,6 +77,13 @@ struct Str {
   // a word read without a per-lane branch (the caller masks words past the value): the
   // canonical arena keeps >= 512 zero bytes after the last value, the replica is clamped
   __device__ __forceinline__ uint32_t word_any(int k) const { return w[(uint64_t)min(k, kmax) * wstride]; }
+  // the same read issued where it stands: an invariant load may be sunk to its use by the
+  // compiler (undoing a software prefetch); a relaxed atomic load is a plain global_load
+  // that stays put
+  __device__ __forceinline__ uint32_t word_pf(int k) const {
+    return __hip_atomic_load(w + (uint64_t)min(k, kmax) * wstride, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
   static __device__ __forceinline__ uint32_t unit(uint32_t x, int u) {
     return sizeof(CT) == 1 ? (x >> (8 * u)) & 0xFFu : (x >> (16 * u)) & 0xFFFFu;
   }
@@ -722,37 +729,92 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
   const int md = rows_cand ? (nq >> 1) : (nc >> 1);
   const int lo_off = rows_cand ? -md : 1 - md, hi_off = rows_cand ? md : md + 1;
   const int md2 = nq >> 1;
-  int c = 0, t = 0, prev = -1;
+  int c = 0, t = 0, prev = -1;  // prev = -1: the first match never counts (jj >= 0)
   MT found = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
   const int maxn = act ? nc : 0;
   int wmax = maxn;
   for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
   constexpr int UPW = Str<CT>::UPW;
-  for (int k = 0; k * UPW < wmax; ++k) {
-    const uint32_t w = cs.word_any(k);  // units past maxn are never used (j < maxn)
+  // Units past a candidate's end read as 0 (zero padded): Peq[0] is empty unless the
+  // query itself holds U+0000 (wave-uniform), and only then do lanes mask past-end units.
+  const bool nul = peq_eq<CT>(peq, 0u) != 0ull;
+  if (sizeof(MT) == 4) {
+    // 32-bit masks (query <= 32 units): the window [j + lo_off, j + hi_off) slides one
+    // position per unit, so it is a 64-bit register shifted left once per step whose high
+    // word holds query positions [0, 32) (positions below 0 live in the low word; Peq has
+    // no bits at or past nq, so no upper clip is needed)
+    const int width = hi_off - lo_off;  // 2 md <= 64
+    uint64_t W = (width >= 64 ? ~0ull : ((1ull << width) - 1ull)) << (32 + lo_off);
+    uint64_t W2 = ((1ull << (2 * md2)) - 1ull) << (32 - md2);  // DUAL: [j - md2, j + md2)
+    auto sweep_word = [&](uint32_t w, int k) {
 #pragma unroll
-    for (int u = 0; u < UPW; ++u) {
-      const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
-      MT pv = 0;
-      if (j < maxn) pv = peq_eq_t<MT, CT>(peq, Str<CT>::unit(w, u));
-      const MT e = pv & range_mask_t<MT>(max(0, j + lo_off), min(nq, j + hi_off));
-      // candidate rows: first match of row j
-      MT ec = rows_cand ? e : (MT)0;
-      if (DUAL && eqlen) ec = pv & range_mask_t<MT>(max(0, j - md2), min(nq, j + md2));
-      const int jj = ffs64((uint64_t)ec | (1ull << 63));
-      const bool has = ec != 0;
-      c += has ? 1 : 0;
-      t += (has && prev != -1 && jj < prev) ? 1 : 0;
-      prev = has ? jj : prev;
-      // query rows: rows first matched at step j
-      const MT m = rows_query ? (MT)(e & ~found) : (MT)0;
-      found |= m;
-      if (j & 1) p0 |= m;
-      if (j & 2) p1 |= m;
-      if (j & 4) p2 |= m;
-      if (j & 8) p3 |= m;
-      if (j & 16) p4 |= m;
-      if (j & 32) p5 |= m;
+      for (int u = 0; u < UPW; ++u) {
+        const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
+        uint32_t pv = (uint32_t)peq_eq_t<MT, CT>(peq, Str<CT>::unit(w, u));
+        if (nul) pv = j < maxn ? pv : 0u;
+        const uint32_t e = pv & (uint32_t)(W >> 32);
+        W <<= 1;
+        // candidate rows: first match of row j
+        uint32_t ec = rows_cand ? e : 0u;
+        if (DUAL) {
+          if (eqlen) ec = pv & (uint32_t)(W2 >> 32);
+          W2 <<= 1;
+        }
+        const int jj = __ffs(ec) - 1;
+        const bool has = ec != 0u;
+        c += has ? 1 : 0;
+        t += (has && jj < prev) ? 1 : 0;
+        prev = has ? jj : prev;
+        // query rows: rows first matched at step j
+        const MT m = rows_query ? (MT)(e & ~(uint32_t)found) : (MT)0;
+        found |= m;
+        if (j & 1) p0 |= m;
+        if (j & 2) p1 |= m;
+        if (j & 4) p2 |= m;
+        if (j & 8) p3 |= m;
+        if (j & 16) p4 |= m;
+        if (j & 32) p5 |= m;
+      }
+    };
+    // candidate words two ahead in two fixed registers (the loop is unrolled by two words,
+    // so a word is consumed two words after its load was issued); word_pf: loads the
+    // compiler keeps where they are issued
+    uint32_t wa = cs.word_pf(0), wb = cs.word_pf(1);
+    for (int k = 0; k * UPW < wmax; k += 2) {
+      sweep_word(wa, k);
+      wa = cs.word_pf(k + 2);
+      if ((k + 1) * UPW < wmax) {
+        sweep_word(wb, k + 1);
+        wb = cs.word_pf(k + 3);
+      }
+    }
+  } else {
+    for (int k = 0; k * UPW < wmax; ++k) {
+      const uint32_t w = cs.word_any(k);  // units past maxn are never used (j < maxn)
+#pragma unroll
+      for (int u = 0; u < UPW; ++u) {
+        const int j = k * UPW + u;  // wave-uniform: the plane updates are scalar branches
+        MT pv = peq_eq_t<MT, CT>(peq, Str<CT>::unit(w, u));
+        if (nul) pv = j < maxn ? pv : (MT)0;
+        const MT e = pv & range_mask_t<MT>(max(0, j + lo_off), min(nq, j + hi_off));
+        // candidate rows: first match of row j
+        MT ec = rows_cand ? e : (MT)0;
+        if (DUAL && eqlen) ec = pv & range_mask_t<MT>(max(0, j - md2), min(nq, j + md2));
+        const int jj = ffs64((uint64_t)ec | (1ull << 63));
+        const bool has = ec != 0;
+        c += has ? 1 : 0;
+        t += (has && jj < prev) ? 1 : 0;
+        prev = has ? jj : prev;
+        // query rows: rows first matched at step j
+        const MT m = rows_query ? (MT)(e & ~found) : (MT)0;
+        found |= m;
+        if (j & 1) p0 |= m;
+        if (j & 2) p1 |= m;
+        if (j & 4) p2 |= m;
+        if (j & 8) p3 |= m;
+        if (j & 16) p4 |= m;
+        if (j & 32) p5 |= m;
+      }
     }
   }
   const int cc = c, tc = t;  // candidate-rows counts (rows_cand lanes, or the reversed pair)
@@ -1405,6 +1467,7 @@ __device__ __forceinline__ uint64_t upper_bound_u64(const uint64_t* a, uint64_t 
 // query's own key is looked up by value, so a superseded or deleted query still finds
 // its block.  LINKAGE keeps only the other group's sub-range (rows are sorted by
 // (key, group, row) and groups are 1 and 2; IncrementalDataSource.java:80-84).
+template <bool PAD>
 __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const BlockTables T,
                         uint2* __restrict__ ranges, uint64_t* __restrict__ counts,
                         uint64_t* __restrict__ real) {
@@ -1428,8 +1491,9 @@ __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const
       ranges[(uint64_t)k * nq + i] = make_uint2((uint32_t)a, (uint32_t)b);
       total += b - a;
     }
-    counts[i] = (total + 63) & ~(uint64_t)63;
+    counts[i] = PAD ? (total + 63) & ~(uint64_t)63 : total;
   }
+  if (!PAD) return;
   uint64_t w = total;
   for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
   if (lane_id() == 0 && w) atomicAdd((unsigned long long*)real, (unsigned long long)w);
@@ -1639,7 +1703,14 @@ hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t
 hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint2* ranges,
                         uint64_t* counts, uint64_t* real, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_count<<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, real);
+  k_count<true><<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, real);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockTables& T,
+                              uint2* ranges, uint64_t* counts, hipStream_t s) {
+  DK_LAUNCH_GUARD(nq);
+  k_count<false><<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, nullptr);
   return hipGetLastError();
 }
 

@@ -26,7 +26,7 @@ KIND_MATCH, KIND_MAYBE = 1, 2
 MATCH_HOST, MATCH_DEVICE = 0, 1
 
 EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
-           "dk_match", "dk_result_copy_to_device",
+           "dk_match", "dk_candidate_counts", "dk_result_copy_to_device",
            "dk_free_result", "dk_result_region_layout", "dk_set_result_region",
            "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite", "dk_num_rows", "dk_set_profiling", "dk_get_profile",
            "dk_reset_profile", "dk_last_error", "dk_abi_version")
@@ -106,6 +106,8 @@ def load():
     L.dk_upsert_transient.argtypes = [vp, C.POINTER(dk_batch), vp]
     L.dk_drop_transient.argtypes = [vp]
     L.dk_match.argtypes = [vp, vp, C.c_uint64, C.c_int, C.POINTER(C.POINTER(dk_result))]
+    L.dk_candidate_counts.argtypes = [vp, vp, C.c_uint64, vp]
+    L.dk_candidate_counts.restype = C.c_int
     L.dk_result_copy_to_device.argtypes = [C.POINTER(dk_result), vp, vp, vp, vp]
     L.dk_result_copy_to_device.restype = C.c_int
     L.dk_free_result.argtypes = [C.POINTER(dk_result)]

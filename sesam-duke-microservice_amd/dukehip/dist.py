@@ -31,12 +31,107 @@ PAGE = mmap.PAGESIZE
 
 
 def tile(n, rank, world):
-    """Contiguous query tile [q0, q1) of `rank`."""
+    """Contiguous query tile [q0, q1) of `rank` (equal query counts)."""
     return n * rank // world, n * (rank + 1) // world
 
 
 def max_tile(n, world):
     return max(tile(n, r, world)[1] - tile(n, r, world)[0] for r in range(world))
+
+
+# A query's fixed cost beside its candidates, in candidate units: one wave's worth of
+# padding on average plus its per-wave tables (the score kernel pads a query to 64 slots)
+QUERY_COST = 32
+
+
+def cost_bounds(counts, world):
+    """Tile boundaries b[0..world] balancing the estimated cost -- the query's candidate
+    count (dk_candidate_counts) plus QUERY_COST -- over contiguous tiles (tiles
+    weighted by their blocks' sizes; Zipfian surname blocks make equal query counts
+    unbalanced).  Every rank computes the same boundaries from its replica of the index."""
+    c = np.asarray(counts, dtype=np.float64) + QUERY_COST
+    pre = np.concatenate([[0.0], np.cumsum(c)])
+    total = pre[-1]
+    b = [0]
+    for r in range(1, world):
+        b.append(int(np.searchsorted(pre, total * r / world, side="left")))
+    b.append(len(c))
+    for r in range(1, world + 1):       # monotone (empty tiles allowed)
+        b[r] = max(b[r], b[r - 1])
+    return b
+
+
+def cost_tile(counts, rank, world):
+    b = cost_bounds(counts, world)
+    return b[rank], b[rank + 1]
+
+
+class SharedBatch:
+    """One batch packed once into SoA columns and shared by every rank of the node (SURVEY
+    §8e: the index is replicated, so every rank upserts the same records).  Rank 0 packs
+    and writes the arrays into one file under /dev/shm; the others map it read-only and
+    wrap zero-copy views, instead of re-packing the strings per rank.  Collective."""
+
+    def __init__(self, dist, rank, arrays=None, shm_dir="/dev/shm"):
+        """arrays (rank 0): {name: numpy array}; the other ranks pass None."""
+        import json
+        meta = [None]
+        if rank == 0:
+            d = shm_dir if os.path.isdir(shm_dir) else None
+            layout, off = {}, 0
+            for k, a in arrays.items():
+                a = np.ascontiguousarray(a)
+                off = -(-off // 64) * 64
+                layout[k] = (off, str(a.dtype), list(a.shape))
+                off += a.nbytes
+            fd, path = tempfile.mkstemp(prefix="dukehip_batch_", dir=d)
+            os.ftruncate(fd, max(off, 1))
+            with os.fdopen(fd, "r+b") as f:
+                mm = mmap.mmap(f.fileno(), max(off, 1))
+                for k, a in arrays.items():
+                    o, dt, shp = layout[k]
+                    a = np.ascontiguousarray(a)
+                    mm[o:o + a.nbytes] = a.tobytes()
+                mm.flush()
+            meta = [json.dumps({"path": path, "size": max(off, 1), "layout": layout})]
+        dist.broadcast_object_list(meta, src=0)
+        m = json.loads(meta[0])
+        with open(m["path"], "rb") as f:
+            self.map = mmap.mmap(f.fileno(), m["size"], access=mmap.ACCESS_READ)
+        dist.barrier()
+        if rank == 0:
+            os.unlink(m["path"])
+        self.arrays = {}
+        for k, (o, dt, shp) in m["layout"].items():
+            n = int(np.prod(shp)) if shp else 1
+            self.arrays[k] = np.frombuffer(self.map, dtype=np.dtype(dt), count=n, offset=o).reshape(shp)
+
+    def close(self):
+        self.arrays = {}
+        try:
+            self.map.close()
+        except BufferError:
+            pass
+
+
+def columns_to_arrays(prefix, columns):
+    """A list of Column -> flat {name: array} (for SharedBatch)."""
+    out = {}
+    for i, c in enumerate(columns):
+        out[f"{prefix}{i}.offsets"] = c.offsets
+        out[f"{prefix}{i}.units"] = c.units
+        if c.present is not None:
+            out[f"{prefix}{i}.present"] = c.present
+    return out
+
+
+def arrays_to_columns(prefix, arrays):
+    cols, i = [], 0
+    while f"{prefix}{i}.offsets" in arrays:
+        cols.append(A.Column(arrays[f"{prefix}{i}.offsets"], arrays[f"{prefix}{i}.units"],
+                             arrays.get(f"{prefix}{i}.present")))
+        i += 1
+    return cols
 
 
 def gather_matches(dist, torch, device, nq, n, scored, fill, world, rank, nq_max):
@@ -91,6 +186,10 @@ class RegionUnavailable(RuntimeError):
     """Raised on every rank when some rank cannot use the shared mapping."""
 
 
+class RegionOverflow(RuntimeError):
+    """Raised on every rank when some rank's match list did not fit its region."""
+
+
 class SharedRegionGather:
     """Node-wide shared host mapping with one result region per rank (SURVEY §8e exchange).
 
@@ -106,6 +205,13 @@ class SharedRegionGather:
                  shm_dir="/dev/shm"):
         self.dist, self.torch, self.device = dist, torch, device
         self.world, self.rank, self.nq_max = world, rank, int(nq_max)
+        self.shm_dir = shm_dir
+        self._setup(engine, capacity)
+
+    def _setup(self, engine, capacity):
+        dist, torch, device, world, rank = self.dist, self.torch, self.device, self.world, self.rank
+        shm_dir, nq_max = self.shm_dir, self.nq_max
+        self.capacity = int(capacity)
         self.slice_bytes = -(-A.region_bytes(nq_max, capacity) // PAGE) * PAGE
         total = self.slice_bytes * world
         name = [None]
@@ -142,15 +248,49 @@ class SharedRegionGather:
             raise RegionUnavailable("a rank could not register its result region")
         self.counts = None
 
-    def exchange(self, nq, n, scored):
-        """All-gather of (entries, pairs scored, queries) per rank: after it every rank's
-        list is complete in the mapping.  Returns the node's pairs scored."""
+    def exchange(self, nq, n, scored, ok=True):
+        """All-gather of (entries, pairs scored, queries, ok) per rank: after it every
+        rank's list is complete in the mapping.  Returns the node's pairs scored.  A rank
+        whose dk_match failed with DK_E_NOMEM (its list did not fit its region) still calls
+        this with ok=False, so no rank blocks: every rank then raises RegionOverflow."""
         torch = self.torch
-        cnt = torch.tensor([n, scored, nq], dtype=torch.int64, device=self.device)
+        cnt = torch.tensor([n, scored, nq, 1 if ok else 0], dtype=torch.int64, device=self.device)
         allc = [torch.zeros_like(cnt) for _ in range(self.world)]
         self.dist.all_gather(allc, cnt)
-        self.counts = [tuple(int(v) for v in c.cpu()) for c in allc]
+        got = [tuple(int(v) for v in c.cpu()) for c in allc]
+        if not all(c[3] for c in got):
+            raise RegionOverflow("a rank's match list did not fit its result region")
+        self.counts = [c[:3] for c in got]
         return sum(c[1] for c in self.counts)
+
+    def match(self, engine, queries):
+        """dk_match into this rank's region + exchange, collective and overflow-safe: when a
+        list does not fit, every rank learns it in the exchange, the regions are re-made
+        (collectively) with room for the largest list, and the match runs again."""
+        while True:
+            try:
+                res, ok = engine.match(queries), True
+            except A.DukeHipError as e:
+                if e.code != A.DK_E_NOMEM:
+                    raise
+                res, ok = None, False
+            try:
+                total = self.exchange(len(queries), res.n if ok else 0,
+                                      res.pairs_scored if ok else 0, ok)
+                return res, total
+            except RegionOverflow:
+                if res is not None:
+                    res.close()
+                probe = engine.match(queries, on_device=True)
+                need = self.torch.tensor([probe.n], dtype=self.torch.int64, device=self.device)
+                probe.close()
+                self.dist.all_reduce(need, op=self.dist.ReduceOp.MAX)
+                self.resize(engine, int(need.item() * 1.25) + 4096)
+
+    def resize(self, engine, capacity):
+        """Collective: a new shared mapping with `capacity` entries per rank."""
+        self.close()
+        self._setup(engine, capacity)
 
     def rank_lists(self):
         """Rank 0: every rank's {first, candidate, prob, kind} views, in rank (= query) order
@@ -169,3 +309,4 @@ class SharedRegionGather:
             self.map.close()
         except BufferError:  # a caller still holds views of the lists; GC unmaps
             pass
+        self.counts = None

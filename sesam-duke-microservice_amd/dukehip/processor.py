@@ -168,6 +168,15 @@ class GpuEngine:
                                   A.MATCH_DEVICE if on_device else A.MATCH_HOST, C.byref(res)))
         return MatchResult(self.lib, res, q)
 
+    def candidate_counts(self, query_rows):
+        """dk_candidate_counts: per query, the candidates blocking produces (cost model of
+        the multi-GPU tiles)."""
+        q = np.ascontiguousarray(query_rows, dtype=np.uint32)
+        out = np.zeros(max(1, q.size), dtype=np.uint64)
+        A.check(self.lib.dk_candidate_counts(self.ctx, q.ctypes.data if q.size else None, q.size,
+                                             out.ctypes.data))
+        return out[:q.size]
+
     def set_result_region(self, buf, max_queries):
         """dk_set_result_region: host-mode match lists land in `buf` (a writable buffer, e.g.
         this rank's slice of a node-wide shared mapping) instead of the library's pool.

@@ -133,3 +133,142 @@ def test_shared_region_gather_world2_gloo():
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+# ---------------------------------------------------------------------------------------
+# cost-weighted tiles, the pack-once shared batch and the overflow-safe region exchange;
+# a gather of REAL match lists (the CPU oracle's, per cost tile) against one full run
+# ---------------------------------------------------------------------------------------
+def test_cost_bounds_balance():
+    rng = np.random.default_rng(5)
+    counts = (rng.zipf(1.3, 5000) * 10).clip(0, 100000)
+    for w in (1, 2, 3, 8):
+        b = dshard.cost_bounds(counts, w)
+        assert b[0] == 0 and b[-1] == len(counts) and all(b[i] <= b[i + 1] for i in range(w))
+        cost = np.asarray(counts, float) + dshard.QUERY_COST
+        per = [cost[b[r]:b[r + 1]].sum() for r in range(w)]
+        assert max(per) - min(per) <= 2 * cost.max() + 1e-9
+    assert dshard.cost_bounds([], 3) == [0, 0, 0, 0]
+
+
+def _batch_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    vals = [["abc", None, "ł\U0001F600", ""], ["x", "y", "z", "w"]]
+    cols = [A.Column.from_strings(v) for v in vals]
+    arrays = None
+    if rank == 0:
+        arrays = dshard.columns_to_arrays("p", cols)
+        arrays["ident"] = np.arange(4, dtype=np.uint64)
+    sb = dshard.SharedBatch(dist, rank, arrays)
+    got = dshard.arrays_to_columns("p", sb.arrays)
+    ok = len(got) == 2 and np.array_equal(sb.arrays["ident"], np.arange(4))
+    for g, c in zip(got, cols):
+        ok = ok and np.array_equal(g.offsets, c.offsets) and np.array_equal(g.units, c.units)
+        ok = ok and ((g.present is None and c.present is None) or np.array_equal(g.present, c.present))
+    out.put((rank, bool(ok)))
+    sb.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _overflow_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = dshard.SharedRegionGather(dist, torch, torch.device("cpu"), None, 10, 100, world, rank)
+    raised = False
+    try:
+        g.exchange(10, 0 if rank else 5, 7, ok=(rank == 0))   # rank 1's list did not fit
+    except dshard.RegionOverflow:
+        raised = True
+    g.resize(None, 1000)
+    total = g.exchange(10, 5, 7)
+    out.put((rank, raised and total == 14 and g.capacity == 1000))
+    g.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _oracle_case():
+    import oracle as O
+    from dukehip import synth
+    p = synth.persons(1200, 400, seed=17)
+    props = [{"comparator": A.CMP_JAROWINKLER, "low": 0.1, "high": 0.95},
+             {"comparator": A.CMP_LEVENSHTEIN, "low": 0.2, "high": 0.8},
+             {"comparator": A.CMP_LEVENSHTEIN, "low": 0.1, "high": 0.85}]
+    keys = synth.keys_config2(p)
+    ot = O.OracleTable(props, [p["name"], p["address"], p["dob"]], keys=keys,
+                       threshold=0.9, maybe=0.7)
+    n = len(p["name"])
+    # candidate counts per query (its bucket sizes), as dk_candidate_counts reports them
+    sizes = []
+    for k in keys:
+        from collections import Counter
+        cnt = Counter(k)
+        sizes.append([cnt[v] for v in k])
+    counts = np.sum(np.array(sizes), axis=0)
+    return ot, n, counts
+
+
+def _oracle_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ot, n, counts = _oracle_case()
+    q0, q1 = dshard.cost_tile(counts, rank, world)
+    r = ot.match(np.arange(q0, q1, dtype=np.uint32))
+    qidx = r["query"].astype(np.int64) - q0
+    my_first = np.searchsorted(qidx, np.arange(q1 - q0 + 1), side="left").astype(np.int64)
+    m = len(r["candidate"])
+
+    def fill(f, c, p, k):
+        f[: len(my_first)] = torch.from_numpy(my_first)
+        c[:m] = torch.from_numpy(r["candidate"].astype(np.int32))
+        p[:m] = torch.from_numpy(r["prob"])
+        k[:m] = torch.from_numpy(r["kind"])
+
+    nq_max = max(b - a for a, b in (dshard.cost_tile(counts, x, world) for x in range(world)))
+    ranks, total = dshard.gather_matches(dist, torch, torch.device("cpu"), q1 - q0, m,
+                                         r["pairs_scored"], fill, world, rank, nq_max)
+    if rank == 0:
+        full = ot.match()
+        got = dshard.concat_ranks(ranks)
+        fq = np.repeat(np.arange(n), np.diff(got["first"]))
+        ok = (np.array_equal(fq, full["query"]) and np.array_equal(got["candidate"], full["candidate"])
+              and np.array_equal(got["prob"], full["prob"]) and np.array_equal(got["kind"], full["kind"])
+              and total == full["pairs_scored"] and len(full["candidate"]) > 0)
+        out.put(bool(ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(target, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs)
+    return q
+
+
+def test_shared_batch_world2_gloo():
+    q = _spawn(_batch_worker)
+    got = sorted(q.get(timeout=5) for _ in range(2))
+    assert got == [(0, True), (1, True)]
+
+
+def test_region_overflow_is_collective_world2_gloo():
+    q = _spawn(_overflow_worker)
+    got = sorted(q.get(timeout=5) for _ in range(2))
+    assert got == [(0, True), (1, True)]
+
+
+def test_oracle_lists_cost_tiles_world2_gloo():
+    q = _spawn(_oracle_worker)
+    assert q.get(timeout=5) is True
