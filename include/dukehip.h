@@ -217,9 +217,79 @@ int dk_compare_values(dk_ctx* ctx, const dk_batch* pair, double* prob);
 int dk_property_similarity(dk_ctx* ctx, int prop, uint32_t r1, uint32_t r2, double* sim);
 int dk_set_overwrite(dk_ctx* ctx, int on);
 uint64_t dk_num_rows(const dk_ctx* ctx);
+/* IncrementalLuceneDatabase.findRecordById: the row of the live version of a record ID
+ * (dk_batch.ident numbering); DK_E_INVALID when none is indexed */
+int dk_row_of_ident(const dk_ctx* ctx, uint64_t ident, uint32_t* row);
 int dk_set_profiling(dk_ctx* ctx, int on);
 int dk_get_profile(const dk_ctx* ctx, dk_profile* out);
 int dk_reset_profile(dk_ctx* ctx);
+/* ---- native ingestion: a POSTed entity batch (JSON text, UTF-8) ->
+ * the SoA columns of a dk_batch, without building Duke Record objects.  Follows
+ * IncrementalDataSource.DatasetDataSourceRecordIterator.next (IncrementalDataSource.java:
+ * 50-101): `_id` (JsonElement.getAsString; missing/empty -> DK_E_INVALID "Got an entity
+ * with no '_id' attribute!"), one value per column (a JSON array contributes
+ * array.getAsString() per element: [] nothing, [x] x, longer -> DK_E_INVALID), the column's
+ * cleaner then RecordBuilder's empty-value skip, the synthetic ID
+ * "<group>__<dataset>__<entity>" and dukeDeleted (`_deleted`.getAsBoolean()).  Strict JSON
+ * only; lenient-Gson input, characters a native cleaner does not cover (>= U+0370) and a
+ * second value for one property return DK_E_UNSUPPORTED: that batch takes the caller's own
+ * packing path.  Record IDs are interned exactly into dk_interner ids (dk_batch.ident). */
+#define DK_CLEAN_NONE 0
+#define DK_CLEAN_LOWERCASE_NORMALIZE 1 /* cleaners.LowerCaseNormalizeCleaner (recalled) */
+#define DK_CLEAN_COUNTRY_NAME 2        /* examples.CountryNameCleaner (recalled) */
+#define DK_CLEAN_CAPITAL 3             /* examples.CapitalCleaner (recalled) */
+
+typedef struct dk_source_column {
+  const char* name;   /* JSON attribute (<column name>), UTF-8 */
+  int32_t prop;       /* schema property it fills (<column property>); -1 = not scored */
+  int32_t cleaner;    /* DK_CLEAN_* (<column cleaner>) */
+} dk_source_column;
+
+/* one part of a key: the property's cleaned value, optionally its whitespace token number
+ * `token` (Python str.split(); negative from the end; INT32_MIN = the whole value), sliced
+ * [start, end) in code points with Python slice rules (INT32_MIN = open end) */
+typedef struct dk_key_part {
+  int32_t prop, token, start, end;
+} dk_key_part;
+
+typedef struct dk_key_function {
+  int32_t nparts;
+  const dk_key_part* parts; /* the key is the parts' concatenation */
+} dk_key_function;
+
+typedef struct dk_source {
+  const char* dataset_id;          /* <param name="dataset-id">, UTF-8 */
+  int32_t group_no;                /* 0: Deduplication; 1 / 2: the RecordLinkage <group> */
+  int32_t ncolumns;
+  const dk_source_column* columns; /* in data-source order */
+  int32_t nprops;                  /* scored properties (schema order) of the packed batch */
+  int32_t nkeys;
+  const dk_key_function* keys;
+} dk_source;
+
+typedef struct dk_packed {
+  uint64_t n;
+  const dk_column* columns;     /* nprops, for dk_batch.columns */
+  const dk_column* key_columns; /* nkeys, for dk_batch.key_columns */
+  const uint64_t* ident;        /* interned record IDs, for dk_batch.ident */
+  const uint8_t* deleted;       /* dukeDeleted, for dk_batch.deleted */
+  const uint8_t* group;         /* dukeGroupNo (NULL in deduplication), for dk_batch.group */
+  dk_column id;                 /* the ID property value of every record */
+  dk_column entity_id;          /* dukeOriginalEntityId */
+} dk_packed;
+
+typedef struct dk_interner dk_interner;
+int dk_interner_create(dk_interner** out);
+void dk_interner_destroy(dk_interner* ids);
+uint64_t dk_interner_size(const dk_interner* ids);
+int dk_interner_find(const dk_interner* ids, const uint16_t* units, uint64_t n, uint64_t* id);
+/* out[i] = the id of record ID string i of `column` (interned if new): the same numbering
+ * dk_pack_json gives, for batches packed by the caller */
+int dk_interner_intern(dk_interner* ids, const dk_column* column, uint64_t n, uint64_t* out);
+int dk_pack_json(const dk_source* source, const char* json, uint64_t len, dk_interner* ids,
+                 dk_packed** out);
+void dk_free_packed(dk_packed* packed);
+
 const char* dk_last_error(void);
 int dk_abi_version(void);
 

@@ -411,6 +411,9 @@ static int validate_schema(const dk_schema* s) {
 
 const char* dk_last_error(void) { return g_err.c_str(); }
 
+// error hook of the host-only ingestion (dk_ingest.cpp)
+extern "C" int dk_fail_ingest(int code, const char* msg) { return fail(code, "%s", msg); }
+
 int dk_abi_version(void) { return DK_ABI_VERSION; }
 
 int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
@@ -474,6 +477,15 @@ void dk_destroy(dk_ctx* c) {
 }
 
 uint64_t dk_num_rows(const dk_ctx* c) { return c ? c->nrows : 0; }
+
+// IncrementalLuceneDatabase.findRecordById (:170-180): the row of the live version
+int dk_row_of_ident(const dk_ctx* c, uint64_t ident, uint32_t* row) {
+  if (!c || !row) return fail(DK_E_INVALID, "NULL argument");
+  const auto it = c->ident_row.find(ident);
+  if (it == c->ident_row.end()) return fail(DK_E_INVALID, "no indexed record with that ID");
+  *row = it->second;
+  return DK_OK;
+}
 
 int dk_set_profiling(dk_ctx* c, int on) {
   if (!c) return fail(DK_E_INVALID, "ctx is NULL");

@@ -28,8 +28,10 @@ MATCH_HOST, MATCH_DEVICE = 0, 1
 EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
            "dk_match", "dk_candidate_counts", "dk_result_copy_to_device",
            "dk_free_result", "dk_result_region_layout", "dk_set_result_region",
-           "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite", "dk_num_rows", "dk_set_profiling", "dk_get_profile",
-           "dk_reset_profile", "dk_last_error", "dk_abi_version")
+           "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite", "dk_num_rows", "dk_row_of_ident", "dk_set_profiling", "dk_get_profile",
+           "dk_reset_profile", "dk_last_error", "dk_abi_version",
+           "dk_interner_create", "dk_interner_destroy", "dk_interner_size", "dk_interner_find",
+           "dk_interner_intern", "dk_pack_json", "dk_free_packed")
 
 
 class DukeHipError(RuntimeError):
@@ -120,6 +122,8 @@ def load():
     L.dk_property_similarity.argtypes = [vp, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
     L.dk_num_rows.argtypes = [vp]
     L.dk_num_rows.restype = C.c_uint64
+    L.dk_row_of_ident.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint32)]
+    L.dk_row_of_ident.restype = C.c_int
     L.dk_set_profiling.argtypes = [vp, C.c_int]
     L.dk_get_profile.argtypes = [vp, C.POINTER(dk_profile)]
     L.dk_reset_profile.argtypes = [vp]

@@ -17,6 +17,8 @@ import numpy as np
 
 from . import _abi as A
 from .config import DukeConfig, ID_PROPERTY, GROUP_NO_PROPERTY_NAME, DELETED_PROPERTY_NAME
+from .config import ORIGINAL_ENTITY_ID_PROPERTY_NAME, DATASET_ID_PROPERTY_NAME
+from .ingest import Interner, NativeSource
 from .records import Record
 
 
@@ -158,6 +160,20 @@ class GpuEngine:
         A.check(fn(self.ctx, C.byref(b), rows.ctypes.data))
         return rows[:n]
 
+    def upsert_packed(self, packed, transient=False):
+        """dk_upsert of a natively packed batch (dukehip.ingest.PackedBatch)."""
+        b = packed.batch()
+        rows = np.zeros(max(1, packed.n), dtype=np.uint32)
+        fn = self.lib.dk_upsert_transient if transient else self.lib.dk_upsert
+        A.check(fn(self.ctx, C.byref(b), rows.ctypes.data))
+        return rows[:packed.n]
+
+    def row_of_ident(self, ident):
+        """dk_row_of_ident: the row of the live version of an interned record ID, or None."""
+        out = C.c_uint32()
+        rc = self.lib.dk_row_of_ident(self.ctx, int(ident), C.byref(out))
+        return None if rc != 0 else int(out.value)
+
     def drop_transient(self):
         A.check(self.lib.dk_drop_transient(self.ctx))
 
@@ -226,6 +242,74 @@ class GpuEngine:
         A.check(self.lib.dk_reset_profile(self.ctx))
 
 
+class RowStore:
+    """row -> Record for every indexed (and transient) row: Record objects of batches packed
+    in Python, and natively packed batches (dukehip.ingest) whose Records are built only
+    when a row is looked at (a listener callback, findRecordById)."""
+
+    def __init__(self, props):
+        self.props = props          # scored property names, schema order
+        self.segs = []              # (row0, n, list of Record | (PackedBatch, [groupNo]))
+        self.n = 0
+
+    def append_records(self, recs):
+        self.segs.append((self.n, len(recs), list(recs)))
+        self.n += len(recs)
+
+    def append_packed(self, packed, group_no=None):
+        self.segs.append((self.n, packed.n, (packed, group_no)))
+        self.n += packed.n
+
+    def truncate(self, n):
+        """Drop rows n.. (dk_drop_transient)."""
+        while self.segs and self.segs[-1][0] >= n:
+            self.segs.pop()
+        if self.segs and self.segs[-1][0] + self.segs[-1][1] > n:
+            r0, cnt, pay = self.segs[-1]
+            self.segs[-1] = (r0, n - r0, pay[:n - r0] if isinstance(pay, list) else pay)
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, row):
+        if isinstance(row, slice):
+            return [self[i] for i in range(*row.indices(self.n))]
+        if row < 0:
+            row += self.n
+        lo, hi = 0, len(self.segs)
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            if self.segs[mid][0] <= row:
+                lo = mid
+            else:
+                hi = mid
+        r0, cnt, pay = self.segs[lo]
+        if not (0 <= row - r0 < cnt):
+            raise IndexError(row)
+        if isinstance(pay, list):
+            return pay[row - r0]
+        return self._materialise(pay, row - r0)
+
+    def _materialise(self, pay, i):
+        packed, group_no = pay
+        cache = getattr(packed, "_cols", None)
+        if cache is None:
+            cache = packed._cols = ([packed.values(p) for p in range(len(self.props))],
+                                    packed.ids(), packed.entity_ids())
+        vals, ids, eids = cache
+        rec = Record({n: v[i] for n, v in zip(self.props, vals) if v[i] is not None})
+        if group_no:
+            rec.add_value(GROUP_NO_PROPERTY_NAME, str(group_no))
+        rec.add_value(ID_PROPERTY, ids[i])
+        rec.add_value(ORIGINAL_ENTITY_ID_PROPERTY_NAME, eids[i])
+        ds = ids[i].split("__", 2)[1 if group_no else 0]
+        rec.add_value(DATASET_ID_PROPERTY_NAME, ds)
+        if packed.deleted[i]:
+            rec.add_value(DELETED_PROPERTY_NAME, "true")
+        return rec
+
+
 class GpuBlockingDatabase:
     """Duke ``Database`` with key-function blocking, resident in HBM.
 
@@ -243,9 +327,10 @@ class GpuBlockingDatabase:
         self.schema, self.props = config.to_schema(mode, nkeys)
         self.engine = GpuEngine(self.schema, device)
         self.pending = []
-        self.rows = []          # row -> Record
-        self.by_id = {}         # ID -> row of the live version
-        self._ident = {}        # ID string -> dense identity number
+        self.rows = RowStore([p.name for p in self.props])   # row -> Record
+        self.by_id = {}         # ID -> row of the live version (Python-packed batches)
+        self.ids = Interner()   # ID string -> dense identity number (both packing paths)
+        self._native = {}       # DataSource id -> NativeSource
         self.overwrite = False
         self.indexing_disabled = False
         self._transient_row0 = None
@@ -279,6 +364,9 @@ class GpuBlockingDatabase:
 
     def find_record_by_id(self, rid):
         row = self.by_id.get(rid)
+        if row is None:
+            ident = self.ids.find(rid)
+            row = None if ident is None else self.engine.row_of_ident(ident)
         return None if row is None else self.rows[row]
 
     def close(self):
@@ -288,7 +376,7 @@ class GpuBlockingDatabase:
         """Removes the query-only rows of a batch processed with indexing disabled."""
         if self._transient_row0 is not None:
             self.engine.drop_transient()
-            del self.rows[self._transient_row0:]
+            self.rows.truncate(self._transient_row0)
             self._transient_row0 = None
 
     # --- bulk path ---
@@ -299,12 +387,10 @@ class GpuBlockingDatabase:
         n = len(records)
         if n == 0:
             return np.zeros(0, np.uint32)
-        ident = np.empty(n, dtype=np.uint64)
-        for i, r in enumerate(records):
-            rid = r.get_value(ID_PROPERTY)
-            if rid is None:
-                raise ValueError("record without ID property")
-            ident[i] = self._ident.setdefault(rid, len(self._ident))
+        rids = [r.get_value(ID_PROPERTY) for r in records]
+        if any(rid is None for rid in rids):
+            raise ValueError("record without ID property")
+        ident = self.ids.intern(rids)
         cols = []
         for p in self.props:
             vals = []
@@ -334,11 +420,51 @@ class GpuBlockingDatabase:
                                   key_columns=key_cols, transient=transient)
         if transient and self._transient_row0 is None:
             self._transient_row0 = len(self.rows)
-        for r, row in zip(records, rows):
-            self.rows.append(r)
-            if not transient:
-                self.by_id[r.get_value(ID_PROPERTY)] = int(row)
+        self.rows.append_records(records)
+        if not transient:
+            for rid, row in zip(rids, rows):
+                self.by_id[rid] = int(row)
         return rows
+
+    def native_source(self, source):
+        ns = self._native.get(id(source))
+        if ns is None:
+            ns = self._native[id(source)] = (NativeSource(source, [p.name for p in self.props],
+                                                          self.key_functions), source)
+        return ns[0]
+
+    def index_json(self, body, source, transient=None):
+        """The POSTed batch `body` (JSON text) of data source `source`, packed natively
+        (dk_pack_json) and upserted (or appended as transient rows).  Returns (rows,
+        packed).  Raises dukehip.ingest.NativeUnsupported for a batch the native reader
+        declines (the caller then uses records_from_entities + index_batch)."""
+        transient = self.indexing_disabled if transient is None else bool(transient)
+        packed = self.native_source(source).pack(body, self.ids)
+        if packed.n == 0:
+            return np.zeros(0, np.uint32), packed
+        if self.mode == A.MODE_LINKAGE and not source.group_no:
+            raise ValueError(f"The '{GROUP_NO_PROPERTY_NAME}' property was missing")
+        rows = self.engine.upsert_packed(packed, transient=transient)
+        if transient and self._transient_row0 is None:
+            self._transient_row0 = len(self.rows)
+        self.rows.append_packed(packed, source.group_no)
+        return rows, packed
+
+
+class _RowView:
+    """records[i] of a batch whose rows are row0 .. row0+n-1 of a RowStore."""
+
+    def __init__(self, rows, row0, n):
+        self.rows, self.row0, self.n = rows, row0, n
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        return (self.rows[self.row0 + i] for i in range(self.n))
+
+    def __getitem__(self, i):
+        return self.rows[self.row0 + i]
 
 
 class GpuProcessor:
@@ -385,6 +511,29 @@ class GpuProcessor:
             l.batch_done()
         if self.database.indexing_disabled:
             self.database.drop_transient()   # the batch never entered the index
+        return res
+
+    def deduplicate_json(self, body, source):
+        """Processor.deduplicate of a POSTed batch given as JSON text: packed natively
+        (dk_pack_json, no Record objects on the way in), then the same index + commit +
+        match + callback replay as deduplicate().  Records handed to the listeners are
+        built only for the rows they name."""
+        db = self.database
+        pending, db.pending = db.pending, []
+        if pending:
+            db.index_batch(pending)
+        rows, packed = db.index_json(body, source)
+        n = len(rows)
+        for l in self.listeners:
+            l.batch_ready(n)
+        res = db.engine.match(rows)
+        if self.listeners:
+            row0 = int(rows[0]) if n else 0
+            self._replay(_RowView(db.rows, row0, n), res)
+        for l in self.listeners:
+            l.batch_done()
+        if db.indexing_disabled:
+            db.drop_transient()
         return res
 
     def _replay(self, records, res: MatchResult):

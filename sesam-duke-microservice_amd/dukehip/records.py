@@ -57,6 +57,18 @@ def _gson_as_string(el):
     return str(el)
 
 
+def _gson_as_boolean(el):
+    """com.google.gson.JsonElement.getAsBoolean: booleans, Boolean.parseBoolean of a string
+    or number's text, a one-element array's element; null / objects / other arrays throw."""
+    if isinstance(el, bool):
+        return el
+    if isinstance(el, list) and len(el) == 1:
+        return _gson_as_boolean(el[0])
+    if isinstance(el, str):
+        return el.lower() == "true"
+    raise ValueError("getAsBoolean is unsupported on %s" % type(el).__name__)
+
+
 class JsonNumber(str):
     """A JSON number kept as its source text (Gson's LazilyParsedNumber): getAsString and
     re-serialisation both give the literal back unchanged."""
@@ -78,6 +90,8 @@ def records_from_entities(entities, source, cleaners=None):
     cleaners = CLEANERS if cleaners is None else cleaners
     out = []
     for entity in entities:
+        if not isinstance(entity, dict):  # (JsonObject) cast, IncrementalDataSource.java:51
+            raise ValueError("an entity of the batch is not a JSON object")
         eid = entity.get("_id")
         eid = None if eid is None else _gson_as_string(eid)
         if not eid:
@@ -107,8 +121,7 @@ def records_from_entities(entities, source, cleaners=None):
         rec.add_value(ID_PROPERTY, rid)
         rec.add_value(ORIGINAL_ENTITY_ID_PROPERTY_NAME, eid)
         rec.add_value(DATASET_ID_PROPERTY_NAME, source.dataset_id)
-        deleted = entity.get("_deleted")
-        if deleted is not None and str(deleted).lower() == "true":
+        if "_deleted" in entity and _gson_as_boolean(entity["_deleted"]):
             rec.add_value(DELETED_PROPERTY_NAME, "true")
         out.append(rec)
     return out

@@ -528,3 +528,45 @@ def test_symmetric_schedule_overwrite_duplicates():
     assert_same(eng.match(q), ot.match(q))
     assert eng.profile()["sym_matches"] == 1
     eng.close()
+
+
+# ---------------------------------------------------------------------------------------
+# native ingestion (dk_pack_json) through the processor == the Record path
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("linkage", [False, True])
+def test_deduplicate_json_equals_record_path(linkage):
+    with open(os.path.join(GOLDEN, "testdukeconfig_schema.json")) as f:
+        key = "RecordLinkage/countries-dbpedia-mondial" if linkage else "Deduplication/countries-dbpedia-mondial"
+        cfg_d = json.load(f)["pipelines"][key]
+    kf = [dh.PartsKey(("NAME", None, 0, 3))]
+    procs, lis = [], []
+    for _ in range(2):
+        cfg = DukeConfig.from_dict(cfg_d)
+        db = dh.GpuBlockingDatabase(cfg, kf)
+        p = dh.GpuProcessor(cfg, db)
+        l = dh.CollectingListener()
+        p.add_match_listener(l)
+        procs.append(p)
+        lis.append(l)
+    srcs = procs[0].config.data_sources
+    for si, (seed, src_i) in enumerate(((11, 0), (12, 1), (13, 0))):
+        ents = stress_entities(1500, seed)
+        for e in ents[::50]:
+            e["country"] = "  The " + e["country"].upper() + "  "   # the cleaners at work
+        body = json.dumps(ents)
+        src0, src1 = procs[0].config.data_sources[src_i], procs[1].config.data_sources[src_i]
+        ref = procs[0].deduplicate(dh.records_from_entities(dh.parse_entities(body)[0], src0))
+        got = procs[1].deduplicate_json(body, src1)
+        assert got.n == ref.n and got.pairs_scored == ref.pairs_scored
+        for k in ("first", "candidate", "prob", "kind"):
+            assert np.array_equal(getattr(got, k), getattr(ref, k)), k
+    assert lis[0].events == lis[1].events and len(lis[0].events) > 100
+    # findRecordById through the native rows
+    db0, db1 = procs[0].database, procs[1].database
+    some = [e for e in lis[0].events if e[0] == "matches"][:20]
+    for ev in some:
+        r0, r1 = db0.find_record_by_id(ev[2]), db1.find_record_by_id(ev[2])
+        assert r1 is not None and r1.get_values("NAME") == r0.get_values("NAME")
+        assert r1.get_value("dukeOriginalEntityId") == r0.get_value("dukeOriginalEntityId")
+    for p in procs:
+        p.database.close()

@@ -1,0 +1,162 @@
+"""CPU: native ingestion (dk_pack_json, host code of libdukehip.so) against the Python
+restatement of IncrementalDataSource.java:50-101 (dukehip.records.records_from_entities +
+Column packing + PartsKey) on the same JSON bodies, and its error contract."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+import dukehip as dh
+from dukehip import _abi as A
+from dukehip import ingest as I
+from dukehip.config import DataSource, DataSourceColumn
+
+CLEAN = {"lc": "no.priv.garshol.duke.cleaners.LowerCaseNormalizeCleaner",
+         "country": "no.priv.garshol.duke.examples.CountryNameCleaner",
+         "capital": "no.priv.garshol.duke.examples.CapitalCleaner"}
+
+
+def source(group=None):
+    cols = [DataSourceColumn("name", "NAME", CLEAN["country"]),
+            DataSourceColumn("city", "CITY", CLEAN["capital"]),
+            DataSourceColumn("note", "NOTE", CLEAN["lc"]),
+            DataSourceColumn("area", "AREA", None),
+            DataSourceColumn("raw", "RAW", None),
+            DataSourceColumn("extra", "UNSCORED", None)]
+    return DataSource("ds-1", cols, group)
+
+
+PROPS = ["AREA", "NAME", "CITY", "NOTE", "RAW"]
+KEYS = [dh.PartsKey(("NAME", None, 0, 3), ("AREA", None, None, None)),
+        dh.PartsKey(("NOTE", -1, -2, None)), dh.PartsKey(("RAW", 0, 1, 5), ("CITY", 1, None, 2))]
+
+
+def rand_text(rng, alpha, lo, hi):
+    return "".join(rng.choice(alpha) for _ in range(rng.randint(lo, hi)))
+
+
+def rand_entities(rng, n):
+    latin = list("abcdeABCDE  \t\xa0\n,()") + ["é", "Ø", "ñ", "ß", "Å", "́", "the ", ", the"]
+    wide = latin + ["ł", "€", "\U0001F600", " "]
+    ents = []
+    for i in range(n):
+        e = {"_id": rng.choice([str(i), i, f"x{i}"])}
+        if rng.random() < 0.9:
+            e["name"] = rand_text(rng, latin, 0, 14)
+        if rng.random() < 0.8:
+            e["city"] = [rand_text(rng, latin, 1, 10)] if rng.random() < 0.2 else rand_text(rng, latin, 0, 12)
+        if rng.random() < 0.8:
+            e["note"] = rand_text(rng, latin, 0, 20)
+        if rng.random() < 0.8:
+            e["area"] = rng.choice([rng.randint(-5, 50), rng.random() * 100, "7", True, False, [3], []])
+        if rng.random() < 0.8:
+            e["raw"] = rand_text(rng, wide, 0, 12)
+        if rng.random() < 0.3:
+            e["extra"] = rand_text(rng, wide, 0, 5)
+        if rng.random() < 0.2:
+            e["_deleted"] = rng.choice([True, False, "TRUE", "no", 1, [True]])
+        ents.append(e)
+    return ents
+
+
+def reference(body, src):
+    ents, _ = dh.parse_entities(body)
+    recs = dh.records_from_entities(ents, src)
+    vals = [[r.get_value(p) for r in recs] for p in PROPS]
+    keys = [[kf.make_key(r) for r in recs] for kf in KEYS]
+    return recs, vals, keys
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_pack_json_matches_python_path(seed):
+    rng = random.Random(seed)
+    src = source(group=None if seed % 2 == 0 else 1 + seed % 2)
+    ns = I.NativeSource(src, PROPS, KEYS)
+    it = I.Interner()
+    ents = rand_entities(rng, 300)
+    body = json.dumps(ents, ensure_ascii=bool(seed % 3 == 0))
+    recs, vals, keys = reference(body, src)
+    pk = ns.pack(body, it)
+    assert pk.n == len(recs)
+    for p in range(len(PROPS)):
+        assert pk.values(p) == vals[p], PROPS[p]
+    for k in range(len(KEYS)):
+        assert pk.keys(k) == keys[k]
+    assert pk.ids() == [r.get_value("ID") for r in recs]
+    assert pk.entity_ids() == [r.get_value("dukeOriginalEntityId") for r in recs]
+    assert list(pk.deleted) == [r.get_value("dukeDeleted") == "true" for r in recs]
+    # exact interning: equal IDs <=> equal idents, stable across batches
+    ids = [r.get_value("ID") for r in recs]
+    ident = list(pk.ident)
+    assert len(set(ident)) == len(set(ids))
+    for a, b in zip(ids, ident):
+        assert it.find(a) == b
+    pk2 = ns.pack(body, it)
+    assert list(pk2.ident) == ident
+    # the columns are what Column.from_strings builds (layout the GPU path takes)
+    for p in range(len(PROPS)):
+        ref_col = A.Column.from_strings(vals[p])
+        c = pk.ptr.contents.columns[p]
+        off = np.ctypeslib.as_array(C_u32(c.offsets), (pk.n + 1,))
+        assert np.array_equal(off, ref_col.offsets)
+        assert c.width == ref_col.units.itemsize
+
+
+def C_u32(p):
+    import ctypes as C
+    return C.cast(p, C.POINTER(C.c_uint32))
+
+
+def test_single_entity_body_and_duplicate_members():
+    src = source()
+    ns = I.NativeSource(src, PROPS, KEYS)
+    it = I.Interner()
+    body = '{"_id": "a1", "name": "X", "name": "The Gambia", "area": 1e3, "raw": "\\u00e9\\ud83d\\ude00"}'
+    pk = ns.pack(body, it)
+    recs, vals, keys = reference(body, src)
+    assert pk.n == 1 and pk.values(1) == ["gambia"] == vals[1]
+    assert pk.values(0) == ["1e3"] and pk.values(4) == ["é\U0001F600"]
+    assert pk.ids() == ["ds-1__a1"]
+
+
+@pytest.mark.parametrize("body,code", [
+    ('[{"name": "x"}]', A.DK_E_INVALID),                  # no _id
+    ('[{"_id": ""}]', A.DK_E_INVALID),                    # empty _id
+    ('[{"_id": null}]', A.DK_E_INVALID),                  # JsonNull.getAsString
+    ('[{"_id": "1", "name": null}]', A.DK_E_INVALID),
+    ('[{"_id": "1", "name": ["a", "b"]}]', A.DK_E_INVALID),  # JsonArray.getAsString
+    ('[{"_id": "1", "name": {"a": 1}}]', A.DK_E_INVALID),
+    ('[{"_id": "1", "_deleted": null}]', A.DK_E_INVALID),
+    ('[1, 2]', A.DK_E_INVALID),                           # entities must be objects
+])
+def test_pack_json_errors(body, code):
+    ns = I.NativeSource(source(), PROPS, KEYS)
+    with pytest.raises(A.DukeHipError) as e:
+        ns.pack(body, I.Interner())
+    assert e.value.code == code
+    if body in ('[{"name": "x"}]', '[{"_id": ""}]'):
+        assert "Got an entity with no '_id' attribute!" in A.load().dk_last_error().decode()
+    with pytest.raises(ValueError):   # the Python restatement rejects the same batches
+        ents, _ = dh.parse_entities(body)
+        dh.records_from_entities(ents, source())
+
+
+@pytest.mark.parametrize("body", [
+    "[{'_id': 'a'}]",                                      # lenient (Gson) JSON
+    '[{"_id": "a", "name": "€"}]',                    # outside the cleaner table
+    '[{"_id": "a", "raw": "x"}] junk',
+])
+def test_pack_json_declines(body):
+    ns = I.NativeSource(source(), PROPS, KEYS)
+    with pytest.raises(I.NativeUnsupported):
+        ns.pack(body, I.Interner())
+
+
+def test_second_value_for_a_property_declines():
+    src = DataSource("d", [DataSourceColumn("a", "NAME", None), DataSourceColumn("b", "NAME", None)])
+    ns = I.NativeSource(src, ["NAME"], [])
+    with pytest.raises(I.NativeUnsupported):
+        ns.pack('[{"_id": "1", "a": "x", "b": "y"}]', I.Interner())
+    pk = ns.pack('[{"_id": "1", "a": "x", "b": ""}]', I.Interner())   # empty: skipped
+    assert pk.values(0) == ["x"]
