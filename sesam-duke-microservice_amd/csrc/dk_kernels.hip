@@ -1081,9 +1081,9 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
 // Block-ordered compaction of a 256-slot block's decisions: wave ballots -> per-wave
 // counts in LDS -> slot-ordered entries at the block's staging region (no atomics on
 // entries), plus the block's scored-pair and operand-byte sums.
-__device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, double prob,
-                                           uint32_t crow, uint32_t qi, uint32_t scored,
-                                           uint32_t bytes) {
+__device__ __forceinline__ void block_emit_at(const StageOut& out, uint64_t blk, uint32_t kind,
+                                              double prob, uint32_t crow, uint32_t qi,
+                                              uint32_t scored, uint32_t bytes) {
   __shared__ uint32_t wcount[kScoreBlock / 64], wscored[kScoreBlock / 64], wbytes[kScoreBlock / 64];
   const uint32_t wave = threadIdx.x >> 6;
   const uint64_t em = __ballot(kind != 0);
@@ -1106,7 +1106,7 @@ __device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, d
     total += cw;
   }
   if (kind != 0) {
-    const uint64_t e = (uint64_t)blockIdx.x * kScoreBlock + before + mask_rank(em);
+    const uint64_t e = blk * kScoreBlock + before + mask_rank(em);
     out.prob[e] = prob;
     out.cand[e] = crow | (kind << kKindShift);
     out.qidx[e] = qi;
@@ -1118,10 +1118,17 @@ __device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, d
       ns += wscored[w];
       nb += wbytes[w];
     }
-    out.bcnt[blockIdx.x] = total;
-    out.bscored[blockIdx.x] = ns;
-    out.bbytes[blockIdx.x] = nb;
+    out.bcnt[blk] = total;
+    out.bscored[blk] = ns;
+    out.bbytes[blk] = nb;
   }
+  __syncthreads();  // the counts in LDS are reused by the block's next call
+}
+
+__device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, double prob,
+                                           uint32_t crow, uint32_t qi, uint32_t scored,
+                                           uint32_t bytes) {
+  block_emit_at(out, blockIdx.x, kind, prob, crow, qi, scored, bytes);
 }
 
 // [Duke 1.2] Processor.compareCandidatesSimple: strict thresholds
@@ -1297,13 +1304,21 @@ void k_score_long(const ScoreParams P, const PairSource S,
 // order (key function, then bucket position); each reads its probability from the owner
 // results -- its own (owned candidates) or the candidate's (candidates in [qa, pq), which
 // own the pair) -- and goes through the same thresholds and block-ordered compaction as
-// k_score.  HBM-bound: a 4-byte row and an 8-byte probability per slot.
-__global__ __launch_bounds__(256) void k_emit(const EmitSource S, uint64_t slot0, uint64_t nslots,
-                                              StageOut out) {
-  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool valid = idx < nslots;
-  const uint64_t s = slot0 + min(idx, nslots - 1);
+// k_score.  A chain of dependent loads per slot (wave map -> offsets -> bucket record ->
+// owner base -> result): each thread walks kEmitGroups slot groups of 64 with the chains
+// of all groups in flight together, instead of one short-lived wave per group.
+constexpr int kEmitGroups = 4;
+
+struct EmitSlot {
+  uint32_t qi, crow;
+  double prob;
+  bool valid;
+};
+
+__device__ __forceinline__ EmitSlot emit_resolve(const EmitSource& S, uint64_t s, bool valid) {
+  EmitSlot o{0u, 0u, __builtin_nan(""), false};
   const uint32_t qi = __builtin_amdgcn_readfirstlane(S.wq[s >> 6]);
+  o.qi = qi;
   uint64_t t = s - S.qoff[qi];
   int k = -1;
   uint4 r = make_uint4(0, 0, 0, 0);
@@ -1320,24 +1335,43 @@ __global__ __launch_bounds__(256) void k_emit(const EmitSource S, uint64_t slot0
     }
   }
   valid = valid && k >= 0;
-  double prob = __builtin_nan("");
-  uint32_t crow = 0;
   if (valid) {
     const uint32_t x = r.x + (uint32_t)t;
-    crow = S.rowof[(uint64_t)k * S.m + x];
+    o.crow = S.rowof[(uint64_t)k * S.m + x];
     const bool in_t = r.w != kNoPos;
     if (in_t && x == r.w) {
       valid = false;  // the query itself (Processor.isSameAs)
     } else if (in_t && x >= r.z && x < r.w) {
       // the candidate owns the pair and pushed compare(this query, it) to our mirror run
-      prob = S.mres[S.mbase[(uint64_t)k * S.nq + qi] + (x - r.z)];
+      o.prob = S.mres[S.mbase[(uint64_t)k * S.nq + qi] + (x - r.z)];
     } else {
       const uint64_t base = S.obase[(uint64_t)k * S.nq + qi];
-      prob = S.ores[x < r.z ? base - (r.z - x) : base + (x - r.w - 1)];
+      o.prob = S.ores[x < r.z ? base - (r.z - x) : base + (x - r.w - 1)];
     }
   }
-  const uint32_t kind = valid ? decide(prob, S.threshold, S.maybe) : 0u;
-  block_emit(out, kind, prob, crow, qi, 0u, 0u);
+  o.valid = valid;
+  return o;
+}
+
+__global__ __launch_bounds__(256) void k_emit(const EmitSource S, uint64_t slot0, uint64_t nslots,
+                                              StageOut out) {
+  // block b covers kEmitGroups consecutive 256-slot staging blocks; wave w of the block
+  // takes slot group g of each: slots (b * G + g) * 256 + w * 64 + lane
+  EmitSlot e[kEmitGroups];
+#pragma unroll
+  for (int g = 0; g < kEmitGroups; ++g) {
+    const uint64_t idx = ((uint64_t)blockIdx.x * kEmitGroups + g) * kScoreBlock + threadIdx.x;
+    const bool in = idx < nslots;
+    const uint64_t s = slot0 + min(idx, nslots - 1);
+    e[g] = emit_resolve(S, s, in);
+  }
+#pragma unroll
+  for (int g = 0; g < kEmitGroups; ++g) {
+    const uint64_t blk = (uint64_t)blockIdx.x * kEmitGroups + g;
+    if (blk * kScoreBlock >= nslots) break;  // block-uniform: past the chunk's staging blocks
+    const uint32_t kind = e[g].valid ? decide(e[g].prob, S.threshold, S.maybe) : 0u;
+    block_emit_at(out, blk, kind, e[g].prob, e[g].crow, e[g].qi, 0u, 0u);
+  }
 }
 
 // Sum the per-block counters of a chunk into counters[0..1]: one atomic pair per block
@@ -1748,7 +1782,7 @@ hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint6
 hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, const StageOut& out,
                        hipStream_t s) {
   DK_LAUNCH_GUARD(nslots);
-  k_emit<<<grid1d(nslots, kScoreBlock), kScoreBlock, 0, s>>>(src, slot0, nslots, out);
+  k_emit<<<grid1d(nslots, kScoreBlock * kEmitGroups), kScoreBlock, 0, s>>>(src, slot0, nslots, out);
   return hipGetLastError();
 }
 
