@@ -486,11 +486,29 @@ __device__ __forceinline__ T from_left(T top, T v, int k) {
   return k == 0 ? top : x;
 }
 
-// Per-wave LDS of the long-value section (inside the wave's Peq slice, zeroed on exit):
-// u16 s2 units [4 rows][kMaxLongUnits], f64 results [64], u32 lane list [64].
-constexpr int kLongS2Words = 4 * kMaxLongUnits * 2 / 8;  // u64 words of the s2 staging
+// Per-wave LDS of the long-value section (inside the wave's table slice, zeroed on exit):
+// s2 units packed with their weight class [4 rows][kMaxLongUnits] (u32: unit | class << 16,
+// so one read per DP step gives both the unit and its WeightedLevenshtein weight), f64
+// results [64], u32 lane list [64].  The long-value kernels give each wave a larger slice.
+constexpr int kLongS2Words = 4 * kMaxLongUnits * 4 / 8;  // u64 words of the s2 staging
 constexpr int kLongLdsWords = kLongS2Words + 64 + 32;
-static_assert(kLongLdsWords <= kPeqEntries, "long-value LDS must fit the Peq slice");
+constexpr int kPeqEntriesLong = kLongLdsWords;
+static_assert(kPeqEntriesLong >= kPeqEntries, "the long slice holds the Peq tables too");
+
+// [Duke 1.2] WeightedLevenshtein.DefaultWeightEstimator weight class of a unit: 0 = 1.0
+// (letters, anything else), 1 = 2.0 (digits), 2 = 0.1 (punctuation and space)
+__device__ __forceinline__ uint32_t wl_class(uint32_t ch) {
+  if ((ch | 0x20u) - 'a' < 26u) return 0u;
+  if (ch - '0' < 10u) return 1u;
+  constexpr uint64_t kPunct = (1ull << ' ') | (1ull << '"') | (1ull << '\'') | (1ull << ',') |
+                              (1ull << '-') | (1ull << '.') | (1ull << '/');
+  if ((ch < 64u && ((kPunct >> ch) & 1ull)) || ch == '\\') return 2u;
+  return 0u;
+}
+
+__device__ __forceinline__ double wl_class_weight(uint32_t cls) {
+  return cls == 1u ? 2.0 : (cls == 2u ? 0.1 : 1.0);
+}
 
 template <int G, int R, bool WL, typename CT>
 __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint64_t* lds, const CT* s1p,
@@ -498,21 +516,23 @@ __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint
   using T = typename std::conditional<WL, double, int>::type;
   constexpr int UPW = 4 / (int)sizeof(CT);
   constexpr int NG = 64 / G;  // candidates per round
-  uint16_t* s2buf = reinterpret_cast<uint16_t*>(lds);
+  uint32_t* s2buf = reinterpret_cast<uint32_t*>(lds);
   double* res = reinterpret_cast<double*>(lds + kLongS2Words);
   const uint32_t* list = reinterpret_cast<const uint32_t*>(lds + kLongS2Words + 64);
   const int lane = (int)lane_id();
   const int grp = lane / G, k = lane % G;
   const int kstar = (n1 - 1) / R, rstar = n1 - kstar * R;
-  uint16_t* row_s2 = s2buf + grp * kMaxLongUnits;
-  // this lane's query rows
+  uint32_t* row_s2 = s2buf + grp * kMaxLongUnits;
+  // this lane's query rows, packed like the staged candidate units (equal packed values
+  // <=> equal units: the class is a function of the unit)
   uint32_t c1[R];
   double w1[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int i = k * R + r;
-    c1[r] = i < n1 ? (uint32_t)s1p[i] : 0xFFFFFFFFu;  // rows past n1 never match
-    w1[r] = WL ? wl_weight(c1[r]) : 0.0;
+    const uint32_t ch = i < n1 ? (uint32_t)s1p[i] : 0u;
+    c1[r] = i < n1 ? (ch | (wl_class(ch) << 16)) : 0xFFFFFFFFu;  // rows past n1 never match
+    w1[r] = WL ? wl_weight(ch) : 0.0;
   }
   const CT* base = reinterpret_cast<const CT*>(D.units);
   for (int r0 = 0; r0 < nneed; r0 += NG) {
@@ -534,7 +554,10 @@ __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint
     for (int w = k; w < nw; w += G) {
       const uint32_t x = s2.word(w);
 #pragma unroll
-      for (int u = 0; u < UPW; ++u) row_s2[w * UPW + u] = (uint16_t)Str<CT>::unit(x, u);
+      for (int u = 0; u < UPW; ++u) {
+        const uint32_t ch = Str<CT>::unit(x, u);
+        row_s2[w * UPW + u] = ch | (wl_class(ch) << 16);
+      }
     }
     wave_lds_sync();
     int tmax = n2 > 0 ? n2 + kstar : 0;
@@ -557,7 +580,7 @@ __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint
       if (j >= 1 && j <= n2) {
         T up = recv, dg = prev;
         if (WL) {
-          const double w2 = wl_weight(ch2);
+          const double w2 = wl_class_weight(ch2 >> 16);
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             const double old = col[r];
@@ -628,8 +651,8 @@ __device__ __forceinline__ double long_sims(const DevProp& D, uint64_t rstride, 
   else if (n1 <= 32) long_dp<16, 2, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
   else if (n1 <= 48) long_dp<16, 3, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
   else if (n1 <= 64 || LR <= 4) long_dp<16, 4, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 96) long_dp<32, 3, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 128 || LR <= 8) long_dp<32, 4, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 96) long_dp<16, 6, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  else if (n1 <= 128 || LR <= 8) long_dp<16, 8, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
   else if (n1 <= 160) long_dp<32, (LR < 16 ? 4 : 5), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
   else if (n1 <= 192) long_dp<32, (LR < 16 ? 4 : 6), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
   else if (n1 <= 224) long_dp<32, (LR < 16 ? 4 : 7), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
@@ -1151,10 +1174,11 @@ __device__ __forceinline__ double property_prob(const DevProp& D, double sim) {
 template <int RMAX, int LR, bool SYM>
 __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
                                            uint64_t nslots, const StageOut& out) {
-  __shared__ uint64_t peq_all[kScoreBlock / 64][kPeqEntries];
+  constexpr int PE = LR > 0 ? kPeqEntriesLong : kPeqEntries;  // the long DP stages more
+  __shared__ uint64_t peq_all[kScoreBlock / 64][PE];
   const uint32_t wave = threadIdx.x >> 6;
   uint64_t* peq = peq_all[wave];
-  for (int e = (int)lane_id(); e < kPeqEntries; e += 64) peq[e] = 0;
+  for (int e = (int)lane_id(); e < PE; e += 64) peq[e] = 0;
 
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in_launch = idx < nslots;
