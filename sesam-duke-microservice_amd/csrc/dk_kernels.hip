@@ -486,14 +486,18 @@ __device__ __forceinline__ T from_left(T top, T v, int k) {
   return k == 0 ? top : x;
 }
 
-// Per-wave LDS of the long-value section (inside the wave's table slice, zeroed on exit):
-// s2 units packed with their weight class [4 rows][kMaxLongUnits] (u32: unit | class << 16,
-// so one read per DP step gives both the unit and its WeightedLevenshtein weight), f64
-// results [64], u32 lane list [64].  The long-value kernels give each wave a larger slice.
-constexpr int kLongS2Words = 4 * kMaxLongUnits * 4 / 8;  // u64 words of the s2 staging
-constexpr int kLongLdsWords = kLongS2Words + 64 + 32;
-constexpr int kPeqEntriesLong = kLongLdsWords;
-static_assert(kPeqEntriesLong >= kPeqEntries, "the long slice holds the Peq tables too");
+// Per-wave LDS of the long-value section, inside the wave's table slice (zeroed on exit so
+// the Peq tables stay clear), in u64 words:
+//   [kLongPtr, +64)   candidate unit pointers by sorted position
+//   [kLongMeta, +32)  u32 by sorted position: n2 | src lane << 16 (first the sort keys)
+//   [kLongRes, +64)   D(n1, n2) by lane (f64 or int bits)
+//   [kLongRing, +256) u32 unit rings [4 groups][128]: unit | weight class << 16
+constexpr int kLongPtr = 0, kLongMeta = 64, kLongRes = 96, kLongRing = 160;
+// the scoring kernels' per-wave table slices (namespace scope, so the out-of-line long DP
+// addresses them as LDS)
+__shared__ uint64_t g_wave_tables[kScoreBlock / 64][kPeqEntries];
+constexpr int kLongLdsWords = kLongRing + 256;
+static_assert(kLongLdsWords <= kPeqEntries, "the long section lives in the wave's Peq slice");
 
 // [Duke 1.2] WeightedLevenshtein.DefaultWeightEstimator weight class of a unit: 0 = 1.0
 // (letters, anything else), 1 = 2.0 (digits), 2 = 0.1 (punctuation and space)
@@ -510,21 +514,44 @@ __device__ __forceinline__ double wl_class_weight(uint32_t cls) {
   return cls == 1u ? 2.0 : (cls == 2u ? 0.1 : 1.0);
 }
 
+// The wave's candidates stream through NG = 64/G lane groups.  long_sims sorts them
+// longest first; group grp takes sorted positions grp, 2NG-1-grp, 2NG+grp, ... (dealt
+// snake-wise, so the groups' column totals come out nearly equal) and runs their DP
+// matrices back to back as ONE systolic stream of columns: lane k works on stream column
+// t - k at step t, so a lane moves on to its next candidate one step after its left
+// neighbour and the pipeline never drains between candidates.  Stream units come from a
+// 128-unit LDS ring per group (two 64-unit blocks): block b+1 is written at step 64b + 32,
+// from registers loaded 64 steps earlier, into the half the group's last lane left 32+
+// steps before; every lane reads its unit one step ahead.  D(n1, n2) leaves as raw bits
+// (long_sims turns it into the similarity), so the candidate switch stays small.
+//
+// Out of line: the stream's registers (column, weights, units, ring cursor) get an
+// allocation of their own instead of competing with the fused kernel's live state, which
+// spilled the weights and units inside the cell loop.
 template <int G, int R, bool WL, typename CT>
-__device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint64_t* lds, const CT* s1p,
-                                        int n1, uint32_t g, uint32_t crow, int lc, int nneed) {
+__device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1p, int n1, int nneed) {
+  uint64_t* lds = g_wave_tables[threadIdx.x >> 6];
   using T = typename std::conditional<WL, double, int>::type;
   constexpr int UPW = 4 / (int)sizeof(CT);
-  constexpr int NG = 64 / G;  // candidates per round
-  uint32_t* s2buf = reinterpret_cast<uint32_t*>(lds);
-  double* res = reinterpret_cast<double*>(lds + kLongS2Words);
-  const uint32_t* list = reinterpret_cast<const uint32_t*>(lds + kLongS2Words + 64);
+  constexpr int NG = 64 / G;  // candidate streams
+  constexpr int UL = 64 / G;  // ring units a lane stages per block
+  static_assert(G <= 32, "the ring half is rewritten 32 steps into the block");
+  const uint64_t* cptr = lds + kLongPtr;
+  const uint32_t* meta = reinterpret_cast<const uint32_t*>(lds + kLongMeta);
+  uint64_t* rbits = lds + kLongRes;
   const int lane = (int)lane_id();
   const int grp = lane / G, k = lane % G;
+  uint32_t* ring = reinterpret_cast<uint32_t*>(lds + kLongRing) + grp * 128;
   const int kstar = (n1 - 1) / R, rstar = n1 - kstar * R;
-  uint32_t* row_s2 = s2buf + grp * kMaxLongUnits;
-  // this lane's query rows, packed like the staged candidate units (equal packed values
-  // <=> equal units: the class is a function of the unit)
+  auto spos = [&](int m) { return m * NG + ((m & 1) ? NG - 1 - grp : grp); };
+  const int cnt = nneed / NG + (spos(nneed / NG) < nneed ? 1 : 0);
+  int tlen = 0;
+  for (int m = 0; m < cnt; ++m) tlen += (int)(meta[spos(m)] & 0xFFFFu);
+  for (int o = 32; o > 0; o >>= 1) tlen = max(tlen, __shfl_xor(tlen, o));
+  const int tend = tlen + kstar + 1;  // lane kstar closes its last matrix at step tlen + kstar
+
+  // this lane's query rows, packed like the ring units (equal packed values <=> equal
+  // units: the class is a function of the unit)
   uint32_t c1[R];
   double w1[R];
 #pragma unroll
@@ -534,98 +561,126 @@ __device__ __forceinline__ void long_dp(const DevProp& D, uint64_t rstride, uint
     c1[r] = i < n1 ? (ch | (wl_class(ch) << 16)) : 0xFFFFFFFFu;  // rows past n1 never match
     w1[r] = WL ? wl_weight(ch) : 0.0;
   }
-  const CT* base = reinterpret_cast<const CT*>(D.units);
-  for (int r0 = 0; r0 < nneed; r0 += NG) {
-    const int idx = r0 + grp;
-    const bool has = idx < nneed;
-    const int src = has ? (int)list[idx] : 0;
-    // cross-lane reads with every lane active (a lane of a group without a pair may still
-    // be the source another group reads from)
-    const uint32_t gg = (uint32_t)__shfl((int)g, src);
-    const uint32_t cr = (uint32_t)__shfl((int)crow, src);
-    const int lsrc = __shfl(lc, src);
-    const int n2 = has ? lsrc : 0;
-    // stage the group's candidate value in LDS as u16 units
-    const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + gg, rstride,
-                                         D.rlmax / Str<CT>::UPW - 1}
-                               : Str<CT>{reinterpret_cast<const uint32_t*>(base + D.off[cr]), 1, 1 << 30};
-    wave_lds_sync();  // previous round's reads of s2buf are done
-    const int nw = (n2 + UPW - 1) / UPW;
-    for (int w = k; w < nw; w += G) {
-      const uint32_t x = s2.word(w);
-#pragma unroll
-      for (int u = 0; u < UPW; ++u) {
-        const uint32_t ch = Str<CT>::unit(x, u);
-        row_s2[w * UPW + u] = ch | (wl_class(ch) << 16);
+
+  // staging cursor: this lane loads stream units k + G*i of each 64-unit block
+  int lm = 0, loff = 0, ln2 = 0;
+  const uint32_t* lptr = nullptr;
+  if (cnt > 0) {
+    ln2 = (int)(meta[spos(0)] & 0xFFFFu);
+    lptr = reinterpret_cast<const uint32_t*>(cptr[spos(0)]);
+  }
+  auto advance = [&](int step) {
+    loff += step;
+    while (lm < cnt && loff >= ln2) {
+      loff -= ln2;
+      if (++lm < cnt) {
+        ln2 = (int)(meta[spos(lm)] & 0xFFFFu);
+        lptr = reinterpret_cast<const uint32_t*>(cptr[spos(lm)]);
       }
     }
-    wave_lds_sync();
-    int tmax = n2 > 0 ? n2 + kstar : 0;
-    for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o));
-    T col[R];
+  };
+  uint32_t stg[UL];
+  uint32_t subs = 0;
+  auto load_block = [&]() {
+    subs = 0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) col[r] = (T)(k * R + r + 1);  // D(i, 0) = i
-    T prev = (T)(k * R);                                      // D(k*R, j-1)
-    T bot = col[R - 1];
-    uint32_t ch_next = row_s2[0];
-    for (int t = 0; t < tmax; ++t) {
-      const int j = t - k + 1;
-      const uint32_t ch2 = ch_next;
-      ch_next = row_s2[min(max(j, 0), kMaxLongUnits - 1)];  // column j+1's unit, one step ahead
-      // lane 0's row above: the matrix's top boundary D(0, j)
-      T top;
-      if (WL) top = n1 == 1 ? col[0] : (T)(j == 1 ? n1 : j);
-      else top = (T)j;
-      const T recv = from_left<G>(top, bot, k);  // D(k*R, j)
-      if (j >= 1 && j <= n2) {
-        T up = recv, dg = prev;
-        if (WL) {
-          const double w2 = wl_class_weight(ch2 >> 16);
+    for (int i = 0; i < UL; ++i) {
+      stg[i] = lm < cnt ? lptr[(uint64_t)(loff / UPW) * wstride] : 0u;
+      subs |= (uint32_t)(loff % UPW) << (2 * i);
+      advance(G);
+    }
+  };
+  auto write_block = [&](int half) {
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const double old = col[r];
-            const double cost = c1[r] == ch2 ? 0.0 : fmax(w1[r], w2);
-            // Math.min(left, Math.min(above, aboveleft)) on non-negative values
-            const double v = fmin((double)up + w1[r], fmin(old + w2, (double)dg + cost));
-            col[r] = (T)v;
-            dg = (T)old;
-            up = (T)v;
-          }
-        } else {
+    for (int i = 0; i < UL; ++i) {
+      const uint32_t ch = Str<CT>::unit(stg[i], (int)((subs >> (2 * i)) & 3u));
+      ring[half * 64 + k + G * i] = ch | (wl_class(ch) << 16);
+    }
+  };
+  advance(k);
+  load_block();
+  write_block(0);
+  load_block();
+  wave_lds_sync();
+
+  T col[R];
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int old = (int)col[r];
-            const int v = imin3((int)up, (int)dg, old) + (c1[r] == ch2 ? 0 : 1);
-            col[r] = (T)v;
-            dg = (T)old;
-            up = (T)v;
-          }
+  for (int r = 0; r < R; ++r) col[r] = (T)(k * R + r + 1);  // D(i, 0) = i
+  T prev = (T)(k * R);                                      // D(k*R, j-1)
+  T bot = col[R - 1];
+  int m = 0, j = 1 - k;  // this lane's candidate and its column at this step
+  int n2c = 0, srcc = 0;
+  if (cnt > 0) {
+    const uint32_t x = meta[spos(0)];
+    n2c = (int)(x & 0xFFFFu);
+    srcc = (int)(x >> 16);
+  }
+  uint32_t lu = ring[(0 - k) & 127];  // the unit of stream column t - k, read a step ahead
+  for (int t = 0; t < tend; ++t) {
+    if ((t & 63) == 32) {  // block b+1 into the half block b-1 held, then load block b+2
+      write_block(((t >> 6) + 1) & 1);
+      load_block();
+    }
+    const uint32_t u = lu;
+    lu = ring[(t + 1 - k) & 127];
+    while (m < cnt && j > n2c) {
+      // column n2c done: D(n1, n2) sits in lane kstar's row rstar
+      if (k == kstar) {
+        // col[rstar - 1] as a mask-or (a select chain becomes a dynamically indexed load)
+        uint64_t bits = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint64_t b = WL ? (uint64_t)__double_as_longlong((double)col[r]) : (uint64_t)(uint32_t)(int)col[r];
+          bits |= b & (0ull - (uint64_t)(r + 1 == rstar));
         }
-        prev = recv;
-        bot = col[R - 1];
+        rbits[srcc] = bits;
       }
-    }
-    if (has && k == kstar) {
-      // col[rstar - 1] as a mask-or (a select chain becomes a dynamically indexed load)
-      uint64_t bits = 0;
+      j -= n2c;
+      if (++m < cnt) {
+        const uint32_t x = meta[spos(m)];
+        n2c = (int)(x & 0xFFFFu);
+        srcc = (int)(x >> 16);
+      }
+      // D(i, 0) = i again, computed here (an opaque base: hoisted constants get spilled)
+      int kb = k * R;
+      asm volatile("" : "+v"(kb));
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint64_t b = WL ? (uint64_t)__double_as_longlong((double)col[r]) : (uint64_t)(uint32_t)(int)col[r];
-        bits |= b & (0ull - (uint64_t)(r + 1 == rstar));
-      }
-      double sim;
-      if (WL) {
-        // [Duke 1.2] WeightedLevenshtein.compare
-        const double maxlen = (double)max(n1, n2);
-        const double dist = __longlong_as_double((long long)bits);
-        sim = dist > maxlen ? 0.0 : 1.0 - (dist / maxlen);
-      } else {
-        // [Duke 1.2] Levenshtein.compare: 1 - min(dist, len) / len
-        const int len = min(n1, n2);
-        sim = 1.0 - ((double)min((int)(uint32_t)bits, len) / (double)len);
-      }
-      res[src] = sim;
+      for (int r = 0; r < R; ++r) col[r] = (T)(kb + r + 1);
+      prev = (T)kb;
     }
+    // lane 0's row above: the matrix's top boundary D(0, j)
+    T top;
+    if (WL) top = n1 == 1 ? col[0] : (T)(j == 1 ? n1 : j);
+    else top = (T)j;
+    const T recv = from_left<G>(top, bot, k);  // D(k*R, j)
+    if (j >= 1 && m < cnt) {
+      T up = recv, dg = prev;
+      if (WL) {
+        const double w2 = wl_class_weight(u >> 16);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double old = col[r];
+          const double cost = c1[r] == u ? 0.0 : fmax(w1[r], w2);
+          // Math.min(left, Math.min(above, aboveleft)) on non-negative values
+          const double v = fmin((double)up + w1[r], fmin(old + w2, (double)dg + cost));
+          col[r] = (T)v;
+          dg = (T)old;
+          up = (T)v;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int old = (int)col[r];
+          const int v = imin3((int)up, (int)dg, old) + (c1[r] == u ? 0 : 1);
+          col[r] = (T)v;
+          dg = (T)old;
+          up = (T)v;
+        }
+      }
+      prev = recv;
+      bot = col[R - 1];
+    }
+    ++j;
   }
 }
 
@@ -638,29 +693,62 @@ __device__ __forceinline__ double long_sims(const DevProp& D, uint64_t rstride, 
   const uint64_t nm = __ballot(need);
   if (nm == 0) return sim;
   const int nneed = __popcll(nm);
-  uint32_t* list = reinterpret_cast<uint32_t*>(lds + kLongS2Words + 64);
-  double* res = reinterpret_cast<double*>(lds + kLongS2Words);
-  if (need) list[mask_rank(nm)] = lane_id();
+  const uint32_t lane = lane_id();
+  uint32_t* meta = reinterpret_cast<uint32_t*>(lds + kLongMeta);
+  // sorted position: longest candidate first, ties in lane order (keys are distinct)
+  const uint32_t key = need ? (((uint32_t)lc << 6) | (63u - lane)) + 1u : 0u;
+  meta[lane] = key;
   wave_lds_sync();
-  const CT* s1p = reinterpret_cast<const CT*>(D.units) + D.off[q];
-  // rows per lane: n1 is wave-uniform, so this is a scalar switch
-  // query rows per lane: 16-lane groups (4 candidates a round) up to 64 rows, 32-lane
-  // groups (2 a round, wave_shr) beyond; R = rows / lanes rounded up, so most of a group's
-  // lanes hold rows and R <= 8 keeps the column, weights and units in VGPRs
-  if (n1 <= 16) long_dp<16, 1, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 32) long_dp<16, 2, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 48) long_dp<16, 3, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 64 || LR <= 4) long_dp<16, 4, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 96) long_dp<16, 6, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 128 || LR <= 8) long_dp<16, 8, WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 160) long_dp<32, (LR < 16 ? 4 : 5), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 192) long_dp<32, (LR < 16 ? 4 : 6), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else if (n1 <= 224) long_dp<32, (LR < 16 ? 4 : 7), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
-  else long_dp<32, (LR < 16 ? 4 : 8), WL, CT>(D, rstride, lds, s1p, n1, g, crow, lc, nneed);
+  int rank = 0;
+  if (need) {
+    for (int i = 0; i < 64; i += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(meta + i);
+      rank += (int)(v.x > key) + (int)(v.y > key) + (int)(v.z > key) + (int)(v.w > key);
+    }
+  }
   wave_lds_sync();
-  if (need) sim = res[lane_id()];
+  const CT* base = reinterpret_cast<const CT*>(D.units);
+  if (need) {
+    meta[rank] = (uint32_t)lc | (lane << 16);
+    const uint32_t* p = D.rlmax ? reinterpret_cast<const uint32_t*>(D.runits) + g
+                                : reinterpret_cast<const uint32_t*>(base + D.off[crow]);
+    lds[kLongPtr + rank] = (uint64_t)p;
+  }
   wave_lds_sync();
-  for (int e = (int)lane_id(); e < kLongLdsWords; e += 64) lds[e] = 0;  // Peq slice stays zero
+  const uint64_t wstride = D.rlmax ? rstride : 1u;
+  const CT* s1p = base + D.off[q];
+  // query rows per lane (n1 is wave-uniform: a scalar switch): 16-lane groups (4 streams,
+  // DPP row_shr) up to 128 rows, 32-lane groups (2 streams, wave_shr) beyond; R = rows /
+  // lanes rounded up, so most of a group's lanes hold rows, and R <= 8 keeps the column,
+  // weights and units in VGPRs.  LR caps the variants a kernel carries.
+  if (n1 <= 16) long_dp<16, 1, WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 32) long_dp<16, 2, WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 48) long_dp<16, 3, WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 64 || LR <= 4) long_dp<16, 4, WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 80) long_dp<16, 5, WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 96) long_dp<16, 6, WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 112) long_dp<16, 7, WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 128 || LR <= 8) long_dp<16, 8, WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 160) long_dp<32, (LR < 16 ? 4 : 5), WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 192) long_dp<32, (LR < 16 ? 4 : 6), WL, CT>(wstride, s1p, n1, nneed);
+  else if (n1 <= 224) long_dp<32, (LR < 16 ? 4 : 7), WL, CT>(wstride, s1p, n1, nneed);
+  else long_dp<32, (LR < 16 ? 4 : 8), WL, CT>(wstride, s1p, n1, nneed);
+  wave_lds_sync();
+  if (need) {
+    const uint64_t bits = lds[kLongRes + lane];
+    if (WL) {
+      // [Duke 1.2] WeightedLevenshtein.compare
+      const double maxlen = (double)max(n1, lc);
+      const double dist = __longlong_as_double((long long)bits);
+      sim = dist > maxlen ? 0.0 : 1.0 - (dist / maxlen);
+    } else {
+      // [Duke 1.2] Levenshtein.compare: 1 - min(dist, len) / len
+      const int len = min(n1, lc);
+      sim = 1.0 - ((double)min((int)(uint32_t)bits, len) / (double)len);
+    }
+  }
+  wave_lds_sync();
+  for (int e = (int)lane; e < kLongLdsWords; e += 64) lds[e] = 0;  // Peq slice stays zero
   wave_lds_sync();
   return sim;
 }
@@ -1174,11 +1262,8 @@ __device__ __forceinline__ double property_prob(const DevProp& D, double sim) {
 template <int RMAX, int LR, bool SYM>
 __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
                                            uint64_t nslots, const StageOut& out) {
-  constexpr int PE = LR > 0 ? kPeqEntriesLong : kPeqEntries;  // the long DP stages more
-  __shared__ uint64_t peq_all[kScoreBlock / 64][PE];
-  const uint32_t wave = threadIdx.x >> 6;
-  uint64_t* peq = peq_all[wave];
-  for (int e = (int)lane_id(); e < PE; e += 64) peq[e] = 0;
+  uint64_t* peq = g_wave_tables[threadIdx.x >> 6];
+  for (int e = (int)lane_id(); e < kPeqEntries; e += 64) peq[e] = 0;
 
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in_launch = idx < nslots;
