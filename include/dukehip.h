@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DK_ABI_VERSION 3
+#define DK_ABI_VERSION 4
 
 /* status codes */
 #define DK_OK 0
@@ -155,6 +155,9 @@ typedef struct dk_profile {
   double ms_copy;         /* device->host copies of the match list (copy stream, overlapped) */
   double ms_emit;         /* symmetric dedup schedule: the emission pass (k_emit) */
   uint64_t sym_matches;   /* dk_match calls that ran the symmetric dedup schedule */
+  uint64_t full_builds;   /* blocking-table builds that sorted every usable row */
+  uint64_t delta_builds;  /* builds that re-sorted only the rows added since the last full
+                             one (sorted base + sorted delta) */
 } dk_profile;
 
 typedef struct dk_ctx dk_ctx;
@@ -289,6 +292,56 @@ int dk_interner_intern(dk_interner* ids, const dk_column* column, uint64_t n, ui
 int dk_pack_json(const dk_source* source, const char* json, uint64_t len, dk_interner* ids,
                  dk_packed** out);
 void dk_free_packed(dk_packed* packed);
+/* the record ID string of an interned id (UTF-16 code units; valid while the interner lives) */
+int dk_interner_string(const dk_interner* ids, uint64_t id, const uint16_t** units, uint64_t* n);
+
+/* ---- link sink: the pipeline's LinkDatabase written in bulk from a match
+ * list.  Replaces the per-callback LinkDatabaseMatchListener that
+ * BaseLinkDatabaseMatchListener.java:53-109 forwards to, writing into a
+ * SinceAwareInMemoryLinkDatabase (SinceAwareInMemoryLinkDatabase.java:12-41; the
+ * "in-memory" link-database-type, App.java:571-573).  Links are between interned record IDs
+ * (dk_interner): ID1 is the smaller ID string (String.compareTo). */
+#define DK_LINK_INFERRED 1   /* LinkStatus.INFERRED */
+#define DK_LINK_RETRACTED 2  /* LinkStatus.RETRACTED */
+#define DK_LINK_SAME 1       /* LinkKind.SAME (matches) */
+#define DK_LINK_MAYBE 2      /* LinkKind.MAYBE (matchesPerhaps) */
+
+typedef struct dk_link_batch {
+  uint64_t nqueries;
+  const uint64_t* query_ident;     /* interned ID of each query record, batch order */
+  const uint64_t* first;           /* nqueries + 1 entry offsets (dk_result.first) */
+  const uint64_t* candidate_ident; /* per entry: interned ID of the candidate */
+  const double* prob;              /* per entry: confidence */
+  const uint8_t* kind;             /* per entry: DK_KIND_MATCH / DK_KIND_MAYBE */
+} dk_link_batch;
+
+typedef struct dk_link_stats {
+  uint64_t asserted;   /* links written (new, or changed status / kind / confidence) */
+  uint64_t unchanged;  /* identical links kept with their old timestamp (1e-6 rule) */
+  uint64_t retracted;  /* INFERRED links of a processed record it no longer produced */
+} dk_link_stats;
+
+typedef struct dk_link_list {
+  uint64_t n;
+  const uint64_t* id1;
+  const uint64_t* id2;
+  const uint8_t* status;     /* DK_LINK_INFERRED / DK_LINK_RETRACTED */
+  const uint8_t* kind;       /* DK_LINK_SAME / DK_LINK_MAYBE */
+  const double* confidence;
+  const int64_t* timestamp;  /* ms since the epoch */
+} dk_link_list;
+
+typedef struct dk_linkdb dk_linkdb;
+int dk_linkdb_create(const dk_interner* ids, dk_linkdb** out);
+void dk_linkdb_destroy(dk_linkdb* db);
+uint64_t dk_linkdb_size(const dk_linkdb* db);
+/* Processor.deduplicate's listener stream of one batch (the query records in batch order,
+ * each with its entries in candidate order), stamped `timestamp` */
+int dk_linkdb_apply(dk_linkdb* db, const dk_link_batch* batch, int64_t timestamp, dk_link_stats* stats);
+/* SinceAwareInMemoryLinkDatabase.getChangesSince: links with timestamp > since, ordered by
+ * (timestamp, assertion order) -- the reference iterates a HashMap (order unpinned) */
+int dk_linkdb_changes_since(const dk_linkdb* db, int64_t since, dk_link_list** out);
+void dk_free_link_list(dk_link_list* list);
 
 const char* dk_last_error(void);
 int dk_abi_version(void);

@@ -1,0 +1,113 @@
+"""Per-callback restatement of the link sink (TEST INFRASTRUCTURE: the checker of
+dk_linkdb_apply / dukehip.links.LinkDatabase; never imported by the product).
+
+* ``SinceAwareLinkDB``   <- SinceAwareInMemoryLinkDatabase.java:12-41 (assertLink's identical-
+  link skip within 1e-6, getChangesSince) over [Duke 1.2, recalled] InMemoryLinkDatabase (one
+  link per ID pair, assertLink replaces it).
+* ``LinkDBListener``     <- [Duke 1.2, recalled] LinkDatabaseMatchListener as
+  BaseLinkDatabaseMatchListener.java:53-109 drives it: per record, its matches /
+  matchesPerhaps collected; when the next record starts (or noMatchFor / batchDone) the
+  record's stored INFERRED links it did not produce again are retracted and its new links
+  asserted.  Link(id1, id2) keeps the smaller ID (String.compareTo, UTF-16 code units) first.
+PARITY UNPINNED: Duke 1.2's LinkDatabaseMatchListener / Link / InMemoryLinkDatabase sources are
+absent from /root/reference; the reference's own SinceAware rules are followed exactly.
+"""
+from __future__ import annotations
+
+INFERRED, RETRACTED = 1, 2
+SAME, MAYBE = 1, 2
+
+
+def _u16(s):
+    return s.encode("utf-16-be", "surrogatepass")   # big-endian bytes order = code-unit order
+
+
+class Link:
+    __slots__ = ("id1", "id2", "status", "kind", "confidence", "timestamp")
+
+    def __init__(self, a, b, status, kind, confidence, timestamp):
+        if _u16(a) > _u16(b):
+            a, b = b, a
+        self.id1, self.id2 = a, b
+        self.status, self.kind = status, kind
+        self.confidence, self.timestamp = confidence, timestamp
+
+    def key(self):
+        return (self.id1, self.id2)
+
+    def copy(self):
+        return Link(self.id1, self.id2, self.status, self.kind, self.confidence, self.timestamp)
+
+
+class SinceAwareLinkDB:
+    def __init__(self):
+        self.links = {}    # (id1, id2) -> Link
+        self.order = {}    # (id1, id2) -> assertion sequence number
+        self.seq = 0
+
+    def all_links_for(self, rid):
+        return [l for k, l in self.links.items() if rid in k]
+
+    def assert_link(self, link):                    # SinceAwareInMemoryLinkDatabase.java:12-30
+        old = self.links.get(link.key())
+        if old is not None and link.status == old.status and link.kind == old.kind:
+            if abs(link.confidence - old.confidence) < 0.000001:
+                return False
+        self.links[link.key()] = link               # InMemoryLinkDatabase.assertLink
+        self.order[link.key()] = self.seq
+        self.seq += 1
+        return True
+
+    def changes_since(self, since):                 # :32-40
+        out = [l for l in self.links.values() if l.timestamp > since]
+        return sorted(out, key=lambda l: (l.timestamp, self.order[l.key()]))
+
+
+class LinkDBListener:
+    """The MatchListener callbacks, one by one.  A query record is passed as (position in
+    the batch, ID) -- Duke compares Record objects, so two records of one ID stay apart."""
+
+    def __init__(self, db: SinceAwareLinkDB, clock):
+        self.db, self.clock = db, clock
+        self.current, self.cur = None, None
+
+    def batch_ready(self, size):
+        self.current = None
+
+    def _start(self, rec):
+        self.current, self.cur = rec, {}
+
+    def _end(self):
+        if self.current is None:
+            return
+        rid, cur = self.current[1], self.cur
+        for l in self.db.all_links_for(rid):
+            if l.key() in cur or l.status != INFERRED:
+                continue
+            r = l.copy()
+            r.status, r.timestamp = RETRACTED, self.clock()
+            self.db.assert_link(r)
+        for l in cur.values():
+            self.db.assert_link(l)
+        self.current = None
+
+    def _add(self, r1, r2, conf, kind):
+        if self.current != r1:
+            self._end()
+            self._start(r1)
+        l = Link(r1[1], r2, INFERRED, kind, conf, self.clock())
+        self.cur[l.key()] = l
+
+    def matches(self, r1, r2, conf):
+        self._add(r1, r2, conf, SAME)
+
+    def matches_perhaps(self, r1, r2, conf):
+        self._add(r1, r2, conf, MAYBE)
+
+    def no_match_for(self, r):
+        self._end()
+        self._start(r)
+        self._end()
+
+    def batch_done(self):
+        self._end()

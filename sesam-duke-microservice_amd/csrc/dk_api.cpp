@@ -237,6 +237,8 @@ struct PropState {
 struct Replica {
   int rlmax = 0;
   int rgmax = 0;
+  int width = 0;
+  uint64_t npos = 0;  // positions the buffers are laid out for (the transposed stride)
   DevBuf rlen, runits, rnum, rnumok, rgoff, rgcnt, rgrams;
 };
 
@@ -296,13 +298,23 @@ struct dk_ctx {
   DevBuf pair_buf;                // dk_compare_rows' query row / rowof / staging
   dk_ctx* pair_ctx = nullptr;     // dk_compare_values: a 2-row ALLPAIRS index of the schema
   // match scratch
-  DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxKeys], rowof, sgroup[kMaxKeys];
+  DevBuf d_queries, sel, pos, usable, gkeys, skeys[kMaxSegs], rowof, sgroup[kMaxSegs];
   // The blocking tables + candidate replica are index state: built by the first dk_match
   // after the index changed (Duke's blocking database keeps its sorted key maps at index
   // time; the reference's Lucene index is likewise maintained by index/commit, not by the
   // query, IncrementalLuceneDatabase.java:146-165,498-575) and reused until the next change.
   uint64_t index_gen = 1, tables_gen = 0, tables_m = 0;
   BlockTables tables{};
+  // base + delta: the base segments hold the usable rows below base_rows as
+  // of the last full sort (base_m of them, each key function's segment followed by dcap
+  // reserved delta positions); later index changes re-sort only the rows from base_rows on
+  // and retire superseded base rows in place (base_dead: rows killed since the tables were
+  // last built).  A full sort again when the delta outgrows dcap, too many base entries
+  // are retired, or the replica's layout no longer fits a new value.
+  bool base_ok = false;
+  uint64_t base_rows = 0, base_m = 0, dcap = 0, base_retired = 0;
+  std::vector<uint32_t> base_dead;
+  DevBuf d_dead;
   const uint32_t* rowof_p = nullptr;  // replica position -> row (rowof, or usable in ALLPAIRS)
   uint64_t rstride = 0;               // replica positions
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
@@ -740,6 +752,10 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517;
   // skipped with overwrite, :515); transient rows are neither alive (never candidates) nor
   // entered in the ID map.  Staged: the ID map changes are applied at commit.
+  for (uint64_t i = 0; i < n; ++i)
+    if (b->ident[i] == kDeadIdent)
+      return fail(DK_E_INVALID, "record %llu: identity 0x%llx is reserved", (unsigned long long)i,
+                  (unsigned long long)kDeadIdent);
   std::vector<uint8_t> flags(n, 0);
   std::vector<uint32_t> dead;
   std::unordered_map<uint64_t, uint32_t> batch_row;  // ID -> newest row of this batch
@@ -794,6 +810,8 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
                           hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));  // host staging goes out of scope
   for (const auto& br : batch_row) c->ident_row[br.first] = br.second;
+  for (uint32_t r : dead)
+    if (c->base_ok && r < c->base_rows) c->base_dead.push_back(r);
   if (nk > 0) c->key_style = style;
   c->nrows += n;
   c->index_gen++;
@@ -945,41 +963,75 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
 }
 
 // Candidate replica: every property's candidate-side values in replica order, units
-// transposed ([unit][position]) for values of at most kMaxReplicaUnits units.
-static int build_replica(dk_ctx* c, std::vector<Replica>& rep, const uint32_t* rowof, uint64_t npos) {
+// transposed ([unit][position]) for values of at most kMaxReplicaUnits units.  The layout
+// (units / codes per value, width) follows the index's current longest values.
+struct ReplicaShape { int rlmax, rgmax, width, rgw; };
+
+static ReplicaShape replica_shape(const PropState& S) {
+  const int op = S.cfg.comparator;
+  const bool strcmp_ = op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER ||
+                       op == DK_CMP_EXACT || uses_codes(op) || op == DK_CMP_WEIGHTED_LEVENSHTEIN;
+  ReplicaShape sh{};
+  sh.width = S.width ? S.width : 1;
+  sh.rlmax = strcmp_ && S.maxlen <= kMaxReplicaUnits ? ((std::max(S.maxlen, 1) + 3) & ~3) : 0;
+  sh.rgmax = op == DK_CMP_QGRAM && S.maxgrams <= kMaxReplicaGrams ? std::max(S.maxgrams, 1) : 0;
+  // codes pack 16 bits per unit (+16 for the POSITIONAL index): q <= 2 fits in a u32
+  const int gram_bits = 16 * S.cfg.qgram_q + (S.cfg.qgram_tokenizer == DK_QGRAM_POSITIONAL ? 16 : 0);
+  sh.rgw = gram_bits <= 32 ? 4 : 8;
+  return sh;
+}
+
+// the replica can take values of the current index (a delta build keeps its layout)
+static bool replica_fits(const dk_ctx* c, const std::vector<Replica>& rep) {
+  if (rep.size() != c->P.size()) return false;
+  for (size_t i = 0; i < c->P.size(); ++i) {
+    const ReplicaShape sh = replica_shape(c->P[i]);
+    if (sh.rlmax != rep[i].rlmax || sh.rgmax != rep[i].rgmax || sh.width != rep[i].width) return false;
+  }
+  return true;
+}
+
+static int layout_replica(dk_ctx* c, std::vector<Replica>& rep, uint64_t npos) {
   hipStream_t s = c->stream;
   rep.resize(c->P.size());
   for (size_t i = 0; i < c->P.size(); ++i) {
     const PropState& S = c->P[i];
     Replica& R = rep[i];
     const int op = S.cfg.comparator;
-    const bool strcmp_ = op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER ||
-                         op == DK_CMP_EXACT || uses_codes(op) ||
-                         op == DK_CMP_WEIGHTED_LEVENSHTEIN;
-    const int W = S.width ? S.width : 1;
-    R.rlmax = strcmp_ && S.maxlen <= kMaxReplicaUnits ? ((std::max(S.maxlen, 1) + 3) & ~3) : 0;
+    const ReplicaShape sh = replica_shape(S);
+    R.rlmax = sh.rlmax;
+    R.rgmax = sh.rgmax;
+    R.width = sh.width;
+    R.npos = npos;
     HIPCHK(R.rlen.reserve(npos * 2 + 8, 0, s));
-    if (R.rlmax) HIPCHK(R.runits.reserve(npos * (uint64_t)R.rlmax * W + 64, 0, s));
-    const bool num = op == DK_CMP_NUMERIC, qg = uses_codes(op);
-    if (num) {
+    if (R.rlmax) HIPCHK(R.runits.reserve(npos * (uint64_t)R.rlmax * sh.width + 64, 0, s));
+    if (op == DK_CMP_NUMERIC) {
       HIPCHK(R.rnum.reserve(npos * 8 + 8, 0, s));
       HIPCHK(R.rnumok.reserve(npos + 8, 0, s));
     }
-    if (qg) {
+    if (uses_codes(op)) {
       HIPCHK(R.rgoff.reserve(npos * 4 + 8, 0, s));
       HIPCHK(R.rgcnt.reserve(npos * 2 + 8, 0, s));
     }
-    R.rgmax = op == DK_CMP_QGRAM && S.maxgrams <= kMaxReplicaGrams ? std::max(S.maxgrams, 1) : 0;
-    // codes pack 16 bits per unit (+16 for the POSITIONAL index): q <= 2 fits in a u32
-    const int gram_bits = 16 * S.cfg.qgram_q + (S.cfg.qgram_tokenizer == DK_QGRAM_POSITIONAL ? 16 : 0);
-    const int rgw = gram_bits <= 32 ? 4 : 8;
-    if (R.rgmax) HIPCHK(R.rgrams.reserve(npos * (uint64_t)R.rgmax * rgw + 64, 0, s));
+    if (R.rgmax) HIPCHK(R.rgrams.reserve(npos * (uint64_t)R.rgmax * sh.rgw + 64, 0, s));
+  }
+  return DK_OK;
+}
+
+// positions [pos0, pos0 + n) <- rows rowof[pos0 ...]
+static int fill_replica(dk_ctx* c, std::vector<Replica>& rep, const uint32_t* rowof, uint64_t pos0,
+                        uint64_t n) {
+  hipStream_t s = c->stream;
+  for (size_t i = 0; i < c->P.size(); ++i) {
+    const PropState& S = c->P[i];
+    Replica& R = rep[i];
+    const int op = S.cfg.comparator;
     ReplicaJob J{};
-    J.width = W;
+    J.width = R.width;
     J.rlmax = R.rlmax;
-    J.has_num = num;
-    J.has_qgram = qg;
-    J.stride = npos;
+    J.has_num = op == DK_CMP_NUMERIC;
+    J.has_qgram = uses_codes(op);
+    J.stride = R.npos;
     J.off = S.off.as<uint32_t>();
     J.len = S.len.as<uint16_t>();
     J.units = S.units.p;
@@ -994,12 +1046,17 @@ static int build_replica(dk_ctx* c, std::vector<Replica>& rep, const uint32_t* r
     J.rgoff = R.rgoff.as<uint32_t>();
     J.rgcnt = R.rgcnt.as<uint16_t>();
     J.rgmax = R.rgmax;
-    J.rg32 = rgw == 4;
+    J.rg32 = replica_shape(S).rgw == 4;
     J.grams = S.grams.as<uint64_t>();
     J.rgrams = R.rgrams.p;
-    HIPCHK(launch_replicate(J, rowof, npos, s));
+    HIPCHK(launch_replicate(J, rowof, pos0, n, s));
   }
   return DK_OK;
+}
+
+static int build_replica(dk_ctx* c, std::vector<Replica>& rep, const uint32_t* rowof, uint64_t npos) {
+  int rc = layout_replica(c, rep, npos);
+  return rc ? rc : fill_replica(c, rep, rowof, 0, npos);
 }
 
 template <typename F>
@@ -1012,89 +1069,230 @@ static hipError_t with_tmp(dk_ctx* c, F&& f) {
   return f(c->tmp.p, bytes);
 }
 
-// usable rows: alive && !deleted, ordered by (group, row) in LINKAGE, row otherwise
-static int build_usable(dk_ctx* c, uint64_t* m_out) {
+// usable rows among [row0, row1): alive && !deleted, ordered by (group, row) in LINKAGE,
+// row otherwise, into c->usable
+static int build_usable(dk_ctx* c, uint64_t row0, uint64_t row1, uint64_t* m_out) {
   hipStream_t s = c->stream;
-  const uint64_t N = c->nrows;
+  const uint64_t N = row1 - row0;
   HIPCHK(c->sel.reserve(N * 4 + 4, 0, s));
   HIPCHK(c->pos.reserve(N * 4 + 4, 0, s));
   HIPCHK(c->usable.reserve(N * 4 + 4, 0, s));
   const bool link = c->schema.mode == DK_MODE_LINKAGE;
   uint64_t m = 0;
-  for (int pass = 0; pass < (link ? 2 : 1); ++pass) {
-    HIPCHK(launch_select_rows(c->flags.as<uint8_t>(), c->group.as<uint8_t>(), N, link ? pass + 1 : 0,
-                              c->sel.as<uint32_t>(), s));
+  for (int pass = 0; pass < (link ? 2 : 1) && N; ++pass) {
+    HIPCHK(launch_select_rows(c->flags.as<uint8_t>(), c->group.as<uint8_t>(), row0, N,
+                              link ? pass + 1 : 0, c->sel.as<uint32_t>(), s));
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return exclusive_scan_u32(t, b, c->sel.as<uint32_t>(), c->pos.as<uint32_t>(), N, s);
     }));
-    HIPCHK(launch_scatter_rows(c->sel.as<uint32_t>(), c->pos.as<uint32_t>(), N, (uint32_t)m,
+    HIPCHK(launch_scatter_rows(c->sel.as<uint32_t>(), c->pos.as<uint32_t>(), row0, N, (uint32_t)m,
                                c->usable.as<uint32_t>(), s));
     uint32_t last_pos = 0, last_sel = 0;
-    if (N) {
-      HIPCHK(hipMemcpyAsync(&last_pos, c->pos.as<uint32_t>() + N - 1, 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(&last_sel, c->sel.as<uint32_t>() + N - 1, 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-    }
+    HIPCHK(hipMemcpyAsync(&last_pos, c->pos.as<uint32_t>() + N - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&last_sel, c->sel.as<uint32_t>() + N - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     m += (uint64_t)last_pos + last_sel;
   }
   *m_out = m;
   return DK_OK;
 }
 
-// The blocking tables and the candidate replica (index state): built by the first call
-// after the index changed, reused until the next change.
-static int ensure_tables(dk_ctx* c, BlockTables* Tout, uint64_t* Mout) {
+// Sort the m usable rows (c->usable) of key function k by key -- stable, so a bucket keeps
+// (group, row) order -- into segment seg at replica position pos0; its sorted keys / groups
+// go to buffers skeys[buf] / sgroup[buf] (k: base, kMaxKeys + k: delta).
+static int sort_segment(dk_ctx* c, BlockTables& T, int k, int buf, int seg, uint64_t pos0, uint64_t m) {
+  hipStream_t s = c->stream;
+  uint32_t* rows = c->rowof.as<uint32_t>() + pos0;
+  HIPCHK(c->gkeys.reserve(m * 8 + 8, 0, s));
+  HIPCHK(c->skeys[buf].reserve(m * 8 + 8, 0, s));
+  if (m) {
+    HIPCHK(launch_gather_keys(c->keys[k].as<uint64_t>(), c->usable.as<uint32_t>(), c->gkeys.as<uint64_t>(), m, s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return sort_pairs_u64_u32(t, b, c->gkeys.as<uint64_t>(), c->skeys[buf].as<uint64_t>(),
+                                c->usable.as<uint32_t>(), rows, m, s);
+    }));
+  }
+  if (T.linkage) {
+    HIPCHK(c->sgroup[buf].reserve(m + 8, 0, s));
+    if (m) HIPCHK(launch_gather_u8(c->group.as<uint8_t>(), rows, c->sgroup[buf].as<uint8_t>(), m, s));
+  }
+  T.skeys[seg] = c->skeys[buf].as<uint64_t>();
+  T.sgroup[seg] = c->sgroup[buf].as<uint8_t>();
+  T.seg_len[seg] = m;
+  T.seg_off[seg] = pos0;
+  return DK_OK;
+}
+
+// replica-ordered identity / keys (the candidate filters) of positions [pos0, pos0 + n)
+static int fill_rows(dk_ctx* c, const BlockTables& T, uint64_t pos0, uint64_t n) {
+  uint64_t* rk[kMaxKeys] = {};
+  for (int k = 0; k + 1 < c->schema.nkeys; ++k) rk[k] = c->rkeys[k].as<uint64_t>();
+  HIPCHK(launch_replicate_rows(c->rowof.as<uint32_t>(), pos0, n, c->ident.as<uint64_t>(),
+                               c->rident.as<uint64_t>(), T, rk, c->stream));
+  return DK_OK;
+}
+
+static bool delta_enabled() {
+  const char* e = getenv("DK_DELTA");
+  return !(e && e[0] == '0');
+}
+
+// delta capacity per key function: an eighth of the base, at least DK_DELTA_MIN rows
+static uint64_t delta_capacity(uint64_t m) {
+  const char* e = getenv("DK_DELTA_MIN");
+  const uint64_t lo = e ? strtoull(e, nullptr, 10) : (1ull << 16);
+  return std::max<uint64_t>(lo, m / 8);
+}
+
+// Full sort: every usable row into the base segments (ALLPAIRS: the usable rows are the
+// replica, no tables).
+static int build_full(dk_ctx* c, BlockTables& T, uint64_t* Mout) {
   hipStream_t s = c->stream;
   const int nk = c->schema.nkeys;
   const bool allpairs = c->schema.mode == DK_MODE_ALLPAIRS;
+  uint64_t M = 0;
+  int rc = build_usable(c, 0, c->nrows, &M);
+  if (rc) return rc;
+  c->base_ok = false;
+  c->base_dead.clear();
+  if (allpairs) {
+    c->rowof_p = c->usable.as<uint32_t>();
+    c->rstride = M;
+    rc = build_replica(c, c->rep, c->rowof_p, M);
+    if (rc) return rc;
+    *Mout = M;
+    return DK_OK;
+  }
+  // transient rows are never usable; the base covers the rows below them
+  const uint64_t rb = c->transient ? c->transient_row0 : c->nrows;
+  uint64_t dcap = delta_enabled() ? delta_capacity(M) : 0;
+  // replica positions (K * (M + dcap)) stay below the u32 sentinel
+  const uint64_t lim = (uint64_t)kSentinel / (uint64_t)nk;
+  if (M + dcap >= lim) dcap = M < lim ? lim - 1 - M : 0;
+  const uint64_t kstride = M + dcap;
+  const uint64_t npos = (uint64_t)nk * kstride;
+  HIPCHK(c->rowof.reserve(npos * 4 + 4, 0, s));
+  T.nseg = nk;
+  T.seg_shift = 0;
+  for (int k = 0; k < nk; ++k) {
+    rc = sort_segment(c, T, k, k, k, (uint64_t)k * kstride, M);
+    if (rc) return rc;
+  }
+  T.rowof = c->rowof.as<uint32_t>();
+  c->rowof_p = T.rowof;
+  c->rstride = npos;
+  rc = layout_replica(c, c->rep, npos);
+  if (rc) return rc;
+  HIPCHK(c->rident.reserve(npos * 8 + 8, 0, s));
+  for (int k = 0; k + 1 < nk; ++k) HIPCHK(c->rkeys[k].reserve(npos * 8 + 8, 0, s));
+  T.rident = c->rident.as<uint64_t>();
+  for (int k = 0; k < nk; ++k) {
+    rc = fill_replica(c, c->rep, T.rowof, T.seg_off[k], M);
+    if (rc) return rc;
+    rc = fill_rows(c, T, T.seg_off[k], M);
+    if (rc) return rc;
+  }
+  c->base_ok = dcap > 0;
+  c->base_rows = rb;
+  c->base_m = M;
+  c->dcap = dcap;
+  c->base_retired = 0;
+  *Mout = M;
+  return DK_OK;
+}
+
+// Delta build: retire the base rows superseded since the last build, re-sort the usable
+// rows from base_rows on into the delta segments and replicate only those.  Cost O(delta
+// + retired rows), independent of the base size.  Returns 1 when a full sort is due.
+static int build_delta(dk_ctx* c, BlockTables& T) {
+  hipStream_t s = c->stream;
+  const int nk = c->schema.nkeys;
+  if (!c->base_ok || c->nrows < c->base_rows || !replica_fits(c, c->rep)) return 1;
+  if (c->base_retired + c->base_dead.size() > c->base_m / 4 + 1024) return 1;
+  uint64_t Md = 0;
+  int rc = build_usable(c, c->base_rows, c->nrows, &Md);
+  if (rc) return rc;
+  if (Md > c->dcap) return 1;
+  const uint64_t kstride = c->base_m + c->dcap;
+  T.nseg = 2 * nk;
+  T.seg_shift = 1;
+  T.rowof = c->rowof.as<uint32_t>();
+  T.rident = c->rident.as<uint64_t>();
+  for (int k = 0; k < nk; ++k) {  // the base segments as sorted
+    T.skeys[2 * k] = c->skeys[k].as<uint64_t>();
+    T.sgroup[2 * k] = c->sgroup[k].as<uint8_t>();
+    T.seg_len[2 * k] = c->base_m;
+    T.seg_off[2 * k] = (uint64_t)k * kstride;
+  }
+  if (!c->base_dead.empty()) {
+    const uint64_t nd = c->base_dead.size();
+    HIPCHK(c->d_dead.reserve(nd * 4 + 4, 0, s));
+    HIPCHK(hipMemcpyAsync(c->d_dead.p, c->base_dead.data(), nd * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_mark_dead(T, c->d_dead.as<uint32_t>(), nd, c->rident.as<uint64_t>(), s));
+    HIPCHK(hipStreamSynchronize(s));  // the host list is reused
+    c->base_retired += nd;
+    c->base_dead.clear();
+  }
+  for (int k = 0; k < nk; ++k) {
+    // delta skeys / sgroup live in the upper half of the segment buffers
+    rc = sort_segment(c, T, k, kMaxKeys + k, 2 * k + 1, (uint64_t)k * kstride + c->base_m, Md);
+    if (rc) return rc;
+    rc = fill_replica(c, c->rep, T.rowof, T.seg_off[2 * k + 1], Md);
+    if (rc) return rc;
+    rc = fill_rows(c, T, T.seg_off[2 * k + 1], Md);
+    if (rc) return rc;
+  }
+  if (Md == 0) {  // nothing added since the base: one segment per key function
+    BlockTables B = T;
+    B.nseg = nk;
+    B.seg_shift = 0;
+    for (int k = 0; k < nk; ++k) {
+      B.skeys[k] = T.skeys[2 * k];
+      B.sgroup[k] = T.sgroup[2 * k];
+      B.seg_len[k] = T.seg_len[2 * k];
+      B.seg_off[k] = T.seg_off[2 * k];
+    }
+    for (int k = nk; k < kMaxSegs; ++k) {
+      B.skeys[k] = nullptr;
+      B.sgroup[k] = nullptr;
+      B.seg_len[k] = B.seg_off[k] = 0;
+    }
+    T = B;
+  }
+  return DK_OK;
+}
+
+// The blocking tables and the candidate replica (index state): built by the first call
+// after the index changed, reused until the next change.  An index that only grew (or lost
+// rows to delete-by-ID) since the last full sort gets a delta build.
+static int ensure_tables(dk_ctx* c, BlockTables* Tout, uint64_t* Mout) {
   if (c->tables_gen == c->index_gen) {
     *Tout = c->tables;
     *Mout = c->tables_m;
     return DK_OK;
   }
-  uint64_t M = 0;
-  int rc = 0;
   BlockTables T{};
-  rc = build_usable(c, &M);
-  if (rc) return rc;
-  T.nkeys = nk;
+  T.nkeys = c->schema.nkeys;
   T.linkage = c->schema.mode == DK_MODE_LINKAGE;
   T.group = c->group.as<uint8_t>();
-  T.m = M;
-  HIPCHK(c->rowof.reserve((uint64_t)std::max(nk, 1) * M * 4 + 4, 0, s));
-  for (int k = 0; k < nk; ++k) {
-    uint32_t* rows_k = c->rowof.as<uint32_t>() + (uint64_t)k * M;
-    HIPCHK(c->gkeys.reserve(M * 8 + 8, 0, s));
-    HIPCHK(c->skeys[k].reserve(M * 8 + 8, 0, s));
-    HIPCHK(launch_gather_keys(c->keys[k].as<uint64_t>(), c->usable.as<uint32_t>(), c->gkeys.as<uint64_t>(), M, s));
-    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
-      return sort_pairs_u64_u32(t, b, c->gkeys.as<uint64_t>(), c->skeys[k].as<uint64_t>(),
-                                c->usable.as<uint32_t>(), rows_k, M, s);
-    }));
-    if (T.linkage) {
-      HIPCHK(c->sgroup[k].reserve(M + 8, 0, s));
-      HIPCHK(launch_gather_u8(c->group.as<uint8_t>(), rows_k, c->sgroup[k].as<uint8_t>(), M, s));
-    }
-    T.keys[k] = c->keys[k].as<uint64_t>();
-    T.skeys[k] = c->skeys[k].as<uint64_t>();
-    T.sgroup[k] = c->sgroup[k].as<uint8_t>();
+  for (int k = 0; k < T.nkeys; ++k) T.keys[k] = c->keys[k].as<uint64_t>();
+  uint64_t M = c->base_m;
+  int rc = c->schema.mode == DK_MODE_ALLPAIRS ? 1 : build_delta(c, T);
+  if (rc == 1) {
+    BlockTables F{};
+    F.nkeys = T.nkeys;
+    F.linkage = T.linkage;
+    F.group = T.group;
+    for (int k = 0; k < T.nkeys; ++k) F.keys[k] = T.keys[k];
+    T = F;
+    rc = build_full(c, T, &M);
+    if (rc == DK_OK) c->prof.full_builds += 1;
+  } else if (rc == DK_OK) {
+    c->prof.delta_builds += 1;
   }
-  T.rowof = c->rowof.as<uint32_t>();
-  // candidate replica in slot-position order: the K sorted tables, or the usable rows
-  c->rowof_p = allpairs ? c->usable.as<uint32_t>() : c->rowof.as<uint32_t>();
-  c->rstride = allpairs ? M : (uint64_t)nk * M;
-  rc = build_replica(c, c->rep, c->rowof_p, c->rstride);
-  if (rc) return rc;
-  if (!allpairs) {  // replica-ordered identity / keys for the candidate filters
-    const uint64_t npos = (uint64_t)nk * M;
-    HIPCHK(c->rident.reserve(npos * 8 + 8, 0, s));
-    uint64_t* rk[kMaxKeys] = {};
-    for (int k = 0; k + 1 < nk; ++k) {
-      HIPCHK(c->rkeys[k].reserve(npos * 8 + 8, 0, s));
-      rk[k] = c->rkeys[k].as<uint64_t>();
-    }
-    HIPCHK(launch_replicate_rows(c->rowof.as<uint32_t>(), npos, c->ident.as<uint64_t>(),
-                                 c->rident.as<uint64_t>(), T, rk, s));
+  if (rc) {
+    c->base_ok = false;  // a failed build leaves no trusted base
+    return rc;
   }
   c->tables = T;
   c->tables_m = M;
@@ -1152,7 +1350,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   const uint32_t r0 = nq ? query_rows[0] : 0;
   uint64_t* hs = c->h_small.as<uint64_t>();
   if (sym) {
-    HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 16 + 16, 0, s));
+    HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 16 + 16, 0, s));
     HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->ocounts.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
@@ -1196,17 +1394,17 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   if (sym) {
     HIPCHK(c->ores.reserve(otot * 8 + 64, 0, s));
     HIPCHK(c->mres.reserve(mtot * 8 + 64, 0, s));
-    HIPCHK(c->mbase.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
+    HIPCHK(c->mbase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
     HIPCHK(hipMemsetAsync(c->mres.p, 0xFF, mtot * 8, s));  // all-ones: a NaN (no entry)
     HIPCHK(c->wq.reserve(total / 64 * 4 + 4, 0, s));
     HIPCHK(c->owq.reserve(otot / 64 * 4 + 4, 0, s));
-    HIPCHK(c->obase.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
+    HIPCHK(c->obase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
     HIPCHK(launch_wavemap(c->qoff.as<uint64_t>(), nq, c->wq.as<uint32_t>(), s));
     HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s));
     HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), c->mqoff.as<uint64_t>(),
-                        nq, nk, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
+                        nq, T.nseg, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
   } else if (!allpairs) {
-    HIPCHK(c->ranges.reserve((uint64_t)nk * nq * 8 + 8, 0, s));
+    HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
     HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
     HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
@@ -1309,6 +1507,9 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     src.ranges = c->ranges.as<uint2>();
     src.nq = nq;
     src.nkeys = nk;
+    src.nseg = T.nseg;
+    src.seg_shift = T.seg_shift;
+    for (int k = 0; k < T.nseg; ++k) src.segoff[k] = T.seg_off[k];
     src.rident = c->rident.as<uint64_t>();
     for (int k = 0; k < nk; ++k) {
       src.qkeys[k] = c->keys[k].as<uint64_t>();
@@ -1336,8 +1537,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     esrc.mbase = c->mbase.as<uint64_t>();
     esrc.rowof = c->rowof.as<uint32_t>();
     esrc.nq = nq;
-    esrc.m = M;
-    esrc.nkeys = nk;
+    esrc.nseg = T.nseg;
+    for (int k = 0; k < T.nseg; ++k) esrc.segoff[k] = T.seg_off[k];
     esrc.r0 = r0;
     esrc.threshold = P.threshold;
     esrc.maybe = P.maybe;
@@ -1551,7 +1752,7 @@ int dk_candidate_counts(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, uint
   }
   HIPCHK(c->d_queries.reserve(nq * 4 + 4, 0, s));
   HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(c->ranges.reserve((uint64_t)c->schema.nkeys * nq * 8 + 8, 0, s));
+  HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
   HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
   HIPCHK(launch_count_exact(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(),
                             c->counts.as<uint64_t>(), s));
@@ -1688,6 +1889,8 @@ static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double
 static void clear_index(dk_ctx* c) {
   c->nrows = 0;
   c->index_gen++;
+  c->base_ok = false;
+  c->base_dead.clear();
   c->ident_row.clear();
   for (auto& t : c->intern) t.clear();
   c->key_style = 0;

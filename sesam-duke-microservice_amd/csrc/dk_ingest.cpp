@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "dk_clean_table.h"
+#include "dk_interner.h"
 #include "dukehip.h"
 
 extern "C" int dk_fail_ingest(int code, const char* msg);  // dk_api.cpp: sets dk_last_error
@@ -417,9 +418,6 @@ struct ColBuild {
 
 }  // namespace
 
-struct dk_interner {
-  std::unordered_map<std::u16string, uint64_t> ids;
-};
 
 namespace {
 
@@ -494,7 +492,7 @@ int dk_interner_intern(dk_interner* it, const dk_column* col, uint64_t n, uint64
       for (uint32_t j = a; j < b; ++j)
         k[j - a] = col->width == 1 ? ((const uint8_t*)col->units)[j] : ((const uint16_t*)col->units)[j];
       const auto f = it->ids.find(k);
-      out[i] = f != it->ids.end() ? f->second : it->ids.emplace(k, (uint64_t)it->ids.size()).first->second;
+      out[i] = f != it->ids.end() ? f->second : it->add(std::move(k));
     }
   } catch (const std::bad_alloc&) {
     return dk_fail_ingest(DK_E_NOMEM, "out of host memory");
@@ -636,8 +634,7 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
       P->deleted.push_back(has[i_del] && as_boolean(got[i_del], side) ? 1 : 0);
       if (src->group_no) P->group.push_back((uint8_t)src->group_no);
       const auto f = ids->ids.find(rid);
-      P->ident.push_back(f != ids->ids.end() ? f->second
-                                             : ids->ids.emplace(rid, (uint64_t)ids->ids.size()).first->second);
+      P->ident.push_back(f != ids->ids.end() ? f->second : ids->add(std::move(rid)));
       ++r;
       if (!batch) break;
       if (R.peek() == ',') {

@@ -11,6 +11,7 @@ namespace dk {
 
 constexpr int kMaxProps = 16;
 constexpr int kMaxKeys = 8;
+constexpr int kMaxSegs = 2 * kMaxKeys;  // per key function: sorted base + sorted delta
 constexpr uint16_t kMissing = 0xFFFF;  // length sentinel: record has no value
 constexpr int kMaxUnits = 64;          // Levenshtein query limit of the lane-per-pair DP
 constexpr int kMaxLongUnits = 256;     // WeightedLevenshtein / long Levenshtein value limit
@@ -27,6 +28,10 @@ __host__ __device__ constexpr bool uses_codes(int op) {
 
 constexpr uint8_t kAlive = 1;    // not superseded by a later upsert of the same ID
 constexpr uint8_t kDeleted = 2;  // dukeDeleted == "true" (IncrementalLuceneDatabase.java:478)
+// replica identity of a base-table position whose row was superseded after the base was
+// sorted (delete-by-ID, IncrementalLuceneDatabase.java:516-517): never a candidate.  dk_upsert
+// rejects this identity value.
+constexpr uint64_t kDeadIdent = ~0ull;
 
 // ---------------------------------------------------------------------------------------
 // HBM layout
@@ -98,8 +103,13 @@ struct PairSource {
   const uint64_t* qoff;     // query index -> first slot
   const uint2* ranges;      // [k * nq + qi]: candidate range of query qi in sorted table k
   uint64_t nq;
-  int32_t nkeys;
+  int32_t nkeys;            // key functions
   int32_t allpairs;
+  // candidate segments (BlockTables): segment k of nseg belongs to key function
+  // k >> seg_shift; its replica positions start at segoff[k]; ranges / sranges / mbase /
+  // obase are indexed [segment * nq + qi]
+  int32_t nseg, seg_shift;
+  uint64_t segoff[kMaxSegs];
   const uint64_t* qkeys[kMaxKeys];  // key of every row (the query side's keys)
   const uint64_t* rident;   // per replica position: ident of its row (Processor.isSameAs)
   const uint64_t* rkeys[kMaxKeys];  // per replica position: key j of its row, j < nkeys - 1
@@ -141,9 +151,10 @@ struct EmitSource {
   const double* ores;
   const double* mres;
   const uint32_t* rowof;
-  uint64_t nq, m;
-  int32_t nkeys;
+  uint64_t nq;
+  int32_t nseg;
   uint32_t r0;
+  uint64_t segoff[kMaxSegs];
   double threshold, maybe;
 };
 
@@ -171,17 +182,26 @@ struct MatchList {
   uint32_t* qidx;
 };
 
-// Blocking tables of one dk_match call: per key function, the usable rows (alive, not
-// deleted) sorted by (key, group, row); table k occupies rowof[k * M, (k + 1) * M).
+// Blocking tables (index state): per key function the usable rows (alive, not deleted)
+// sorted by (key, group, row).  Each key function has a BASE segment (the rows below
+// base_rows when the tables were last fully sorted) and, once rows were added after that,
+// a DELTA segment (the usable rows from base_rows on, re-sorted per index change; SURVEY
+// §8f-1).  Segment s belongs to key function s >> seg_shift (seg_shift 0: no delta, one
+// segment per key function); its entries are replica positions [seg_off[s], seg_off[s] +
+// seg_len[s]) with rows rowof[...].  All delta rows are above all base rows, so a bucket's
+// base entries followed by its delta entries are in (group, row) order -- the full sort's.
 struct BlockTables {
   int32_t nkeys;
   int32_t linkage;
-  uint64_t m;                       // usable rows
+  int32_t nseg, seg_shift;
   const uint64_t* keys[kMaxKeys];   // per key function, per row
   const uint8_t* group;             // per row (LINKAGE)
-  const uint64_t* skeys[kMaxKeys];  // sorted keys of table k
-  const uint8_t* sgroup[kMaxKeys];  // group of table k's entries (LINKAGE)
-  const uint32_t* rowof;            // K * M
+  const uint64_t* skeys[kMaxSegs];  // sorted keys of segment s
+  const uint8_t* sgroup[kMaxSegs];  // group of segment s's entries (LINKAGE)
+  uint64_t seg_len[kMaxSegs];
+  uint64_t seg_off[kMaxSegs];
+  const uint32_t* rowof;            // replica position -> row
+  const uint64_t* rident;           // replica position -> identity (kDeadIdent: superseded)
 };
 
 // One property's replica build.
@@ -218,11 +238,16 @@ hipError_t launch_gather_keys(const uint64_t* keys, const uint32_t* rows, uint64
                               uint64_t n, hipStream_t s);
 hipError_t launch_gather_u8(const uint8_t* src, const uint32_t* rows, uint8_t* out, uint64_t n,
                             hipStream_t s);
-hipError_t launch_select_rows(const uint8_t* flags, const uint8_t* group, uint64_t nrows,
-                              int want_group, uint32_t* flag_out, hipStream_t s);
-hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64_t nrows,
-                               uint32_t base, uint32_t* rows_out, hipStream_t s);
-hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t npos,
+// rows [row0, row0 + nrows): flag_out[i] = row row0 + i is usable (of want_group)
+hipError_t launch_select_rows(const uint8_t* flags, const uint8_t* group, uint64_t row0,
+                              uint64_t nrows, int want_group, uint32_t* flag_out, hipStream_t s);
+hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64_t row0,
+                               uint64_t nrows, uint32_t base, uint32_t* rows_out, hipStream_t s);
+// replica positions [pos0, pos0 + npos)
+hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t pos0, uint64_t npos,
+                            hipStream_t s);
+// superseded base rows: their positions in every base segment get rident = kDeadIdent
+hipError_t launch_mark_dead(const BlockTables& T, const uint32_t* rows, uint64_t n, uint64_t* rident,
                             hipStream_t s);
 // counts[i] = candidate slots of query i rounded up to 64 (one query per score wave);
 // real[0] += the unpadded total
@@ -234,9 +259,9 @@ hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockT
 // wq[w] = qi for the waves of query qi's slots (qoff in slots, multiples of 64)
 hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s);
 // replica-ordered identity and keys 0..nkeys-2 of the rows at replica positions
-hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t npos, const uint64_t* ident,
-                                 uint64_t* rident, const BlockTables& T, uint64_t* const* rkeys,
-                                 hipStream_t s);
+hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t pos0, uint64_t npos,
+                                 const uint64_t* ident, uint64_t* rident, const BlockTables& T,
+                                 uint64_t* const* rkeys, hipStream_t s);
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                         uint64_t nslots, const StageOut& out, hipStream_t s);
 // symmetric dedup schedule: per query its bucket positions (sranges), full and owner slot
@@ -245,7 +270,7 @@ hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTab
                             uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* mcounts,
                             uint64_t* real, hipStream_t s);
 hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint64_t* mqoff,
-                        uint64_t nq, int nkeys, uint64_t* obase, uint64_t* mbase, hipStream_t s);
+                        uint64_t nq, int nseg, uint64_t* obase, uint64_t* mbase, hipStream_t s);
 hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, const StageOut& out,
                        hipStream_t s);
 hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,

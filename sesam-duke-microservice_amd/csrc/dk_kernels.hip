@@ -1291,7 +1291,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     // query's keys are wave-uniform.
     uint64_t t = s - S.qoff[qi];
     int k = -1;
-    for (int kk = 0; kk < S.nkeys; ++kk) {
+    for (int kk = 0; kk < S.nseg; ++kk) {
       if (SYM) {  // owned candidates: [lo, qa) then (pq, hi)
         const uint4 r = S.sranges[(uint64_t)kk * S.nq + qi];
         const bool in_t = r.w != kNoPos;
@@ -1301,7 +1301,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
           if (t < len) {
             k = kk;
             const uint64_t x = t < nlow ? r.x + t : r.w + 1 + (t - nlow);
-            g = (uint32_t)((uint64_t)kk * S.m + x);
+            g = (uint32_t)(S.segoff[kk] + x);
             mirror = in_t;
             ksel = kk;
             rsel = r;
@@ -1315,7 +1315,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
         if (k < 0) {
           if (t < len) {
             k = kk;
-            g = (uint32_t)((uint64_t)kk * S.m + r.x + t);
+            g = (uint32_t)(S.segoff[kk] + r.x + t);
           } else {
             t -= len;
           }
@@ -1324,9 +1324,12 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     }
     valid = valid && k >= 0;
     if (!valid) g = 0u;  // lanes without a pair read replica position 0 (always in range)
-    bool ok = S.rident[g] != P.ident[q];
+    // isSameAs, and a base position superseded since the base was sorted (kDeadIdent)
+    const uint64_t rid = S.rident[g];
+    bool ok = rid != P.ident[q] && rid != kDeadIdent;
+    const int kf = k >> S.seg_shift;  // the segment's key function
     for (int j = 0; j < S.nkeys - 1; ++j)
-      if (j < k) ok = ok && S.rkeys[j][g] != S.qkeys[j][q];
+      if (j < kf) ok = ok && S.rkeys[j][g] != S.qkeys[j][q];
     valid = valid && ok;
   }
   const uint32_t crow = P.rowof[g];
@@ -1431,7 +1434,7 @@ __device__ __forceinline__ EmitSlot emit_resolve(const EmitSource& S, uint64_t s
   uint64_t t = s - S.qoff[qi];
   int k = -1;
   uint4 r = make_uint4(0, 0, 0, 0);
-  for (int kk = 0; kk < S.nkeys; ++kk) {
+  for (int kk = 0; kk < S.nseg; ++kk) {
     const uint4 rr = S.sranges[(uint64_t)kk * S.nq + qi];
     const uint64_t len = (uint64_t)(rr.y - rr.x);
     if (k < 0) {
@@ -1446,7 +1449,7 @@ __device__ __forceinline__ EmitSlot emit_resolve(const EmitSource& S, uint64_t s
   valid = valid && k >= 0;
   if (valid) {
     const uint32_t x = r.x + (uint32_t)t;
-    o.crow = S.rowof[(uint64_t)k * S.m + x];
+    o.crow = S.rowof[S.segoff[k] + x];
     const bool in_t = r.w != kNoPos;
     if (in_t && x == r.w) {
       valid = false;  // the query itself (Processor.isSameAs)
@@ -1554,9 +1557,10 @@ __device__ __forceinline__ void replicate_units(const ReplicaJob& J, uint64_t g,
 }
 
 __global__ __launch_bounds__(256) void k_replicate(const ReplicaJob J, const uint32_t* __restrict__ rowof,
-                                                   uint64_t npos) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= npos) return;
+                                                   uint64_t pos0, uint64_t npos) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npos) return;
+  const uint64_t g = pos0 + i;
   const uint32_t row = rowof[g];
   const int l = J.len[row];
   J.rlen[g] = (uint16_t)l;
@@ -1618,10 +1622,10 @@ __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const
   uint64_t total = 0;
   if (i < nq) {
     const uint32_t q = queries[i];
-    for (int k = 0; k < T.nkeys; ++k) {
-      const uint64_t key = T.keys[k][q];
-      const uint64_t lo = lower_bound_u64(T.skeys[k], T.m, key);
-      const uint64_t hi = upper_bound_u64(T.skeys[k], lo, T.m, key);
+    for (int k = 0; k < T.nseg; ++k) {
+      const uint64_t key = T.keys[k >> T.seg_shift][q];
+      const uint64_t lo = lower_bound_u64(T.skeys[k], T.seg_len[k], key);
+      const uint64_t hi = upper_bound_u64(T.skeys[k], lo, T.seg_len[k], key);
       uint64_t a = lo, b = hi;
       if (T.linkage) {
         uint64_t s = lo, e = hi;  // first position with group >= 2
@@ -1662,14 +1666,16 @@ __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, c
   uint64_t total = 0, own = 0, mir = 0;
   if (i < nq) {
     const uint32_t q = queries[i];
-    for (int k = 0; k < T.nkeys; ++k) {
-      const uint64_t key = T.keys[k][q];
-      const uint64_t lo = lower_bound_u64(T.skeys[k], T.m, key);
-      const uint64_t hi = upper_bound_u64(T.skeys[k], lo, T.m, key);
-      const uint32_t* rows = T.rowof + (uint64_t)k * T.m;
+    for (int k = 0; k < T.nseg; ++k) {
+      const uint64_t key = T.keys[k >> T.seg_shift][q];
+      const uint64_t lo = lower_bound_u64(T.skeys[k], T.seg_len[k], key);
+      const uint64_t hi = upper_bound_u64(T.skeys[k], lo, T.seg_len[k], key);
+      const uint32_t* rows = T.rowof + T.seg_off[k];
       const uint64_t qa = lower_bound_u32(rows, lo, hi, r0);
       const uint64_t p = lower_bound_u32(rows, qa, hi, q);
-      const bool in_t = p < hi && rows[p] == q;
+      // a superseded base entry is no candidate, so its query is not "in" the segment
+      // either: it owns its whole bucket and expects no mirrored results
+      const bool in_t = p < hi && rows[p] == q && T.rident[T.seg_off[k] + p] != kDeadIdent;
       const uint32_t qa_eff = in_t ? (uint32_t)qa : (uint32_t)hi;
       sranges[(uint64_t)k * nq + i] =
           make_uint4((uint32_t)lo, (uint32_t)hi, qa_eff, in_t ? (uint32_t)p : kNoPos);
@@ -1691,12 +1697,12 @@ __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, c
 // and mbase[k][qi] = mirror slot of bucket position qa (the query's mirror runs [qa, pq)
 // start at mqoff[qi], key function by key function)
 __global__ void k_obase(const uint4* __restrict__ sranges, const uint64_t* __restrict__ oqoff,
-                        const uint64_t* __restrict__ mqoff, uint64_t nq, int nkeys,
+                        const uint64_t* __restrict__ mqoff, uint64_t nq, int nseg,
                         uint64_t* __restrict__ obase, uint64_t* __restrict__ mbase) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
   uint64_t cum = oqoff[i], mcum = mqoff[i];
-  for (int k = 0; k < nkeys; ++k) {
+  for (int k = 0; k < nseg; ++k) {
     const uint4 r = sranges[(uint64_t)k * nq + i];
     const uint64_t nlow = r.z - r.x;
     const bool in_t = r.w != kNoPos;
@@ -1723,15 +1729,44 @@ __global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32
 
 // replica-ordered identity and keys (the score kernel's candidate filters read them
 // coalesced, 64 consecutive positions per wave)
-__global__ __launch_bounds__(256) void k_replicate_rows(const uint32_t* __restrict__ rowof, uint64_t npos,
-                                                        const uint64_t* __restrict__ ident,
+__global__ __launch_bounds__(256) void k_replicate_rows(const uint32_t* __restrict__ rowof, uint64_t pos0,
+                                                        uint64_t npos, const uint64_t* __restrict__ ident,
                                                         uint64_t* __restrict__ rident, const BlockTables T,
                                                         RowKeys rk) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= npos) return;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npos) return;
+  const uint64_t g = pos0 + i;
   const uint32_t row = rowof[g];
   rident[g] = ident[row];
   for (int j = 0; j < T.nkeys - 1; ++j) rk.p[j][g] = T.keys[j][row];
+}
+
+// A row superseded after the base was sorted (delete-by-ID of a re-posted ID): find its
+// entry in key function k's base segment -- its key's bucket, its group's sub-range
+// (LINKAGE), then the row, the bucket being sorted by row within a group -- and retire it.
+// One thread per (row, key function).
+__global__ void k_mark_dead(const BlockTables T, const uint32_t* __restrict__ rows, uint64_t n,
+                            uint64_t* __restrict__ rident) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * (uint64_t)T.nkeys) return;
+  const uint32_t row = rows[i / T.nkeys];
+  const int k = (int)(i % T.nkeys);
+  const int sg = k << T.seg_shift;  // the key function's base segment
+  const uint64_t key = T.keys[k][row];
+  uint64_t lo = lower_bound_u64(T.skeys[sg], T.seg_len[sg], key);
+  uint64_t hi = upper_bound_u64(T.skeys[sg], lo, T.seg_len[sg], key);
+  if (T.linkage) {
+    const uint8_t g = T.group[row];
+    uint64_t s = lo, e = hi;  // first position with group >= 2
+    while (s < e) {
+      const uint64_t mid = (s + e) >> 1;
+      if (T.sgroup[sg][mid] < 2) s = mid + 1; else e = mid;
+    }
+    if (g < 2) hi = s; else lo = s;
+  }
+  const uint32_t* rs = T.rowof + T.seg_off[sg];
+  const uint64_t p = lower_bound_u32(rs, lo, hi, row);
+  if (p < hi && rs[p] == row) rident[T.seg_off[sg] + p] = kDeadIdent;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1761,18 +1796,19 @@ __global__ void k_gather_u8(const uint8_t* __restrict__ src, const uint32_t* __r
 
 // usable = alive and not deleted; LINKAGE selects one group per pass (want_group > 0)
 __global__ void k_select_rows(const uint8_t* __restrict__ flags, const uint8_t* __restrict__ group,
-                              uint64_t n, int want_group, uint32_t* __restrict__ out) {
+                              uint64_t row0, uint64_t n, int want_group, uint32_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  bool ok = (flags[i] & (kAlive | kDeleted)) == kAlive;
-  if (want_group > 0) ok = ok && ((int)group[i] == want_group || (want_group == 2 && group[i] > 2));
+  const uint64_t r = row0 + i;
+  bool ok = (flags[r] & (kAlive | kDeleted)) == kAlive;
+  if (want_group > 0) ok = ok && ((int)group[r] == want_group || (want_group == 2 && group[r] > 2));
   out[i] = ok ? 1u : 0u;
 }
 
 __global__ void k_scatter_rows(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
-                               uint64_t n, uint32_t base, uint32_t* __restrict__ rows) {
+                               uint64_t row0, uint64_t n, uint32_t base, uint32_t* __restrict__ rows) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && flag[i]) rows[base + pos[i]] = (uint32_t)i;
+  if (i < n && flag[i]) rows[base + pos[i]] = (uint32_t)(row0 + i);
 }
 
 __global__ void k_fill_u32(uint32_t* p, uint32_t v, uint64_t n) {
@@ -1822,24 +1858,31 @@ hipError_t launch_gather_u8(const uint8_t* src, const uint32_t* rows, uint8_t* o
   return hipGetLastError();
 }
 
-hipError_t launch_select_rows(const uint8_t* flags, const uint8_t* group, uint64_t nrows,
-                              int want_group, uint32_t* flag_out, hipStream_t s) {
+hipError_t launch_select_rows(const uint8_t* flags, const uint8_t* group, uint64_t row0,
+                              uint64_t nrows, int want_group, uint32_t* flag_out, hipStream_t s) {
   DK_LAUNCH_GUARD(nrows);
-  k_select_rows<<<grid1d(nrows), 256, 0, s>>>(flags, group, nrows, want_group, flag_out);
+  k_select_rows<<<grid1d(nrows), 256, 0, s>>>(flags, group, row0, nrows, want_group, flag_out);
   return hipGetLastError();
 }
 
-hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64_t nrows,
-                               uint32_t base, uint32_t* rows_out, hipStream_t s) {
+hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64_t row0,
+                               uint64_t nrows, uint32_t base, uint32_t* rows_out, hipStream_t s) {
   DK_LAUNCH_GUARD(nrows);
-  k_scatter_rows<<<grid1d(nrows), 256, 0, s>>>(flag, pos, nrows, base, rows_out);
+  k_scatter_rows<<<grid1d(nrows), 256, 0, s>>>(flag, pos, row0, nrows, base, rows_out);
   return hipGetLastError();
 }
 
-hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t npos,
+hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t pos0, uint64_t npos,
                             hipStream_t s) {
   DK_LAUNCH_GUARD(npos);
-  k_replicate<<<grid1d(npos), 256, 0, s>>>(J, rowof, npos);
+  k_replicate<<<grid1d(npos), 256, 0, s>>>(J, rowof, pos0, npos);
+  return hipGetLastError();
+}
+
+hipError_t launch_mark_dead(const BlockTables& T, const uint32_t* rows, uint64_t n, uint64_t* rident,
+                            hipStream_t s) {
+  DK_LAUNCH_GUARD(n);
+  k_mark_dead<<<grid1d(n * (uint64_t)T.nkeys), 256, 0, s>>>(T, rows, n, rident);
   return hipGetLastError();
 }
 
@@ -1863,13 +1906,13 @@ hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipSt
   return hipGetLastError();
 }
 
-hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t npos, const uint64_t* ident,
-                                 uint64_t* rident, const BlockTables& T, uint64_t* const* rkeys,
-                                 hipStream_t s) {
+hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t pos0, uint64_t npos,
+                                 const uint64_t* ident, uint64_t* rident, const BlockTables& T,
+                                 uint64_t* const* rkeys, hipStream_t s) {
   DK_LAUNCH_GUARD(npos);
   RowKeys rk{};
   for (int j = 0; j < T.nkeys - 1; ++j) rk.p[j] = rkeys[j];
-  k_replicate_rows<<<grid1d(npos), 256, 0, s>>>(rowof, npos, ident, rident, T, rk);
+  k_replicate_rows<<<grid1d(npos), 256, 0, s>>>(rowof, pos0, npos, ident, rident, T, rk);
   return hipGetLastError();
 }
 
@@ -1882,9 +1925,9 @@ hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTab
 }
 
 hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint64_t* mqoff,
-                        uint64_t nq, int nkeys, uint64_t* obase, uint64_t* mbase, hipStream_t s) {
+                        uint64_t nq, int nseg, uint64_t* obase, uint64_t* mbase, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_obase<<<grid1d(nq), 256, 0, s>>>(sranges, oqoff, mqoff, nq, nkeys, obase, mbase);
+  k_obase<<<grid1d(nq), 256, 0, s>>>(sranges, oqoff, mqoff, nq, nseg, obase, mbase);
   return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@ MODE_DEDUP, MODE_LINKAGE, MODE_ALLPAIRS = 0, 1, 2
 KIND_MATCH, KIND_MAYBE = 1, 2
 
 MATCH_HOST, MATCH_DEVICE = 0, 1
+ABI_VERSION = 4   # include/dukehip.h DK_ABI_VERSION
 
 EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
            "dk_match", "dk_candidate_counts", "dk_result_copy_to_device",
@@ -31,7 +32,9 @@ EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_dr
            "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite", "dk_num_rows", "dk_row_of_ident", "dk_set_profiling", "dk_get_profile",
            "dk_reset_profile", "dk_last_error", "dk_abi_version",
            "dk_interner_create", "dk_interner_destroy", "dk_interner_size", "dk_interner_find",
-           "dk_interner_intern", "dk_pack_json", "dk_free_packed")
+           "dk_interner_intern", "dk_pack_json", "dk_free_packed", "dk_interner_string",
+           "dk_linkdb_create", "dk_linkdb_destroy", "dk_linkdb_size", "dk_linkdb_apply",
+           "dk_linkdb_changes_since", "dk_free_link_list")
 
 
 class DukeHipError(RuntimeError):
@@ -81,7 +84,8 @@ class dk_profile(C.Structure):
                 ("ms_gather", C.c_double), ("ms_total", C.c_double),
                 ("score_launches", C.c_uint64), ("pairs_scored", C.c_uint64),
                 ("pairs_generated", C.c_uint64), ("score_bytes", C.c_uint64),
-                ("ms_copy", C.c_double), ("ms_emit", C.c_double), ("sym_matches", C.c_uint64)]
+                ("ms_copy", C.c_double), ("ms_emit", C.c_double), ("sym_matches", C.c_uint64),
+                ("full_builds", C.c_uint64), ("delta_builds", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -135,6 +139,8 @@ def load():
               "dk_result_region_layout", "dk_set_result_region",
               "dk_get_profile", "dk_reset_profile"):
         getattr(L, f).restype = C.c_int
+    if L.dk_abi_version() != ABI_VERSION:   # the struct layouts below are this version's
+        raise ImportError(f"{path}: ABI version {L.dk_abi_version()}, dukehip expects {ABI_VERSION}")
     _lib = L
     return L
 

@@ -330,6 +330,7 @@ class GpuBlockingDatabase:
         self.rows = RowStore([p.name for p in self.props])   # row -> Record
         self.by_id = {}         # ID -> row of the live version (Python-packed batches)
         self.ids = Interner()   # ID string -> dense identity number (both packing paths)
+        self.row_ident = np.zeros(0, np.uint64)   # row -> its record ID's interned id
         self._native = {}       # DataSource id -> NativeSource
         self.overwrite = False
         self.indexing_disabled = False
@@ -377,6 +378,7 @@ class GpuBlockingDatabase:
         if self._transient_row0 is not None:
             self.engine.drop_transient()
             self.rows.truncate(self._transient_row0)
+            self.row_ident = self.row_ident[:self._transient_row0]
             self._transient_row0 = None
 
     # --- bulk path ---
@@ -421,6 +423,7 @@ class GpuBlockingDatabase:
         if transient and self._transient_row0 is None:
             self._transient_row0 = len(self.rows)
         self.rows.append_records(records)
+        self.row_ident = np.concatenate([self.row_ident, np.asarray(ident, np.uint64)])
         if not transient:
             for rid, row in zip(rids, rows):
                 self.by_id[rid] = int(row)
@@ -448,6 +451,7 @@ class GpuBlockingDatabase:
         if transient and self._transient_row0 is None:
             self._transient_row0 = len(self.rows)
         self.rows.append_packed(packed, source.group_no)
+        self.row_ident = np.concatenate([self.row_ident, np.asarray(packed.ident, np.uint64)])
         return rows, packed
 
 
@@ -476,12 +480,25 @@ class GpuProcessor:
         self.listeners = []
         self.threads = 1
         self.profiling = False
+        self.link_database = None
 
     def add_match_listener(self, listener):
         self.listeners.append(listener)
 
     def get_database(self):
         return self.database
+
+    def set_link_database(self, link_database):
+        """The pipeline's LinkDatabase (dukehip.links.LinkDatabase), written in bulk after each
+        batch's match -- what BaseLinkDatabaseMatchListener's wrapped
+        LinkDatabaseMatchListener does per callback (BaseLinkDatabaseMatchListener.java:50,
+        53-109).  Skipped while indexing is disabled (httptransform: App.java:1131-1132)."""
+        self.link_database = link_database
+
+    def _write_links(self, rows, res):
+        db = self.database
+        if self.link_database is not None and not db.indexing_disabled:
+            self.link_database.apply_result(res, db.row_ident[np.asarray(rows, np.int64)], db.row_ident)
 
     def set_threads(self, n):
         self.threads = int(n)  # the GPU path does not use host threads for matching
@@ -507,6 +524,7 @@ class GpuProcessor:
         rows = db.index_batch(pending + records)[len(pending):]
         res = db.engine.match(rows)
         self._replay(records, res)
+        self._write_links(rows, res)
         for l in self.listeners:
             l.batch_done()
         if self.database.indexing_disabled:
@@ -530,6 +548,7 @@ class GpuProcessor:
         if self.listeners:
             row0 = int(rows[0]) if n else 0
             self._replay(_RowView(db.rows, row0, n), res)
+        self._write_links(rows, res)
         for l in self.listeners:
             l.batch_done()
         if db.indexing_disabled:

@@ -570,3 +570,72 @@ def test_deduplicate_json_equals_record_path(linkage):
         assert r1.get_value("dukeOriginalEntityId") == r0.get_value("dukeOriginalEntityId")
     for p in procs:
         p.database.close()
+
+
+class _LinkAdapter(dh.MatchListener):
+    """Feeds the per-callback link-sink checker (oracle/linkdb_ref.py) from the replay."""
+
+    def __init__(self, L):
+        self.L, self.pos = L, {}
+
+    def batch_ready(self, size):
+        self.pos = {}
+        self.L.batch_ready(size)
+
+    def _q(self, r):
+        return (self.pos.setdefault(id(r), len(self.pos)), r.get_value("ID"))
+
+    def matches(self, r1, r2, c):
+        self.L.matches(self._q(r1), r2.get_value("ID"), c)
+
+    def matches_perhaps(self, r1, r2, c):
+        self.L.matches_perhaps(self._q(r1), r2.get_value("ID"), c)
+
+    def no_match_for(self, r):
+        self.L.no_match_for(self._q(r))
+
+    def batch_done(self):
+        self.L.batch_done()
+
+
+def test_link_database_written_in_bulk_equals_callbacks():
+    """GpuProcessor with a LinkDatabase: after each deduplicate batch the bulk-written link
+    database equals the per-callback LinkDatabaseMatchListener over the same replay."""
+    import time
+    import linkdb_ref as R
+    from dukehip.links import LinkDatabase, interned_string
+    p, props, vals, keys = persons_case(500, 250, 44)
+    n = len(vals[0])
+    cfg = dh.DukeConfig([dh.Property("NAME", dh.Comparator(DUKE_CMP + "JaroWinkler"), 0.1, 0.95),
+                         dh.Property("ADDRESS", dh.Comparator(DUKE_CMP + "Levenshtein"), 0.2, 0.8),
+                         dh.Property("DOB", dh.Comparator(DUKE_CMP + "Levenshtein"), 0.1, 0.85)],
+                        threshold=0.9, maybe_threshold=0.7)
+    kfs = [dh.PartsKey(("NAME", -1, 0, 3), ("DOB", None, 0, 4)),
+           dh.PartsKey(("NAME", 0, 0, 2), ("DOB", None, 5, 10))]
+    db = dh.GpuBlockingDatabase(cfg, kfs)
+    proc = dh.GpuProcessor(cfg, db)
+    ldb = LinkDatabase(db.ids)
+    proc.set_link_database(ldb)
+    ref = R.SinceAwareLinkDB()
+    clock = {"t": 0}
+    adapter = _LinkAdapter(R.LinkDBListener(ref, lambda: clock["t"]))
+    proc.add_match_listener(adapter)
+    rng = np.random.default_rng(44)
+    ids = [f"ds__{i}" for i in range(n)]
+    for bi, (a, b) in enumerate([(0, 300), (300, 600), (600, n), (0, 200)]):
+        recs = []
+        for i in range(a, b):
+            j = i if bi < 3 else int(rng.integers(0, n))   # last batch re-posts, changed values
+            recs.append(dh.Record({"ID": ids[i], "NAME": p["name"][j], "ADDRESS": p["address"][j],
+                                   "DOB": p["dob"][j]}))
+        clock["t"] = int(time.time() * 1000) + bi * 10   # timestamps are not compared
+        before = len(ref.links)
+        proc.deduplicate(recs)
+        assert len(ref.links) >= before
+    ch = ldb.changes_since(0)
+    got = {(interned_string(db.ids, x), interned_string(db.ids, y)): (int(s), int(k), float(c))
+           for x, y, s, k, c in zip(ch["id1"], ch["id2"], ch["status"], ch["kind"], ch["confidence"])}
+    want = {l.key(): (l.status, l.kind, l.confidence) for l in ref.links.values()}
+    assert got == want
+    assert any(v[0] == R.RETRACTED for v in want.values())
+    db.close()
