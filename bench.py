@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--comparator", default="lev", choices=["lev", "jw"],
                     help="allpairs: the field's comparator")
     ap.add_argument("--dup-frac", type=float, default=0.1)
+    ap.add_argument("--utf16-frac", type=float, default=0.0,
+                    help="dedup: fraction of given names drawn from a non-Latin-1 vocabulary "
+                         "(SURVEY §8d's 1%% UTF-16 slice: the NAME column becomes width 2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the oracle baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -77,6 +80,20 @@ def parse():
     return ap.parse_args()
 
 
+def heartbeat(rank):
+    """Progress on stderr every 60 s while a long workload builds or runs (a silent GPU
+    command looks hung to the job runner)."""
+    import threading
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(60)
+            print(f"[bench rank {rank}] {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
 def prop(name, op, low, high, **kw):
     return {"name": name, "comparator": op, "low": low, "high": high, **kw}
 
@@ -89,9 +106,10 @@ def build_workload(args):
     w = {"name": args.workload, "keys": [], "group": None, "threshold": 0.9, "maybe": 0.7}
     if args.workload == "dedup":
         n_dup = int(n * args.dup_frac)
-        p = synth.persons(n - n_dup, n_dup)
+        p = synth.persons(n - n_dup, n_dup, utf16_frac=args.utf16_frac)
         w.update(desc="BASELINE configs[1]: 1M synthetic person records dedup, key blocking "
-                      "K1=surname[0:3]+dob[0:4] K2=given[0:2]+dob[5:10]",
+                      "K1=surname[0:3]+dob[0:4] K2=given[0:2]+dob[5:10]"
+                      + (f", {args.utf16_frac:.0%} UTF-16 names" if args.utf16_frac else ""),
                  props=[prop("NAME", A.CMP_JAROWINKLER, 0.1, 0.95),
                         prop("ADDRESS", A.CMP_LEVENSHTEIN, 0.2, 0.8),
                         prop("DOB", A.CMP_LEVENSHTEIN, 0.1, 0.85)],
@@ -163,6 +181,7 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    heartbeat(rank)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None

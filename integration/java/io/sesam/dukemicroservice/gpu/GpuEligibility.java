@@ -1,0 +1,97 @@
+package io.sesam.dukemicroservice.gpu;
+
+import java.lang.reflect.Field;
+
+import no.priv.garshol.duke.Comparator;
+import no.priv.garshol.duke.Configuration;
+import no.priv.garshol.duke.Property;
+
+/**
+ * Whether a pipeline can run on the GPU, and the DK_CMP_* opcode of each comparator
+ * (include/dukehip.h; the same table as dukehip/config.py COMPARATOR_CLASSES).  A pipeline is
+ * GPU-eligible as a whole: any comparator without a kernel keeps it on stock Duke, so there is
+ * no silent divergence.  The bean parameters ConfigLoader set (QGramComparator q / formula /
+ * tokenizer, NumericComparator min-ratio) are read back by field name [Duke 1.2, recalled].
+ */
+public final class GpuEligibility {
+    private GpuEligibility() {}
+
+    public static final class Opcode {
+        public final int comparator, q, formula, tokenizer;
+        public final double minRatio;
+
+        Opcode(int comparator, int q, int formula, int tokenizer, double minRatio) {
+            this.comparator = comparator;
+            this.q = q;
+            this.formula = formula;
+            this.tokenizer = tokenizer;
+            this.minRatio = minRatio;
+        }
+    }
+
+    public static boolean check(Configuration config) {
+        try {
+            for (Property p : config.getProperties())
+                if (!p.isIdProperty() && !p.isIgnoreProperty()) opcode(p.getComparator());
+            return true;
+        } catch (IllegalArgumentException e) {
+            return false;
+        }
+    }
+
+    public static Opcode opcode(Comparator c) {
+        if (c == null) return new Opcode(DukeHip.CMP_NONE, 2, 0, 0, 0.0);
+        String name = c.getClass().getName();
+        switch (name) {
+            case "no.priv.garshol.duke.comparators.Levenshtein":
+                return new Opcode(DukeHip.CMP_LEVENSHTEIN, 2, 0, 0, 0.0);
+            case "no.priv.garshol.duke.comparators.JaroWinkler":
+                return new Opcode(DukeHip.CMP_JAROWINKLER, 2, 0, 0, 0.0);
+            case "no.priv.garshol.duke.comparators.ExactComparator":
+                return new Opcode(DukeHip.CMP_EXACT, 2, 0, 0, 0.0);
+            case "no.priv.garshol.duke.comparators.WeightedLevenshtein":
+                return new Opcode(DukeHip.CMP_WEIGHTED_LEVENSHTEIN, 2, 0, 0, 0.0);
+            case "no.priv.garshol.duke.comparators.NumericComparator":
+                return new Opcode(DukeHip.CMP_NUMERIC, 2, 0, 0, ((Number) field(c, "minratio")).doubleValue());
+            case "no.priv.garshol.duke.comparators.QGramComparator": {
+                int q = ((Number) field(c, "q")).intValue();
+                int formula = ordinal(field(c, "formula"), "OVERLAP", "JACCARD", "DICE");
+                int tok = ordinal(field(c, "tokenizer"), "BASIC", "POSITIONAL", "ENDS");
+                if (q < 1 || q > 4 || (tok == 1 && q > 3)) throw new IllegalArgumentException("q");
+                return new Opcode(DukeHip.CMP_QGRAM, q, formula, tok, 0.0);
+            }
+            case "no.priv.garshol.duke.comparators.DiceCoefficientComparator":
+            case "no.priv.garshol.duke.comparators.JaccardIndexComparator": {
+                Object sub = field(c, "subcomp");
+                if (sub != null && !sub.getClass().getName().equals("no.priv.garshol.duke.comparators.ExactComparator"))
+                    throw new IllegalArgumentException("sub-comparator");
+                return new Opcode(name.endsWith("DiceCoefficientComparator") ? DukeHip.CMP_DICE_TOKENS
+                                                                           : DukeHip.CMP_JACCARD_TOKENS, 2, 0, 0, 0.0);
+            }
+            default:
+                throw new IllegalArgumentException("no GPU kernel for " + name);
+        }
+    }
+
+    private static Object field(Object o, String name) {
+        for (Class<?> k = o.getClass(); k != null; k = k.getSuperclass()) {
+            try {
+                Field f = k.getDeclaredField(name);
+                f.setAccessible(true);
+                return f.get(o);
+            } catch (NoSuchFieldException e) {
+                // superclass next
+            } catch (IllegalAccessException e) {
+                throw new IllegalArgumentException(e);
+            }
+        }
+        throw new IllegalArgumentException("field " + name);
+    }
+
+    private static int ordinal(Object enumValue, String... names) {
+        String s = String.valueOf(enumValue);
+        for (int i = 0; i < names.length; i++)
+            if (names[i].equals(s)) return i;
+        throw new IllegalArgumentException(s);
+    }
+}
