@@ -92,6 +92,23 @@ typedef struct dk_property {
   double min_ratio;        /* NumericComparator.setMinRatio (default 0.0) */
 } dk_property;
 
+/* Lucene-compatible candidate source: the reference's own
+ * IncrementalLuceneDatabase.findCandidateMatches (IncrementalLuceneDatabase.java:459-492) --
+ * every lookup property value's StandardAnalyzer tokens as SHOULD TermQuerys (after
+ * escapeLucene, :295-342), MUST_NOT the query's dukeGroupNo (LINKAGE) and dukeDeleted, the
+ * top max_hits documents by Lucene's DefaultSimilarity TF-IDF score (doQuery :377-414) kept
+ * while score >= min_relevance (App.configureDatabase :550-563 defaults: 10, 0.9).  Candidates
+ * reach Processor.compare in hit order; the query itself can be a hit (isSameAs drops it
+ * there, as in Duke).  [Lucene 4.x scoring / analysis recalled: parity unpinned.]  Values of
+ * lookup properties must lie in U+0000-U+00FF (else DK_E_UNSUPPORTED) and give <= 256 query
+ * clauses per record. */
+typedef struct dk_lucene {
+  int32_t nlookup;            /* lookup properties (Configuration.getLookupProperties order) */
+  const int32_t* lookup_prop; /* their indices into dk_schema.props */
+  int32_t max_hits;           /* setMaxSearchHits: 1..100 */
+  float min_relevance;        /* setMinRelevance */
+} dk_lucene;
+
 typedef struct dk_schema {
   int32_t nprops;           /* scored properties, in Processor.compare iteration order */
   const dk_property* props;
@@ -99,6 +116,8 @@ typedef struct dk_schema {
   double maybe_threshold;   /* <maybe-threshold>; 0.0 = none (Duke's default) */
   int32_t mode;             /* DK_MODE_* */
   int32_t nkeys;            /* key functions (blocking); ignored in ALLPAIRS mode; <= 8 */
+  const dk_lucene* lucene;  /* non-NULL: Lucene-compatible candidates instead of key
+                               functions (nkeys 0; DEDUP or LINKAGE) */
 } dk_schema;
 
 /* One property's values for the n records of a batch. */
@@ -342,6 +361,11 @@ int dk_linkdb_apply(dk_linkdb* db, const dk_link_batch* batch, int64_t timestamp
  * (timestamp, assertion order) -- the reference iterates a HashMap (order unpinned) */
 int dk_linkdb_changes_since(const dk_linkdb* db, int64_t since, dk_link_list** out);
 void dk_free_link_list(dk_link_list* list);
+
+/* the StandardAnalyzer tokens of one value (escape: escapeLucene first, the query side),
+ * '\n'-joined into out (test hook of the DK_CAND_LUCENE analysis) */
+int dk_lucene_analyze(const uint16_t* units, uint64_t n, int escape, char* out, uint64_t cap,
+                      uint64_t* ntokens);
 
 const char* dk_last_error(void);
 int dk_abi_version(void);

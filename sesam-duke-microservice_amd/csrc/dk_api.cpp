@@ -22,6 +22,11 @@
 
 using namespace dk;
 
+namespace dk {  // dk_lucene.cpp (host): the StandardAnalyzer restatement
+bool lucene_analyze(const uint32_t* u, size_t n, bool escape, std::vector<std::string>& out);
+uint8_t lucene_norm_byte(uint32_t ntokens);
+}  // namespace dk
+
 // ----------------------------------------------------------------------------------------
 // errors
 // ----------------------------------------------------------------------------------------
@@ -347,6 +352,20 @@ struct dk_ctx {
   // profiling (Processor.setPerformanceProfiling)
   bool profiling = false;
   dk_profile prof{};
+  // Lucene-compatible candidate source (dk_schema.lucene): per lookup field a term
+  // dictionary; per row its query clauses (host offsets + device copy) and length norms;
+  // the postings of indexed rows, appended per upsert and sorted by the first match after
+  // an index change (index state, like the blocking tables)
+  struct Lucene {
+    bool on = false;
+    std::vector<int> fields;
+    int max_hits = 10;
+    float min_rel = 0.9f;
+    std::vector<std::unordered_map<std::string, uint32_t>> dict;
+    std::vector<uint64_t> qoff{0};
+    uint64_t npost = 0, nsorted = 0, max_doc = 0;
+    DevBuf pkey, ptf, qoff_d, qterm, norm, skey, stf, tkey, hits, exact;
+  } luc;
 };
 
 static hipError_t grow_rows(dk_ctx* c, uint64_t need) {
@@ -361,6 +380,11 @@ static hipError_t grow_rows(dk_ctx* c, uint64_t need) {
   GROW(c->flags, uint8_t);
   GROW(c->group, uint8_t);
   for (int k = 0; k < c->schema.nkeys; ++k) GROW(c->keys[k], uint64_t);
+  if (c->luc.on) {
+    const uint64_t nf = c->luc.fields.size();
+    if ((e = c->luc.norm.reserve(nc * nf, n * nf, s)) != hipSuccess) return e;
+    if ((e = c->luc.qoff_d.reserve((nc + 1) * 8, (n + 1) * 8, s)) != hipSuccess) return e;
+  }
   for (auto& p : c->P) {
     GROW(p.off, uint32_t);
     GROW(p.len, uint16_t);
@@ -385,8 +409,25 @@ static int validate_schema(const dk_schema* s) {
   if (s->nprops > 0 && !s->props) return fail(DK_E_INVALID, "props is NULL");
   if (s->mode < DK_MODE_DEDUP || s->mode > DK_MODE_ALLPAIRS)
     return fail(DK_E_INVALID, "unknown mode %d", s->mode);
-  if (s->mode != DK_MODE_ALLPAIRS && (s->nkeys < 1 || s->nkeys > kMaxKeys))
+  if (s->lucene) {
+    const dk_lucene& L = *s->lucene;
+    if (s->mode == DK_MODE_ALLPAIRS)
+      return fail(DK_E_INVALID, "the Lucene candidate source needs DEDUP or LINKAGE mode");
+    if (s->nkeys != 0) return fail(DK_E_INVALID, "the Lucene candidate source takes no key functions");
+    if (L.nlookup < 1 || L.nlookup > s->nprops || !L.lookup_prop)
+      return fail(DK_E_INVALID, "nlookup %d out of range [1, %d]", L.nlookup, s->nprops);
+    for (int i = 0; i < L.nlookup; ++i) {
+      if (L.lookup_prop[i] < 0 || L.lookup_prop[i] >= s->nprops)
+        return fail(DK_E_INVALID, "lookup property %d out of range", L.lookup_prop[i]);
+      for (int j = 0; j < i; ++j)
+        if (L.lookup_prop[j] == L.lookup_prop[i]) return fail(DK_E_INVALID, "lookup property repeated");
+    }
+    if (L.max_hits < 1 || L.max_hits > kLuceneMaxHits)
+      return fail(DK_E_UNSUPPORTED, "max_hits %d (supported 1..%d: larger values grow the search "
+                  "limit adaptively, EstimateResultTracker)", L.max_hits, kLuceneMaxHits);
+  } else if (s->mode != DK_MODE_ALLPAIRS && (s->nkeys < 1 || s->nkeys > kMaxKeys)) {
     return fail(DK_E_INVALID, "nkeys %d out of range [1, %d]", s->nkeys, kMaxKeys);
+  }
   for (int i = 0; i < s->nprops; ++i) {
     const dk_property& p = s->props[i];
     switch (p.comparator) {
@@ -443,6 +484,14 @@ int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
   if (!c) return fail(DK_E_NOMEM, "out of host memory");
   c->schema = *schema;
   c->schema.props = nullptr;
+  c->schema.lucene = nullptr;
+  if (schema->lucene) {
+    c->luc.on = true;
+    c->luc.fields.assign(schema->lucene->lookup_prop, schema->lucene->lookup_prop + schema->lucene->nlookup);
+    c->luc.max_hits = schema->lucene->max_hits;
+    c->luc.min_rel = schema->lucene->min_relevance;
+    c->luc.dict.resize(schema->lucene->nlookup);
+  }
   c->P.resize(schema->nprops);
   for (int i = 0; i < schema->nprops; ++i) c->P[i].cfg = schema->props[i];
   if (c->schema.mode == DK_MODE_ALLPAIRS) c->schema.nkeys = 0;
@@ -709,6 +758,83 @@ static int stage_keys(dk_ctx* c, const dk_batch* b, int style, std::vector<uint6
   return DK_OK;
 }
 
+// The Lucene source's share of a batch (IncrementalLuceneDatabase.index :505-575 and the
+// query side of findCandidateMatches :459-492): per lookup field, each value analyzed as
+// stored (postings + length norm; rows that enter the index only) and escaped (the row's
+// query clauses, in lookup-field order).  Host only; term ids are interned into the ctx's
+// dictionaries (an entry of a failed batch is harmless).
+struct LuceneStage {
+  std::vector<uint64_t> pkey;
+  std::vector<uint32_t> ptf, qterm;
+  std::vector<uint64_t> qoff;   // absolute clause offsets of rows row0 + 1 .. row0 + n
+  std::vector<uint8_t> norm;    // [i * nfields + f]
+};
+
+static int stage_lucene(dk_ctx* c, const dk_batch* b, uint64_t n, uint64_t row0, bool transient,
+                        LuceneStage& S) {
+  auto& L = c->luc;
+  const int nf = (int)L.fields.size();
+  S.norm.assign(n * nf, 0);
+  S.qoff.resize(n);
+  std::vector<uint32_t> u;
+  std::vector<std::string> toks;
+  std::unordered_map<uint32_t, uint32_t> tf;
+  uint64_t at = L.qoff.back();
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t nclauses = 0;
+    for (int f = 0; f < nf; ++f) {
+      const dk_column& col = b->columns[L.fields[f]];
+      if (col.present && !col.present[i]) continue;
+      const uint32_t a = col.offsets[i], e = col.offsets[i + 1];
+      u.resize(e - a);
+      for (uint32_t j = a; j < e; ++j)
+        u[j - a] = col.width == 1 ? ((const uint8_t*)col.units)[j] : ((const uint16_t*)col.units)[j];
+      auto& dict = L.dict[f];
+      auto term_id = [&](const std::string& t, uint32_t* id) {
+        auto it = dict.find(t);
+        if (it == dict.end()) {
+          if (dict.size() >= (1u << 24)) return false;
+          it = dict.emplace(t, (uint32_t)dict.size()).first;
+        }
+        *id = ((uint32_t)f << 24) | it->second;
+        return true;
+      };
+      if (!transient && !u.empty()) {  // index side: the value as stored ("" is skipped, :558)
+        if (!lucene_analyze(u.data(), u.size(), false, toks))
+          return fail(DK_E_UNSUPPORTED, "record %llu: a lookup value outside U+0000-U+00FF "
+                      "(the native StandardAnalyzer covers Latin-1)", (unsigned long long)i);
+        S.norm[i * nf + f] = lucene_norm_byte((uint32_t)toks.size());
+        tf.clear();
+        for (const auto& t : toks) {
+          uint32_t id;
+          if (!term_id(t, &id)) return fail(DK_E_UNSUPPORTED, "more than 2^24 terms in a lookup field");
+          tf[id] += 1;
+        }
+        for (const auto& kv : tf) {
+          S.pkey.push_back(((uint64_t)kv.first << 32) | (row0 + i));
+          S.ptf.push_back(kv.second);
+        }
+      }
+      // query side: escapeLucene, then the same analyzer (parseTokens)
+      if (!lucene_analyze(u.data(), u.size(), true, toks))
+        return fail(DK_E_UNSUPPORTED, "record %llu: a lookup value outside U+0000-U+00FF",
+                    (unsigned long long)i);
+      for (const auto& t : toks) {
+        uint32_t id;
+        if (!term_id(t, &id)) return fail(DK_E_UNSUPPORTED, "more than 2^24 terms in a lookup field");
+        S.qterm.push_back(id);
+        ++nclauses;
+      }
+    }
+    if (nclauses > (uint64_t)kLuceneMaxClauses)
+      return fail(DK_E_UNSUPPORTED, "record %llu: %llu query clauses (the GPU path holds %d)",
+                  (unsigned long long)i, (unsigned long long)nclauses, kLuceneMaxClauses);
+    at += nclauses;
+    S.qoff[i] = at;
+  }
+  return DK_OK;
+}
+
 static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool transient) {
   if (!c || !b) return fail(DK_E_INVALID, "NULL argument");
   if (!transient && c->transient)
@@ -749,6 +875,11 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     int rc = stage_keys(c, b, style, kv);
     if (rc) return rc;
   }
+  LuceneStage ls;
+  if (c->luc.on) {
+    int rc = stage_lucene(c, b, n, row0, transient, ls);
+    if (rc) return rc;
+  }
   // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517;
   // skipped with overwrite, :515); transient rows are neither alive (never candidates) nor
   // entered in the ID map.  Staged: the ID map changes are applied at commit.
@@ -783,6 +914,13 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   }
   DevBuf d_dead;
   if (!dead.empty()) HIPCHK(d_dead.reserve(dead.size() * 4, 0, s));
+  auto& L = c->luc;
+  if (L.on) {
+    const uint64_t np = L.npost + ls.pkey.size(), nqt = L.qoff.back();
+    HIPCHK(L.pkey.reserve(np * 8 + 8, L.npost * 8, s));
+    HIPCHK(L.ptf.reserve(np * 4 + 4, L.npost * 4, s));
+    HIPCHK(L.qterm.reserve((nqt + ls.qterm.size()) * 4 + 4, nqt * 4, s));
+  }
 
   // 3. commit
   c->index_gen++;
@@ -808,7 +946,28 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   for (int k = 0; k < nk; ++k)
     HIPCHK(hipMemcpyAsync(c->keys[k].as<uint64_t>() + row0, kv.data() + (uint64_t)k * n, n * 8,
                           hipMemcpyHostToDevice, s));
+  if (L.on) {
+    const uint64_t nf = L.fields.size(), nqt = L.qoff.back();
+    if (!ls.pkey.empty()) {
+      HIPCHK(hipMemcpyAsync(L.pkey.as<uint64_t>() + L.npost, ls.pkey.data(), ls.pkey.size() * 8,
+                            hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(L.ptf.as<uint32_t>() + L.npost, ls.ptf.data(), ls.ptf.size() * 4,
+                            hipMemcpyHostToDevice, s));
+    }
+    if (!ls.qterm.empty())
+      HIPCHK(hipMemcpyAsync(L.qterm.as<uint32_t>() + nqt, ls.qterm.data(), ls.qterm.size() * 4,
+                            hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(L.norm.as<uint8_t>() + row0 * nf, ls.norm.data(), n * nf,
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(L.qoff_d.as<uint64_t>() + row0, &L.qoff[row0], 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(L.qoff_d.as<uint64_t>() + row0 + 1, ls.qoff.data(), n * 8,
+                          hipMemcpyHostToDevice, s));
+  }
   HIPCHK(hipStreamSynchronize(s));  // host staging goes out of scope
+  if (L.on) {
+    L.npost += ls.pkey.size();
+    L.qoff.insert(L.qoff.end(), ls.qoff.begin(), ls.qoff.end());
+  }
   for (const auto& br : batch_row) c->ident_row[br.first] = br.second;
   for (uint32_t r : dead)
     if (c->base_ok && r < c->base_rows) c->base_dead.push_back(r);
@@ -839,6 +998,7 @@ int dk_drop_transient(dk_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   c->nrows = c->transient_row0;
   c->index_gen++;
+  if (c->luc.on) c->luc.qoff.resize(c->nrows + 1);  // transient rows add no postings
   for (size_t p = 0; p < c->P.size(); ++p) {
     const auto& m = c->transient_mark[p];
     c->P[p].units_used = m.units;
@@ -1262,6 +1422,38 @@ static int build_delta(dk_ctx* c, BlockTables& T) {
   return DK_OK;
 }
 
+// Lucene source: the postings of the rows in the index (kAlive: superseded versions were
+// deleted by ID, transient rows never entered; dukeDeleted rows stay, as in the reference's
+// index) sorted by (field, term, row), and maxDoc.  Index state, built like the blocking
+// tables by the first match after an index change.
+static int build_lucene(dk_ctx* c, BlockTables& T, uint64_t* Mout) {
+  auto& L = c->luc;
+  hipStream_t s = c->stream;
+  const uint64_t np = L.npost;
+  HIPCHK(L.tkey.reserve(np * 8 + 8, 0, s));
+  HIPCHK(L.skey.reserve(np * 8 + 8, 0, s));
+  HIPCHK(L.stf.reserve(np * 4 + 4, 0, s));
+  uint64_t* cnt = c->counters.as<uint64_t>() + 2;
+  HIPCHK(hipMemsetAsync(cnt, 0, 16, s));
+  HIPCHK(launch_lucene_prep(L.pkey.as<uint64_t>(), np, c->flags.as<uint8_t>(), c->nrows,
+                            L.tkey.as<uint64_t>(), cnt, s));
+  if (np) {
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return sort_pairs_u64_u32(t, b, L.tkey.as<uint64_t>(), L.skey.as<uint64_t>(), L.ptf.as<uint32_t>(),
+                                L.stf.as<uint32_t>(), np, s);
+    }));
+  }
+  uint64_t h[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(h, cnt, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  L.nsorted = h[0];
+  L.max_doc = h[1];
+  T.nseg = 1;
+  T.seg_shift = 0;
+  *Mout = L.max_doc;
+  return DK_OK;
+}
+
 // The blocking tables and the candidate replica (index state): built by the first call
 // after the index changed, reused until the next change.  An index that only grew (or lost
 // rows to delete-by-ID) since the last full sort gets a delta build.
@@ -1269,6 +1461,20 @@ static int ensure_tables(dk_ctx* c, BlockTables* Tout, uint64_t* Mout) {
   if (c->tables_gen == c->index_gen) {
     *Tout = c->tables;
     *Mout = c->tables_m;
+    return DK_OK;
+  }
+  if (c->luc.on) {
+    BlockTables T{};
+    T.group = c->group.as<uint8_t>();
+    uint64_t M = 0;
+    int rc = build_lucene(c, T, &M);
+    if (rc) return rc;
+    c->prof.full_builds += 1;
+    c->tables = T;
+    c->tables_m = M;
+    c->tables_gen = c->index_gen;
+    *Tout = T;
+    *Mout = M;
     return DK_OK;
   }
   BlockTables T{};
@@ -1322,6 +1528,76 @@ static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
   return true;
 }
 
+// Lucene source, per dk_match: every query's hits (k_lucene_topk) become its candidate
+// range -- positions qi * max_hits + j of a per-call candidate replica, in hit order -- and
+// the slot layout (counts, offsets, wave map) of the direct schedule.  d_queries holds the
+// query rows.  exact (host, optional): the hits per query.
+static int lucene_candidates(dk_ctx* c, uint64_t nq, uint64_t* total, uint64_t* generated,
+                             uint64_t* exact) {
+  auto& L = c->luc;
+  hipStream_t s = c->stream;
+  const uint64_t K = (uint64_t)L.max_hits, npos = std::max<uint64_t>(nq * K, 1);
+  HIPCHK(L.hits.reserve(npos * 4 + 4, 0, s));
+  HIPCHK(hipMemsetAsync(L.hits.p, 0, npos * 4, s));  // unused positions name row 0
+  HIPCHK(c->ranges.reserve(nq * 8 + 8, 0, s));
+  HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
+  HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
+  if (exact) HIPCHK(L.exact.reserve(nq * 8 + 8, 0, s));
+  HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
+  LuceneParams P{};
+  P.queries = c->d_queries.as<uint32_t>();
+  P.nq = nq;
+  P.qoff = L.qoff_d.as<uint64_t>();
+  P.qterm = L.qterm.as<uint32_t>();
+  P.skey = L.skey.as<uint64_t>();
+  P.stf = L.stf.as<uint32_t>();
+  P.npost = L.nsorted;
+  P.norm = L.norm.as<uint8_t>();
+  P.nfields = (int32_t)L.fields.size();
+  P.linkage = c->schema.mode == DK_MODE_LINKAGE;
+  P.flags = c->flags.as<uint8_t>();
+  P.group = c->group.as<uint8_t>();
+  P.max_doc = L.max_doc;
+  P.max_hits = L.max_hits;
+  P.min_relevance = L.min_rel;
+  P.hits = L.hits.as<uint32_t>();
+  P.ranges = c->ranges.as<uint2>();
+  P.counts = c->counts.as<uint64_t>();
+  P.exact = exact ? L.exact.as<uint64_t>() : nullptr;
+  P.real = c->counters.as<uint64_t>() + 2;
+  HIPCHK(launch_lucene_topk(P, s));
+  if (exact) {
+    HIPCHK(hipMemcpyAsync(exact, L.exact.p, nq * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return DK_OK;
+  }
+  uint64_t* hs = c->h_small.as<uint64_t>();
+  HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
+  HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+    return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
+  }));
+  HIPCHK(hipMemcpyAsync(&hs[3], c->qoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&hs[2], c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *total = hs[3];
+  *generated = hs[2];
+  HIPCHK(c->wq.reserve(*total / 64 * 4 + 4, 0, s));
+  HIPCHK(launch_wavemap(c->qoff.as<uint64_t>(), nq, c->wq.as<uint32_t>(), s));
+  // the hits' values in candidate-replica order, and their identities (isSameAs)
+  c->rowof_p = L.hits.as<uint32_t>();
+  c->rstride = npos;
+  int rc = layout_replica(c, c->rep, npos);
+  if (rc) return rc;
+  rc = fill_replica(c, c->rep, c->rowof_p, 0, npos);
+  if (rc) return rc;
+  HIPCHK(c->rident.reserve(npos * 8 + 8, 0, s));
+  BlockTables T{};
+  uint64_t* rk[kMaxKeys] = {};
+  HIPCHK(launch_replicate_rows(c->rowof_p, 0, npos, c->ident.as<uint64_t>(), c->rident.as<uint64_t>(),
+                               T, rk, s));
+  return DK_OK;
+}
+
 static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
                      ResultHolder* R, bool contiguous) {
   hipStream_t s = c->stream;
@@ -1345,8 +1621,13 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   // ---- candidate counts per query -> slot offsets ----
   Timer t_gen(c, &c->prof.ms_generate, s);
   uint64_t total = 0, generated = 0, mpad = 0, otot = 0, mtot = 0;
+  const bool lucene = c->luc.on;
+  if (lucene) {
+    rc = lucene_candidates(c, nq, &total, &generated, nullptr);
+    if (rc) return rc;
+  }
   const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
-  bool sym = contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
+  bool sym = !lucene && contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
   const uint32_t r0 = nq ? query_rows[0] : 0;
   uint64_t* hs = c->h_small.as<uint64_t>();
   if (sym) {
@@ -1403,7 +1684,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s));
     HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), c->mqoff.as<uint64_t>(),
                         nq, T.nseg, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
-  } else if (!allpairs) {
+  } else if (!allpairs && !lucene) {
     HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
     HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
@@ -1422,7 +1703,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     // every wave of slots knows its query
     HIPCHK(c->wq.reserve(total / 64 * 4 + 4, 0, s));
     HIPCHK(launch_wavemap(c->qoff.as<uint64_t>(), nq, c->wq.as<uint32_t>(), s));
-  } else {
+  } else if (allpairs) {
     mpad = (M + 63) & ~(uint64_t)63;
     total = nq * mpad;
     generated = nq * M;
@@ -1509,7 +1790,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     src.nkeys = nk;
     src.nseg = T.nseg;
     src.seg_shift = T.seg_shift;
-    for (int k = 0; k < T.nseg; ++k) src.segoff[k] = T.seg_off[k];
+    for (int k = 0; k < T.nseg; ++k) src.segoff[k] = T.seg_off[k];  // Lucene: one segment at 0
     src.rident = c->rident.as<uint64_t>();
     for (int k = 0; k < nk; ++k) {
       src.qkeys[k] = c->keys[k].as<uint64_t>();
@@ -1752,6 +2033,7 @@ int dk_candidate_counts(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, uint
   }
   HIPCHK(c->d_queries.reserve(nq * 4 + 4, 0, s));
   HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
+  if (c->luc.on) return lucene_candidates(c, nq, nullptr, nullptr, counts);  // the hits
   HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
   HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
   HIPCHK(launch_count_exact(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(),
@@ -1891,6 +2173,11 @@ static void clear_index(dk_ctx* c) {
   c->index_gen++;
   c->base_ok = false;
   c->base_dead.clear();
+  if (c->luc.on) {
+    c->luc.qoff.assign(1, 0);
+    c->luc.npost = 0;
+    for (auto& d : c->luc.dict) d.clear();
+  }
   c->ident_row.clear();
   for (auto& t : c->intern) t.clear();
   c->key_style = 0;

@@ -230,7 +230,43 @@ struct ReplicaJob {
   void* rgrams;
 };
 
+// Lucene-compatible candidate source (DK_CAND_LUCENE, include/dukehip.h dk_lucene).
+// Postings: one entry per (lookup field, term, row) of the rows in the index, key =
+// (field << 24 | term) << 32 | row, value = the term's frequency in the row's value; sorted by
+// key they give every term's documents in row order (= Lucene doc id order).
+constexpr int kLuceneMaxClauses = 256;
+constexpr int kLuceneMaxHits = 100;
+constexpr int kLuceneTile = 2048;      // rows per accumulation tile (LDS)
+
+struct LuceneParams {
+  const uint32_t* queries;
+  uint64_t nq;
+  const uint64_t* qoff;     // per row: its query clauses [qoff[row], qoff[row+1]) in qterm
+  const uint32_t* qterm;    // field << 24 | term of each clause, in clause order
+  const uint64_t* skey;     // sorted postings keys
+  const uint32_t* stf;      // their term frequencies
+  uint64_t npost;
+  const uint8_t* norm;      // [row * nfields + field]: SmallFloat-encoded length norm
+  int32_t nfields;
+  int32_t linkage;
+  const uint8_t* flags;     // kDeleted rows are never hits (MUST_NOT dukeDeleted:true)
+  const uint8_t* group;     // LINKAGE: MUST_NOT dukeGroupNo == the query's group
+  uint64_t max_doc;         // documents in the index (IndexReader.maxDoc of a merged index)
+  int32_t max_hits;
+  float min_relevance;
+  uint32_t* hits;           // [qi * max_hits + j]: row of hit j of query qi (score order)
+  uint2* ranges;            // [qi]: its hit positions {qi * max_hits, + nhits}
+  uint64_t* counts;         // [qi]: nhits rounded up to 64 (score slots)
+  uint64_t* exact;          // [qi]: nhits (NULL: not written)
+  uint64_t* real;           // += nhits
+};
+
 // ---- launchers (dk_kernels.hip) ----
+// postings of rows that are in the index (kAlive): key kept, others set to ~0 (sorted last);
+// counts[0] += entries kept, counts[1] += rows in the index among [0, nrows)
+hipError_t launch_lucene_prep(const uint64_t* key, uint64_t npost, const uint8_t* flags, uint64_t nrows,
+                              uint64_t* out_key, uint64_t* counts, hipStream_t s);
+hipError_t launch_lucene_topk(const LuceneParams& L, hipStream_t s);
 hipError_t launch_widen_u8(const uint8_t* src, uint16_t* dst, uint64_t n, hipStream_t s);
 hipError_t launch_clear_flag(uint8_t* flags, const uint32_t* rows, uint64_t n, uint8_t bit,
                              hipStream_t s);

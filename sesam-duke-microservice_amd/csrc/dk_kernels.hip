@@ -1770,6 +1770,178 @@ __global__ void k_mark_dead(const BlockTables T, const uint32_t* __restrict__ ro
 }
 
 // ------------------------------------------------------------------------------------
+// Lucene-compatible candidate source (DK_CAND_LUCENE): IncrementalLuceneDatabase.
+// findCandidateMatches + EstimateResultTracker.doQuery over a postings table
+// ------------------------------------------------------------------------------------
+__global__ void k_lucene_prep(const uint64_t* __restrict__ key, uint64_t npost,
+                              const uint8_t* __restrict__ flags, uint64_t nrows,
+                              uint64_t* __restrict__ out_key, uint64_t* __restrict__ counts) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t kept = 0, docs = 0;
+  if (i < npost) {
+    const uint64_t k = key[i];
+    const bool in = (flags[(uint32_t)k] & kAlive) != 0;
+    out_key[i] = in ? k : ~0ull;
+    kept = in;
+  }
+  if (i < nrows) docs = (flags[i] & kAlive) != 0;
+  for (int o = 32; o > 0; o >>= 1) {
+    kept += __shfl_xor(kept, o);
+    docs += __shfl_xor(docs, o);
+  }
+  if (lane_id() == 0) {
+    if (kept) atomicAdd((unsigned long long*)&counts[0], (unsigned long long)kept);
+    if (docs) atomicAdd((unsigned long long*)&counts[1], (unsigned long long)docs);
+  }
+}
+
+__device__ __forceinline__ uint64_t lower_bound_key(const uint64_t* a, uint64_t lo, uint64_t hi,
+                                                    uint64_t v) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// SmallFloat.byte315ToFloat: the decoded length norm
+__device__ __forceinline__ float decode_norm(uint32_t b) {
+  return b == 0 ? 0.0f : __uint_as_float((b << 21) + ((63u - 15u) << 24));
+}
+
+// One workgroup per query.  The query's clauses (its lookup values' tokens, escaped) are
+// TermQuerys on the postings; DefaultSimilarity [Lucene 4.x, recalled]:
+//   idf = (float)(ln(maxDoc / (double)(df + 1)) + 1), queryNorm = (float)(1 / sqrt(sum idf^2)),
+//   clause weight = (idf * queryNorm) * idf, term score = ((float)sqrt(tf) * weight) * norm,
+//   document score = (float)(sum over matching clauses in clause order, in double) * coord,
+//   coord = overlap / (float)clauses.
+// Rows are visited in tiles of kLuceneTile (only tiles holding a posting): the clauses add
+// into a per-tile LDS accumulator one after another (a barrier between clauses keeps the sum
+// order), then rows that reach min_relevance and beat the current max_hits-th hit are merged
+// into the hit list (score descending, row ascending: Lucene's doc-id tie break).
+__global__ __launch_bounds__(256) void k_lucene_topk(const LuceneParams L) {
+  __shared__ double acc[kLuceneTile];
+  __shared__ uint16_t cnt[kLuceneTile];
+  __shared__ uint64_t cur[kLuceneMaxClauses], endp[kLuceneMaxClauses], hip_[kLuceneMaxClauses];
+  __shared__ uint32_t cft[kLuceneMaxClauses];
+  __shared__ float w[kLuceneMaxClauses];
+  __shared__ float coordf[kLuceneMaxClauses + 1];
+  __shared__ float topS[kLuceneMaxHits];
+  __shared__ uint32_t topR[kLuceneMaxHits];
+  __shared__ float cbS[kLuceneTile];
+  __shared__ uint32_t cbR[kLuceneTile];
+  __shared__ int ntop, ncb;
+  __shared__ uint32_t tile0;
+  __shared__ float qnorm;
+  const uint64_t qi = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint32_t q = L.queries[qi];
+  const uint64_t c0 = L.qoff[q];
+  const int nc = (int)(L.qoff[q + 1] - c0);  // <= kLuceneMaxClauses (checked by dk_upsert)
+  const int K = L.max_hits;
+  const uint8_t qgroup = L.group[q];
+  if (tid < nc) {
+    const uint32_t ft = L.qterm[c0 + tid];
+    const uint64_t lo = lower_bound_key(L.skey, 0, L.npost, (uint64_t)ft << 32);
+    const uint64_t hi = lower_bound_key(L.skey, lo, L.npost, (uint64_t)(ft + 1) << 32);
+    cft[tid] = ft;
+    cur[tid] = lo;
+    hip_[tid] = hi;
+    w[tid] = (float)(log((double)L.max_doc / (double)(hi - lo + 1)) + 1.0);  // idf
+  }
+  for (int k = tid; k <= nc; k += 256) coordf[k] = nc ? (float)k / (float)nc : 0.0f;
+  if (tid == 0) {
+    ntop = 0;
+    float ssw = 0.0f;  // BooleanWeight.getValueForNormalization: float, clause order
+    for (int c = 0; c < nc; ++c) ssw += w[c] * w[c];
+    float qn = (float)(1.0 / sqrt((double)ssw));
+    if (!(qn == qn) || qn == __builtin_inff()) qn = 1.0f;
+    qnorm = qn;
+  }
+  __syncthreads();
+  if (tid < nc) w[tid] = (w[tid] * qnorm) * w[tid];
+  __syncthreads();
+  for (;;) {
+    if (tid == 0) {
+      uint32_t m = 0xFFFFFFFFu;
+      for (int c = 0; c < nc; ++c)
+        if (cur[c] < hip_[c]) m = min(m, (uint32_t)L.skey[cur[c]]);
+      tile0 = m == 0xFFFFFFFFu ? m : m / kLuceneTile * kLuceneTile;
+      ncb = 0;
+    }
+    __syncthreads();
+    const uint32_t t0 = tile0;
+    if (t0 == 0xFFFFFFFFu) break;
+    for (int j = tid; j < kLuceneTile; j += 256) {
+      acc[j] = 0.0;
+      cnt[j] = 0;
+    }
+    if (tid < nc) {  // the clause's postings inside this tile
+      const uint64_t end = ((uint64_t)cft[tid] << 32) | ((uint64_t)t0 + kLuceneTile);
+      endp[tid] = lower_bound_key(L.skey, cur[tid], hip_[tid], end);
+    }
+    __syncthreads();
+    for (int c = 0; c < nc; ++c) {
+      const int f = (int)(cft[c] >> 24);
+      const float wc = w[c];
+      for (uint64_t e = cur[c] + tid; e < endp[c]; e += 256) {
+        const uint32_t row = (uint32_t)L.skey[e];
+        const float tf = (float)sqrt((double)L.stf[e]);
+        const float sc = (tf * wc) * decode_norm(L.norm[(uint64_t)row * L.nfields + f]);
+        acc[row - t0] += (double)sc;
+        cnt[row - t0] += 1;
+      }
+      __syncthreads();
+    }
+    if (tid < nc) cur[tid] = endp[tid];
+    // candidates of the tile: eligible rows that reach min_relevance and the hit list
+    const int full = ntop == K;
+    const float worst = full ? topS[K - 1] : 0.0f;
+    for (int j = tid; j < kLuceneTile; j += 256) {
+      const int k = cnt[j];
+      if (!k) continue;
+      const uint32_t row = t0 + (uint32_t)j;
+      if (L.flags[row] & kDeleted) continue;
+      if (L.linkage && L.group[row] == qgroup) continue;
+      const float score = (float)(acc[j] * (double)coordf[k]);
+      if (!(score >= L.min_relevance)) continue;
+      if (full && !(score > worst)) continue;  // later rows lose ties (doc-id order)
+      const int at = atomicAdd(&ncb, 1);
+      cbS[at] = score;
+      cbR[at] = row;
+    }
+    __syncthreads();
+    if (tid == 0) {  // insertion into the sorted hit list
+      int n = ntop;
+      for (int i = 0; i < ncb; ++i) {
+        const float sc = cbS[i];
+        const uint32_t r = cbR[i];
+        int pos = n;
+        while (pos > 0 && (topS[pos - 1] < sc || (topS[pos - 1] == sc && topR[pos - 1] > r))) --pos;
+        if (pos >= K) continue;
+        for (int m = min(n, K - 1); m > pos; --m) {
+          topS[m] = topS[m - 1];
+          topR[m] = topR[m - 1];
+        }
+        topS[pos] = sc;
+        topR[pos] = r;
+        if (n < K) ++n;
+      }
+      ntop = n;
+    }
+    __syncthreads();
+  }
+  const int n = ntop;
+  if (tid < n) L.hits[qi * (uint64_t)K + tid] = topR[tid];
+  if (tid == 0) {
+    L.ranges[qi] = make_uint2((uint32_t)(qi * (uint64_t)K), (uint32_t)(qi * (uint64_t)K + n));
+    L.counts[qi] = ((uint64_t)n + 63) & ~(uint64_t)63;
+    if (L.exact) L.exact[qi] = (uint64_t)n;
+    if (L.real && n) atomicAdd((unsigned long long*)L.real, (unsigned long long)n);
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // small utility kernels
 // ------------------------------------------------------------------------------------
 __global__ void k_widen_u8(const uint8_t* __restrict__ src, uint16_t* __restrict__ dst, uint64_t n) {
@@ -1991,6 +2163,21 @@ hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nbl
 hipError_t launch_first(const uint32_t* qidx, uint64_t n, uint64_t nq, uint64_t* first,
                         hipStream_t s) {
   k_first<<<grid1d(nq + 1), 256, 0, s>>>(qidx, n, nq, first);
+  return hipGetLastError();
+}
+
+hipError_t launch_lucene_prep(const uint64_t* key, uint64_t npost, const uint8_t* flags, uint64_t nrows,
+                              uint64_t* out_key, uint64_t* counts, hipStream_t s) {
+  const uint64_t n = std::max(npost, nrows);
+  DK_LAUNCH_GUARD(n);
+  k_lucene_prep<<<grid1d(n), 256, 0, s>>>(key, npost, flags, nrows, out_key, counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_lucene_topk(const LuceneParams& L, hipStream_t s) {
+  DK_LAUNCH_GUARD(L.nq);
+  if (L.max_hits < 1 || L.max_hits > kLuceneMaxHits || L.nq > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  k_lucene_topk<<<(unsigned)L.nq, 256, 0, s>>>(L);
   return hipGetLastError();
 }
 

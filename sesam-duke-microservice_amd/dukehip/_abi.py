@@ -34,7 +34,7 @@ EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_dr
            "dk_interner_create", "dk_interner_destroy", "dk_interner_size", "dk_interner_find",
            "dk_interner_intern", "dk_pack_json", "dk_free_packed", "dk_interner_string",
            "dk_linkdb_create", "dk_linkdb_destroy", "dk_linkdb_size", "dk_linkdb_apply",
-           "dk_linkdb_changes_since", "dk_free_link_list")
+           "dk_linkdb_changes_since", "dk_free_link_list", "dk_lucene_analyze")
 
 
 class DukeHipError(RuntimeError):
@@ -49,10 +49,25 @@ class dk_property(C.Structure):
                 ("min_ratio", C.c_double)]
 
 
+class dk_lucene(C.Structure):
+    _fields_ = [("nlookup", C.c_int32), ("lookup_prop", C.POINTER(C.c_int32)),
+                ("max_hits", C.c_int32), ("min_relevance", C.c_float)]
+
+
 class dk_schema(C.Structure):
     _fields_ = [("nprops", C.c_int32), ("props", C.POINTER(dk_property)),
                 ("threshold", C.c_double), ("maybe_threshold", C.c_double),
-                ("mode", C.c_int32), ("nkeys", C.c_int32)]
+                ("mode", C.c_int32), ("nkeys", C.c_int32), ("lucene", C.POINTER(dk_lucene))]
+
+
+def lucene_source(schema, lookup_props, max_hits=10, min_relevance=0.9):
+    """Switch `schema` (a dk_schema with nkeys 0) to the Lucene-compatible candidate source
+    over the schema properties `lookup_props` (indices, lookup order)."""
+    idx = (C.c_int32 * max(1, len(lookup_props)))(*lookup_props)
+    lu = dk_lucene(len(lookup_props), idx, int(max_hits), float(min_relevance))
+    schema.lucene = C.pointer(lu)
+    schema._keep_lucene = (idx, lu)
+    return schema
 
 
 class dk_column(C.Structure):

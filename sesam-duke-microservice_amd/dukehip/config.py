@@ -73,13 +73,15 @@ class Comparator:
 
 @dataclass
 class Property:
-    """[Duke 1.2] PropertyImpl: name, comparator, low, high, id / ignore flags."""
+    """[Duke 1.2] PropertyImpl: name, comparator, low, high, id / ignore flags, lookup
+    behaviour (<property lookup="true|false|required">; "default" when absent)."""
     name: str
     comparator: Comparator | None = None
     low: float = 0.5
     high: float = 0.5
     is_id: bool = False
     ignore: bool = False
+    lookup: str = "default"
 
     def scored(self):
         return not self.is_id and not self.ignore
@@ -127,7 +129,8 @@ class DukeConfig:
         return {"threshold": self.threshold, "maybe_threshold": self.maybe_threshold,
                 "linkage": self.linkage,
                 "properties": [{"name": p.name, "comparator": comp(p.comparator), "low": p.low,
-                                "high": p.high, "is_id": p.is_id, "ignore": p.ignore}
+                                "high": p.high, "is_id": p.is_id, "ignore": p.ignore,
+                                **({"lookup": p.lookup} if p.lookup != "default" else {})}
                                for p in self.properties],
                 "data_sources": [{"dataset_id": d.dataset_id, "group_no": d.group_no,
                                   "columns": [{"name": c.name, "property": c.property,
@@ -142,7 +145,8 @@ class DukeConfig:
             return Comparator(c["class"], {k: (comp(v) if isinstance(v, dict) else v)
                                            for k, v in c.get("params", {}).items()})
         props = [Property(p["name"], comp(p["comparator"]), p["low"], p["high"],
-                          p.get("is_id", False), p.get("ignore", False)) for p in d["properties"]]
+                          p.get("is_id", False), p.get("ignore", False), p.get("lookup", "default"))
+                 for p in d["properties"]]
         sources = [DataSource(s["dataset_id"], [DataSourceColumn(c["name"], c["property"],
                                                                  c.get("cleaner"))
                                                 for c in s["columns"]], s.get("group_no"))
@@ -261,7 +265,8 @@ def parse_duke_config(xml, linkage=None) -> DukeConfig:
             comp = objects.get(cname) or Comparator(cname, {})
         low = float(_text(pe, "low", "0.5"))
         high = float(_text(pe, "high", "0.5"))
-        props.append(Property(name, comp, low, high, is_id=typ == "id", ignore=typ == "ignore"))
+        props.append(Property(name, comp, low, high, is_id=typ == "id", ignore=typ == "ignore",
+                              lookup=(pe.get("lookup") or "default").strip().lower()))
     sources = []
     groups = root.findall("group")
     if linkage is None:

@@ -317,14 +317,28 @@ class GpuBlockingDatabase:
     IncrementalLuceneDatabase.java:516-517, 578-590).  Records marked
     dukeDeleted=true stay indexed but are never candidates (:478)."""
 
-    def __init__(self, config: DukeConfig, key_functions, mode=None, device=0):
+    def __init__(self, config: DukeConfig, key_functions=(), mode=None, device=0, lucene=None):
+        """key_functions: Duke blocking key functions (the GPU blocking contract); none ->
+        the reference's own Lucene candidate semantics (IncrementalLuceneDatabase.
+        findCandidateMatches, dukehip.lucene; `lucene` = LuceneOptions, default from the
+        environment like App.configureDatabase)."""
         self.config = config
-        self.key_functions = list(key_functions)
+        self.key_functions = list(key_functions or ())
         if mode is None:
             mode = A.MODE_LINKAGE if config.linkage else A.MODE_DEDUP
         self.mode = mode
         nkeys = 0 if mode == A.MODE_ALLPAIRS else len(self.key_functions)
         self.schema, self.props = config.to_schema(mode, nkeys)
+        self.lookup = None
+        if mode != A.MODE_ALLPAIRS and not self.key_functions:
+            from .lucene import LuceneOptions, lookup_properties
+            opts = lucene or LuceneOptions.from_env()
+            opts.check()
+            self.lookup = lookup_properties(config, self.props)
+            if not self.lookup:
+                raise ValueError("no lookup properties: the Lucene query would match nothing")
+            idx = {p.name: i for i, p in enumerate(self.props)}
+            A.lucene_source(self.schema, [idx[n] for n in self.lookup], opts.max_hits, opts.min_relevance)
         self.engine = GpuEngine(self.schema, device)
         self.pending = []
         self.rows = RowStore([p.name for p in self.props])   # row -> Record
@@ -415,7 +429,7 @@ class GpuBlockingDatabase:
         deleted = np.array([r.get_value(DELETED_PROPERTY_NAME) == "true" for r in records],
                            dtype=np.uint8)
         key_cols = None
-        if self.mode != A.MODE_ALLPAIRS:
+        if self.mode != A.MODE_ALLPAIRS and self.key_functions:
             key_cols = [A.Column.from_strings([kf.make_key(r) for r in records])
                         for kf in self.key_functions]
         rows = self.engine.upsert(n, ident, cols, group=group, deleted=deleted,

@@ -1,0 +1,160 @@
+"""GPU parity of the Lucene-compatible candidate source: the reference's own
+IncrementalLuceneDatabase.findCandidateMatches semantics on the device (postings, TF-IDF
+top-k, min-relevance), then Processor.compare over the hits in hit order -- against the
+Python restatement of the query (oracle/lucene_ref.py) and the C oracle's compare_rows.
+
+PARITY UNPINNED: Lucene and Duke are absent from /root/reference (see lucene_ref.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import lucene_ref as R
+import oracle as O
+import dukehip as dh
+from dukehip import _abi as A
+from dukehip import synth
+from test_gpu_parity import schema_of
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def expected(props, vals, lookup, ident, in_index, deleted, group, queries, thr, maybe, max_hits,
+             min_rel, mode):
+    ref = R.LuceneIndexRef([f"f{i}" for i in lookup], max_hits, min_rel, linkage=mode == "linkage")
+    ref.set_docs([vals[i] for i in lookup], in_index, deleted, group)
+    ot = O.OracleTable(props, vals, ident=ident, threshold=thr, maybe=maybe)
+    out = {"query": [], "candidate": [], "prob": [], "kind": []}
+    scored = 0
+    for q in queries:
+        for c in ref.candidates(int(q)):
+            if ident[c] == ident[q]:          # Processor.isSameAs
+                continue
+            scored += 1
+            p = ot.compare_rows(int(q), int(c))
+            kind = 1 if p > thr else (2 if maybe != 0.0 and p > maybe else 0)
+            if kind:
+                out["query"].append(int(q))
+                out["candidate"].append(int(c))
+                out["prob"].append(p)
+                out["kind"].append(kind)
+    return out, scored
+
+
+def check(res, want, scored):
+    assert res.pairs_scored == scored
+    assert list(res.query) == want["query"]
+    assert list(res.candidate) == want["candidate"]
+    assert list(res.kind) == want["kind"]
+    assert list(res.prob) == want["prob"]
+
+
+def upsert(eng, vals, ident, a, b, deleted=None, group=None, transient=False):
+    eng.upsert(b - a, ident[a:b], [dh.Column.from_strings(v[a:b]) for v in vals],
+               deleted=None if deleted is None else deleted[a:b],
+               group=None if group is None else group[a:b], transient=transient)
+
+
+PROPS = [{"comparator": A.CMP_JAROWINKLER, "low": 0.1, "high": 0.95},
+         {"comparator": A.CMP_LEVENSHTEIN, "low": 0.2, "high": 0.8},
+         {"comparator": A.CMP_LEVENSHTEIN, "low": 0.1, "high": 0.85}]
+
+
+@pytest.mark.parametrize("mode", ["dedup", "linkage"])
+@pytest.mark.parametrize("lookup,max_hits,min_rel", [([0], 10, 0.9), ([1, 2, 0], 10, 0.9),
+                                                     ([0, 1], 5, 0.3)])
+def test_lucene_candidates_equal_restatement(mode, lookup, max_hits, min_rel):
+    p = synth.persons(1200, 500, seed=61)
+    vals = [p["name"], p["address"], p["dob"]]
+    n = len(vals[0])
+    rng = np.random.default_rng(61)
+    ident = np.arange(n, dtype=np.uint64)
+    ident[1500:1580] = ident[100:180]               # re-posted IDs: delete-by-ID
+    deleted = (rng.random(n) < 0.03).astype(np.uint8)
+    group = np.where(rng.random(n) < 0.5, 1, 2).astype(np.uint8) if mode == "linkage" else None
+    sch = schema_of(PROPS, 0.9, 0.7, mode, 0)
+    A.lucene_source(sch, lookup, max_hits, min_rel)
+    eng = dh.GpuEngine(sch)
+    plan = [(0, 1000), (1000, 1500), (1500, n)]
+    for a, b in plan:
+        upsert(eng, vals, ident, a, b, deleted, group)
+        alive = np.ones(b, bool)
+        last = {}
+        for r in range(b):
+            if int(ident[r]) in last:
+                alive[last[int(ident[r])]] = False
+            last[int(ident[r])] = r
+        for q in (np.arange(a, b, dtype=np.uint32), np.arange(0, b, 7, dtype=np.uint32)):
+            res = eng.match(q)
+            want, scored = expected(PROPS, [v[:b] for v in vals], lookup, ident[:b], alive,
+                                    deleted[:b], None if group is None else group[:b], q, 0.9, 0.7,
+                                    max_hits, min_rel, mode)
+            check(res, want, scored)
+            assert res.pairs_scored > 0
+            res.close()
+    counts = eng.candidate_counts(np.arange(0, n, 11, dtype=np.uint32))
+    assert counts.max() <= max_hits
+    eng.close()
+
+
+def test_lucene_transient_queries():
+    """httptransform: query-only rows are matched against the index, never hits themselves."""
+    p = synth.persons(600, 300, seed=62)
+    vals = [p["name"], p["address"], p["dob"]]
+    n = len(vals[0])
+    ident = np.arange(n, dtype=np.uint64)
+    sch = schema_of(PROPS, 0.9, 0.7, "dedup", 0)
+    A.lucene_source(sch, [1, 2, 0], 10, 0.9)
+    eng = dh.GpuEngine(sch)
+    upsert(eng, vals, ident, 0, 700)
+    upsert(eng, vals, ident, 700, n, transient=True)
+    q = np.arange(700, n, dtype=np.uint32)
+    res = eng.match(q)
+    in_index = np.r_[np.ones(700, bool), np.zeros(n - 700, bool)]
+    want, scored = expected(PROPS, vals, [1, 2, 0], ident, in_index, np.zeros(n, np.uint8), None, q,
+                            0.9, 0.7, 10, 0.9, "dedup")
+    check(res, want, scored)
+    res.close()
+    eng.drop_transient()
+    eng.close()
+
+
+def test_reference_pipeline_on_lucene_semantics():
+    """The reference's own pipeline (testdukeconfig.xml, no key functions: the GPU runs its
+    Lucene candidate semantics, lookup property NAME) over the stress-test entities, posted in
+    batches through GpuProcessor.deduplicate -- no reconfiguration needed."""
+    from test_gpu_configs import stress_entities, alive_after, oracle_props
+    from dukehip.config import DukeConfig
+    with open(os.path.join(HERE, "golden", "testdukeconfig_schema.json")) as f:
+        cfg = DukeConfig.from_dict(json.load(f)["pipelines"]["Deduplication/countries-dbpedia-mondial"])
+    dbpedia, mondial = cfg.data_sources
+    db = dh.GpuBlockingDatabase(cfg)                # no key functions -> Lucene semantics
+    assert db.lookup == ["NAME"]
+    proc = dh.GpuProcessor(cfg, db)
+    batches = []
+    for src, seed in ((dbpedia, 1234), (mondial, 4321)):
+        ents = stress_entities(3000, seed)
+        for a in range(0, len(ents), 1000):
+            batches.append(dh.records_from_entities(ents[a:a + 1000], src))
+    allrecs, ids, results = [], {}, []
+    for recs in batches:
+        res = proc.deduplicate(recs)
+        results.append((len(allrecs), len(allrecs) + len(recs), res))
+        allrecs += recs
+    props = oracle_props(db.props)
+    vals = [[r.get_value(p.name) for r in allrecs] for p in db.props]
+    ident = np.array([ids.setdefault(r.get_value("ID"), len(ids)) for r in allrecs], np.uint64)
+    deleted = np.array([r.get_value("dukeDeleted") == "true" for r in allrecs], np.uint8)
+    lookup = [i for i, p in enumerate(db.props) if p.name == "NAME"]
+    total = 0
+    for a, e, res in results:
+        alive = alive_after(list(ident), e).astype(bool)
+        want, scored = expected(props, [v[:e] for v in vals], lookup, ident[:e], alive, deleted[:e],
+                                None, np.arange(a, e), cfg.threshold, cfg.maybe_threshold, 10, 0.9,
+                                "dedup")
+        check(res, want, scored)
+        total += res.n
+    assert total > 100
+    db.close()
