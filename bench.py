@@ -10,6 +10,9 @@ GPU configurations for measurement runs (not the headline line):
             field, --comparator lev|jw
   longtext  configs[4]: text linkage, 64-256 chars, WeightedLevenshtein + QGram q=3
             JACCARD, key = first two tokens (default 200k x 200k; published 5M x 5M)
+  reference configs[0]: the reference's own pipeline (testdukeconfig.xml, parsed into
+            tests/golden/testdukeconfig_schema.json) over 2 x 10,000 stress-test entities,
+            with its own Lucene candidate semantics (no key functions) on the GPU
 
 One step = one dk_match over every query record of this rank (candidate generation, fused
 scoring, threshold and the device-side compaction of the match list), with the index
@@ -40,7 +43,8 @@ import numpy as np  # noqa: E402
 METRIC = "candidate pairs scored/sec (node) + records/sec deduped, 1/2/4/8 MI355X"
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
 VALU_PEAK = 1024 * 2.4e9 / 2  # wave64 VALU instructions/s: 256 CUs x 4 SIMD-32, 2 cycles each
-DEFAULT_RECORDS = {"dedup": 1_000_000, "linkage": 1_000_000, "allpairs": 200_000, "longtext": 200_000}
+DEFAULT_RECORDS = {"dedup": 1_000_000, "linkage": 1_000_000, "allpairs": 200_000, "longtext": 200_000,
+                   "reference": 20_000}
 
 
 def parse():
@@ -135,6 +139,32 @@ def build_workload(args):
                  props=[prop("FIELD", op, 0.1, 0.95)], values={"FIELD": vals},
                  mode=A.MODE_ALLPAIRS, queries=np.arange(n),
                  threshold=0.85 if args.comparator == "lev" else 0.93, maybe=0.0)
+    elif args.workload == "reference":
+        import dukehip as dh
+        from dukehip.config import DukeConfig
+        from dukehip.lucene import lookup_properties
+        with open(os.path.join(ROOT, "tests", "golden", "testdukeconfig_schema.json")) as f:
+            cfg = DukeConfig.from_dict(json.load(f)["pipelines"]["Deduplication/countries-dbpedia-mondial"])
+        recs = []
+        for src, seed in zip(cfg.data_sources, (1234, 4321)):
+            recs += dh.records_from_entities(synth.stress_entities(n // 2, seed), src)
+        props = cfg.scored_properties()
+        ids = {}
+        w.update(desc=f"BASELINE configs[0]: the reference's testdukeconfig.xml dedup pipeline over "
+                      f"{len(recs)} stress-test entities, Lucene candidate semantics "
+                      "(lookup NAME, top 10, min-relevance 0.9)",
+                 props=[dict(name=p.name, **{k: getattr(p.comparator.to_c(p.low, p.high), f)
+                                             for k, f in (("comparator", "comparator"), ("low", "low"),
+                                                          ("high", "high"), ("q", "qgram_q"),
+                                                          ("formula", "qgram_formula"),
+                                                          ("tokenizer", "qgram_tokenizer"),
+                                                          ("min_ratio", "min_ratio"))})
+                        for p in props],
+                 values={p.name: [r.get_value(p.name) for r in recs] for p in props},
+                 ident=np.array([ids.setdefault(r.get_value("ID"), len(ids)) for r in recs], np.uint64),
+                 deleted=np.array([r.get_value("dukeDeleted") == "true" for r in recs], np.uint8),
+                 lucene=lookup_properties(cfg, props), mode=A.MODE_DEDUP,
+                 queries=np.arange(len(recs)), threshold=cfg.threshold, maybe=cfg.maybe_threshold)
     else:  # longtext
         texts, group = synth.long_texts(n)
         w.update(desc=f"BASELINE configs[4]: text linkage {n} x {len(group) - n}, 64-256 units, "
@@ -169,6 +199,9 @@ def make_schema(w):
                                p.get("min_ratio", 0.0))
     s = A.dk_schema(len(w["props"]), arr, w["threshold"], w["maybe"], w["mode"], w["nkeys"])
     s._keep = arr
+    if w.get("lucene"):
+        names = [p["name"] for p in w["props"]]
+        A.lucene_source(s, [names.index(x) for x in w["lucene"]], 10, 0.9)
     return s
 
 
@@ -244,7 +277,8 @@ def main():
     eng = dh.GpuEngine(make_schema(w), device=local)
     torch.cuda.synchronize()
     t_up = time.perf_counter()
-    eng.upsert(n, np.arange(n, dtype=np.uint64), cols, group=w["group"], key_columns=kcols)
+    eng.upsert(n, w.get("ident", np.arange(n, dtype=np.uint64)), cols, group=w["group"],
+               deleted=w.get("deleted"), key_columns=kcols)
     t_upsert = time.perf_counter() - t_up
     del cols, kcols
     t_index = time.time() - t0
@@ -481,7 +515,8 @@ def warm_batch(eng, w, n, queries, torch):
     cols = [synth.column(w["values"][p["name"]]) for p in w["props"]]
     kcols = [synth.column(k) for k in w["keys"]] or None
     t1 = time.perf_counter()
-    eng.upsert(n, np.arange(n, dtype=np.uint64), cols, group=w["group"], key_columns=kcols)
+    eng.upsert(n, w.get("ident", np.arange(n, dtype=np.uint64)), cols, group=w["group"],
+               deleted=w.get("deleted"), key_columns=kcols)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     res = eng.match(queries)
@@ -499,6 +534,8 @@ def cpu_baseline(w, gpu_res, args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from dukehip import _abi as A
+    if w.get("lucene"):
+        return cpu_baseline_lucene(w, gpu_res, O)
     mode = {A.MODE_DEDUP: "dedup", A.MODE_LINKAGE: "linkage", A.MODE_ALLPAIRS: "allpairs"}[w["mode"]]
     props = [{k: v for k, v in p.items() if k != "name"} for p in w["props"]]
     ot = O.OracleTable(props, [w["values"][p["name"]] for p in w["props"]], keys=w["keys"],
@@ -557,6 +594,47 @@ def cpu_baseline(w, gpu_res, args):
         # bound of the host's all-core rate, the conservative denominator for GPU/CPU)
         out["all_core_linear_bound"] = single["value"] * nproc
     return out
+
+
+def cpu_baseline_lucene(w, gpu_res, O):
+    """configs[0] on the CPU: the restated Lucene query (oracle/lucene_ref.py, pure Python)
+    for candidates, the C oracle's Processor.compare for each hit, one thread; the whole list
+    is checked against the GPU's."""
+    import lucene_ref as R
+    props = [{k: v for k, v in p.items() if k != "name"} for p in w["props"]]
+    names = [p["name"] for p in w["props"]]
+    vals = [w["values"][nm] for nm in names]
+    n = len(vals[0])
+    ident = w["ident"]
+    alive = np.zeros(n, bool)
+    last = {}
+    for r in range(n):
+        last[int(ident[r])] = r
+    alive[list(last.values())] = True
+    t0 = time.perf_counter()
+    ref = R.LuceneIndexRef(w["lucene"], 10, 0.9)
+    ref.set_docs([w["values"][f] for f in w["lucene"]], alive, w["deleted"])
+    ot = O.OracleTable(props, vals, ident=ident, threshold=w["threshold"], maybe=w["maybe"])
+    t1 = time.perf_counter()
+    q_out, c_out, p_out, k_out = [], [], [], []
+    scored = 0
+    for q in w["queries"]:
+        for c in ref.candidates(int(q)):
+            if ident[c] == ident[q]:
+                continue
+            scored += 1
+            p = ot.compare_rows(int(q), int(c))
+            kind = 1 if p > w["threshold"] else (2 if w["maybe"] != 0.0 and p > w["maybe"] else 0)
+            if kind:
+                q_out.append(int(q)); c_out.append(int(c)); p_out.append(p); k_out.append(kind)
+    el = time.perf_counter() - t1
+    gq = np.repeat(w["queries"], np.diff(gpu_res.first).astype(np.int64))
+    ok = (list(gq) == q_out and list(gpu_res.candidate) == c_out and list(gpu_res.prob) == p_out
+          and list(gpu_res.kind) == k_out)
+    return {"value": scored / el, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"all {len(w['queries'])} query records ({scored} pairs): Lucene query restated "
+                      f"in Python + C Processor.compare; index build excluded ({t1 - t0:.1f} s)",
+            "seconds": el, "matches_identical_to_gpu": bool(ok), "single_core": None}
 
 
 if __name__ == "__main__":

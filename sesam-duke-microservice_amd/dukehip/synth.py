@@ -211,6 +211,29 @@ def long_texts(n_group1, dup_frac=0.3, lo=64, hi=256, vocab=50000, seed=SEED + 4
     return out, group
 
 
+def stress_entities(n, seed):
+    """configs[0]'s input: entities shaped like the reference's stress test
+    (sesam_node_deduplication_stresstest_config.conf.json:18-71 -- country = a first name,
+    capital = a last name, area in 1..10, ids from a 1..1,000,000 pool, so IDs recur), every
+    97th one `_deleted`.  JSON-like dicts for records_from_entities / dk_pack_json."""
+    from .records import JsonNumber
+    rng = np.random.Generator(np.random.PCG64(seed))
+    first = _vocab(rng, 3000, 1, 3)
+    last = _vocab(rng, 8000, 2, 3)
+    fi = _zipf_choice(rng, len(first), 1.1, n)
+    li = _zipf_choice(rng, len(last), 1.07, n)
+    ids = rng.integers(1, 1_000_001, n)
+    area = rng.integers(1, 11, n)
+    ents = []
+    for i in range(n):
+        e = {"_id": str(int(ids[i])), "country": first[fi[i]], "capital": last[li[i]],
+             "area": JsonNumber(str(int(area[i]))), "id": str(int(ids[i]))}
+        if i % 97 == 5:
+            e["_deleted"] = True
+        ents.append(e)
+    return ents
+
+
 def keys_first_two_tokens(texts):
     """BASELINE config 5 key: the first two tokens."""
     return [[" ".join(t.split(" ")[:2]) for t in texts]]

@@ -60,21 +60,7 @@ def alive_after(ident, upto):
 # Blocking contract (stated; the reference itself uses Lucene): key = NAME[0:3].
 # ---------------------------------------------------------------------------------------
 def stress_entities(n, seed):
-    rng = np.random.Generator(np.random.PCG64(seed))
-    first = synth._vocab(rng, 3000, 1, 3)
-    last = synth._vocab(rng, 8000, 2, 3)
-    fi = synth._zipf_choice(rng, len(first), 1.1, n)
-    li = synth._zipf_choice(rng, len(last), 1.07, n)
-    ids = rng.integers(1, 1_000_001, n)
-    area = rng.integers(1, 11, n)
-    ents = []
-    for i in range(n):
-        e = {"_id": str(int(ids[i])), "country": first[fi[i]], "capital": last[li[i]],
-             "area": dh.records.JsonNumber(str(int(area[i]))), "id": str(int(ids[i]))}
-        if i % 97 == 5:
-            e["_deleted"] = True
-        ents.append(e)
-    return ents
+    return synth.stress_entities(n, seed)
 
 
 def test_reference_schema_dedup_gpu():
