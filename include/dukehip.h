@@ -311,7 +311,8 @@ int dk_interner_intern(dk_interner* ids, const dk_column* column, uint64_t n, ui
 int dk_pack_json(const dk_source* source, const char* json, uint64_t len, dk_interner* ids,
                  dk_packed** out);
 void dk_free_packed(dk_packed* packed);
-/* the record ID string of an interned id (UTF-16 code units; valid while the interner lives) */
+/* the record ID string of an interned id (UTF-16 code units; valid until the next call that
+ * interns into `ids`: copy it out before packing another batch) */
 int dk_interner_string(const dk_interner* ids, uint64_t id, const uint16_t** units, uint64_t* n);
 
 /* ---- link sink: the pipeline's LinkDatabase written in bulk from a match

@@ -15,9 +15,11 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
+#include "dk_interner.h"
 #include "dk_internal.h"
 
 using namespace dk;
@@ -50,6 +52,86 @@ static int fail(int code, const char* fmt, ...) {
       return fail(DK_E_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
                   __FILE__, __LINE__);                                               \
   } while (0)
+
+// ----------------------------------------------------------------------------------------
+// host helpers
+// ----------------------------------------------------------------------------------------
+// Record identity -> the row of its newest version (IncrementalLuceneDatabase's ID term).
+// Dense identities (interner ids, sequence numbers) index a vector; any other u64 lives in
+// a hash map.  kNoRow = absent.
+struct IdentMap {
+  static constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+  std::vector<uint32_t> dense;
+  std::unordered_map<uint64_t, uint32_t> sparse;
+  uint64_t dense_limit = 1u << 20;
+
+  // identities below the limit go dense: a table of at most 8 entries per row (+ 1M)
+  void plan(uint64_t rows) { dense_limit = std::min<uint64_t>(1ull << 28, 8 * rows + (1u << 20)); }
+  uint32_t get(uint64_t id) const {
+    if (id < dense.size() && dense[id] != kNoRow) return dense[id];
+    if (sparse.empty()) return kNoRow;
+    const auto it = sparse.find(id);
+    return it == sparse.end() ? kNoRow : it->second;
+  }
+  void set(uint64_t id, uint32_t row) {
+    if (id >= dense.size() && id < dense_limit && row != kNoRow)
+      dense.resize(std::min<uint64_t>(dense_limit, std::max<uint64_t>(id + 1, 2 * dense.size())), kNoRow);
+    if (id < dense.size()) {
+      dense[id] = row;
+      if (!sparse.empty()) sparse.erase(id);  // an entry made while the limit was lower
+    } else if (row == kNoRow) {
+      sparse.erase(id);
+    } else {
+      sparse[id] = row;
+    }
+  }
+  void clear() {
+    dense.clear();
+    sparse.clear();
+  }
+};
+
+// Runs task(i) for i < n on up to n threads (inline when `parallel` is false); returns the
+// first failing task's code in task order, with its dk_last_error message.
+template <typename F>
+static int run_tasks(int n, bool parallel, F&& task) {
+  std::vector<int> rc(n, DK_OK);
+  std::vector<std::string> msg(n);
+  auto one = [&](int i) {
+    rc[i] = task(i);
+    if (rc[i] != DK_OK) msg[i] = g_err;
+  };
+  if (!parallel || n <= 1) {
+    for (int i = 0; i < n; ++i) {
+      one(i);
+      if (rc[i] != DK_OK) return rc[i];
+    }
+    return DK_OK;
+  }
+  std::vector<std::thread> th;
+  for (int i = 1; i < n; ++i) th.emplace_back(one, i);
+  one(0);
+  for (auto& t : th) t.join();
+  for (int i = 0; i < n; ++i)
+    if (rc[i] != DK_OK) {
+      g_err = msg[i];
+      return rc[i];
+    }
+  return DK_OK;
+}
+
+// f(lo, hi) over [0, n) in `parts` contiguous ranges on their own threads
+template <typename F>
+static void parallel_ranges(uint64_t n, int parts, F&& f) {
+  if (parts <= 1 || n < 2u * (uint64_t)parts) {
+    f((uint64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 1; t < parts; ++t) th.emplace_back([&f, n, parts, t] { f(n * t / parts, n * (t + 1) / parts); });
+  f((uint64_t)0, n / parts);
+  for (auto& x : th) x.join();
+}
 
 // ----------------------------------------------------------------------------------------
 // device buffers
@@ -288,8 +370,8 @@ struct dk_ctx {
   uint64_t nrows = 0, cap = 0;
   DevBuf ident, flags, group;
   DevBuf keys[kMaxKeys];
-  std::unordered_map<uint64_t, uint32_t> ident_row;
-  std::vector<std::unordered_map<std::u16string, uint64_t>> intern;
+  IdentMap ident_row;
+  std::vector<U16Table> intern;  // key strings per key function (key style 2)
   int key_style = 0;  // 0 unset, 1 u64 keys, 2 interned strings
   // transient rows (dk_upsert_transient): the newest rows from transient_row0 on; the
   // arena fills at that point, restored by dk_drop_transient
@@ -542,9 +624,9 @@ uint64_t dk_num_rows(const dk_ctx* c) { return c ? c->nrows : 0; }
 // IncrementalLuceneDatabase.findRecordById (:170-180): the row of the live version
 int dk_row_of_ident(const dk_ctx* c, uint64_t ident, uint32_t* row) {
   if (!c || !row) return fail(DK_E_INVALID, "NULL argument");
-  const auto it = c->ident_row.find(ident);
-  if (it == c->ident_row.end()) return fail(DK_E_INVALID, "no indexed record with that ID");
-  *row = it->second;
+  const uint32_t r = c->ident_row.get(ident);
+  if (r == IdentMap::kNoRow) return fail(DK_E_INVALID, "no indexed record with that ID");
+  *row = r;
   return DK_OK;
 }
 
@@ -570,7 +652,7 @@ int dk_reset_profile(dk_ctx* c) {
 // dk_upsert: Database.index(Record) for each record of the batch + Database.commit()
 //
 // Failure atomicity: a batch is validated and packed on the host first (stage_column,
-// stage_keys), then the device buffers are grown, and only then is anything committed —
+// stage_key), then the device buffers are grown, and only then is anything committed —
 // the ID map, the tombstones of older versions and the arenas.  A rejected batch (bad
 // offsets, a value the GPU path does not hold, a bad group) leaves the index exactly as
 // it was, so a caller may hand that batch to stock Duke and keep using the ctx.  This is
@@ -606,17 +688,15 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
   S.len.resize(n);
   S.maxlen = P.maxlen;
   S.maxgrams = P.maxgrams;
-  uint64_t cur = 0;
   // values on the DP comparators are bounded by the long-value DP (query rows <= 256)
   const bool is_dp = P.cfg.comparator == DK_CMP_LEVENSHTEIN ||
                      P.cfg.comparator == DK_CMP_WEIGHTED_LEVENSHTEIN;
-  std::vector<uint16_t> u16;
-  std::vector<uint64_t> g;
   const bool is_num = P.cfg.comparator == DK_CMP_NUMERIC;
   const bool is_qg = uses_codes(P.cfg.comparator);
   const bool is_tok = P.cfg.comparator != DK_CMP_QGRAM;
-  if (is_num) { S.num.assign(n, 0.0); S.numok.assign(n, 0); }
-  if (is_qg) { S.goff.assign(n, 0); S.gcnt.assign(n, 0); }
+  // pass 1: validate, lay out (4-byte aligned values)
+  uint64_t cur = 0;
+  int maxlen = S.maxlen;
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t a = col->offsets[i], b = col->offsets[i + 1];
     if (b < a) return fail(DK_E_INVALID, "property %d: offsets not monotone at %llu", pidx,
@@ -633,26 +713,48 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
     S.off[i] = (uint32_t)cur;
     S.len[i] = present ? (uint16_t)L : kMissing;
     if (!present) continue;
-    S.maxlen = std::max<int>(S.maxlen, (int)L);
-    u16.resize(L);
-    for (uint64_t k = 0; k < L; ++k)
-      u16[k] = col->width == 1 ? ((const uint8_t*)col->units)[a + k] : ((const uint16_t*)col->units)[a + k];
-    const uint64_t padded = (L + align - 1) / align * align;
-    const size_t at = S.bytes.size();
-    S.bytes.resize(at + padded * W, 0);
-    if (W == 1) for (uint64_t k = 0; k < L; ++k) S.bytes[at + k] = (uint8_t)u16[k];
-    else memcpy(S.bytes.data() + at, u16.data(), L * 2);
-    cur += padded;
+    maxlen = std::max<int>(maxlen, (int)L);
+    cur += (L + align - 1) / align * align;
+  }
+  S.maxlen = maxlen;
+  if (P.units_used + cur >= (1ull << 32))
+    return fail(DK_E_UNSUPPORTED, "property %d: arena over 4G units", pidx);
+  S.units = cur;
+  // pass 2: the units at the arena width (row ranges in parallel for large batches)
+  S.bytes.assign(cur * W, 0);
+  const uint8_t* u8 = (const uint8_t*)col->units;
+  const uint16_t* u16 = (const uint16_t*)col->units;
+  parallel_ranges(n, n >= (1u << 16) ? 4 : 1, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i) {
+      if (S.len[i] == kMissing) continue;
+      const uint64_t a = col->offsets[i], L = S.len[i];
+      uint8_t* d = S.bytes.data() + (uint64_t)S.off[i] * W;
+      if (col->width == W) memcpy(d, (const uint8_t*)col->units + a * W, L * W);
+      else  // u8 input into a u16 arena
+        for (uint64_t k = 0; k < L; ++k) reinterpret_cast<uint16_t*>(d)[k] = u8[a + k];
+    }
+  });
+  if (!is_num && !is_qg) return DK_OK;
+  // numeric values / q-gram and token codes (per value, in row order)
+  std::vector<uint16_t> v16;
+  std::vector<uint64_t> g;
+  if (is_num) { S.num.assign(n, 0.0); S.numok.assign(n, 0); }
+  if (is_qg) { S.goff.assign(n, 0); S.gcnt.assign(n, 0); }
+  for (uint64_t i = 0; i < n; ++i) {
+    if (S.len[i] == kMissing) continue;
+    const uint64_t a = col->offsets[i], L = S.len[i];
+    v16.resize(L);
+    for (uint64_t k = 0; k < L; ++k) v16[k] = col->width == 1 ? u8[a + k] : u16[a + k];
     if (is_num) {
       double v = 0.0;
-      S.numok[i] = java_parse_double(u16.data(), L, &v) ? 1 : 0;
+      S.numok[i] = java_parse_double(v16.data(), L, &v) ? 1 : 0;
       S.num[i] = v;
     }
     if (is_qg) {
       // token ids are interned per property; an id handed out by a batch that is then
       // rejected is merely unused (ids only need to be equal <=> tokens equal)
-      if (is_tok) token_codes(u16.data(), (int)L, P.tokens, g);
-      else qgram_codes(u16.data(), (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, g);
+      if (is_tok) token_codes(v16.data(), (int)L, P.tokens, g);
+      else qgram_codes(v16.data(), (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, g);
       if (g.size() >= kMissing)
         return fail(DK_E_UNSUPPORTED, "property %d: %zu q-grams / tokens", pidx, g.size());
       S.goff[i] = (uint32_t)S.grams.size();
@@ -661,11 +763,8 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
       S.grams.insert(S.grams.end(), g.begin(), g.end());
     }
   }
-  if (P.units_used + cur >= (1ull << 32))
-    return fail(DK_E_UNSUPPORTED, "property %d: arena over 4G units", pidx);
   if (P.grams_used + S.grams.size() >= (1ull << 32))
     return fail(DK_E_UNSUPPORTED, "property %d: over 4G q-gram / token codes", pidx);
-  S.units = cur;
   return DK_OK;
 }
 
@@ -723,37 +822,48 @@ static int commit_column(dk_ctx* c, int pidx, ColStage& S, uint64_t n, uint64_t 
   return DK_OK;
 }
 
-// Key ids of the batch per key function (u64 keys as given, or key strings interned
+// Key ids of the batch for key function k (u64 keys as given, or key strings interned
 // exactly).  Interning a key of a batch that is later rejected only adds an unused id.
-static int stage_keys(dk_ctx* c, const dk_batch* b, int style, std::vector<uint64_t>& kv) {
-  const int nk = c->schema.nkeys;
+static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, std::vector<uint64_t>& kv) {
   const uint64_t n = b->n;
-  kv.resize((uint64_t)nk * n);
-  for (int k = 0; k < nk; ++k) {
-    uint64_t* dst = kv.data() + (uint64_t)k * n;
-    if (style == 1) {
-      memcpy(dst, b->keys + (uint64_t)k * n, n * 8);
-      continue;
+  uint64_t* dst = kv.data() + (uint64_t)k * n;
+  if (style == 1) {
+    memcpy(dst, b->keys + (uint64_t)k * n, n * 8);
+    return DK_OK;
+  }
+  const dk_column& kc = b->key_columns[k];
+  if (!kc.offsets || (kc.width != 1 && kc.width != 2) ||
+      (n && !kc.units && kc.offsets[n] != kc.offsets[0]))
+    return fail(DK_E_INVALID, "key function %d: bad key column", k);
+  for (uint64_t i = 0; i < n; ++i)
+    if (kc.offsets[i + 1] < kc.offsets[i])
+      return fail(DK_E_INVALID, "key function %d: offsets not monotone at %llu", k,
+                  (unsigned long long)i);
+  // the key strings as UTF-16 and their hashes (row ranges in parallel), then the ordered
+  // insert into the key function's table
+  const uint64_t base = n ? kc.offsets[0] : 0, tot = n ? kc.offsets[n] - base : 0;
+  std::vector<char16_t> wide;
+  const char16_t* units = reinterpret_cast<const char16_t*>(kc.units) + (kc.width == 2 ? base : 0);
+  std::vector<uint64_t> h(n);
+  if (kc.width == 1) wide.resize(tot);
+  const uint8_t* u8 = (const uint8_t*)kc.units + base;
+  parallel_ranges(n, n >= (1u << 16) ? 4 : 1, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i) {
+      const uint64_t a = kc.offsets[i] - base, e = kc.offsets[i + 1] - base;
+      if (kc.width == 1) {
+        for (uint64_t j = a; j < e; ++j) wide[j] = u8[j];
+        h[i] = U16Table::hash(wide.data() + a, e - a);
+      } else {
+        h[i] = U16Table::hash(units + a, e - a);
+      }
     }
-    const dk_column& kc = b->key_columns[k];
-    if (!kc.offsets || (kc.width != 1 && kc.width != 2) ||
-        (n && !kc.units && kc.offsets[n] != kc.offsets[0]))
-      return fail(DK_E_INVALID, "key function %d: bad key column", k);
-    for (uint64_t i = 0; i < n; ++i)
-      if (kc.offsets[i + 1] < kc.offsets[i])
-        return fail(DK_E_INVALID, "key function %d: offsets not monotone at %llu", k,
-                    (unsigned long long)i);
-    auto& tab = c->intern[k];
-    std::u16string str;
-    for (uint64_t i = 0; i < n; ++i) {
-      const uint64_t a = kc.offsets[i], e = kc.offsets[i + 1];
-      str.resize(e - a);
-      for (uint64_t j = a; j < e; ++j)
-        str[j - a] = kc.width == 1 ? ((const uint8_t*)kc.units)[j] : ((const uint16_t*)kc.units)[j];
-      auto it = tab.find(str);
-      if (it == tab.end()) it = tab.emplace(str, (uint64_t)tab.size()).first;
-      dst[i] = it->second;
-    }
+  });
+  if (kc.width == 1) units = wide.data();
+  auto& tab = c->intern[k];
+  tab.reserve(n, tot);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t a = kc.offsets[i] - base, e = kc.offsets[i + 1] - base;
+    dst[i] = tab.find_or_add(units + a, e - a, h[i]);
   }
   return DK_OK;
 }
@@ -864,45 +974,52 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   if (row0 + n >= (1ull << 29))
     return fail(DK_E_UNSUPPORTED, "index would exceed %u rows", 1u << 29);
 
-  // 1. validate + pack on the host (no index state changes)
+  // 1. validate + pack on the host (no index state changes): one task per property, key
+  // function and the Lucene source, on their own threads for large batches
   std::vector<ColStage> cols(c->schema.nprops);
-  for (int p = 0; p < c->schema.nprops; ++p) {
-    int rc = stage_column(c, p, &b->columns[p], n, cols[p]);
-    if (rc) return rc;
-  }
-  std::vector<uint64_t> kv;
-  if (nk > 0) {
-    int rc = stage_keys(c, b, style, kv);
-    if (rc) return rc;
-  }
+  std::vector<uint64_t> kv((uint64_t)nk * n);
   LuceneStage ls;
-  if (c->luc.on) {
-    int rc = stage_lucene(c, b, n, row0, transient, ls);
+  const int np = c->schema.nprops, ntask = np + nk + (c->luc.on ? 1 : 0);
+  {
+    int rc = run_tasks(ntask, n >= 8192, [&](int t) {
+      if (t < np) return stage_column(c, t, &b->columns[t], n, cols[t]);
+      if (t < np + nk) return stage_key(c, b, style, t - np, kv);
+      return stage_lucene(c, b, n, row0, transient, ls);
+    });
     if (rc) return rc;
   }
   // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517;
   // skipped with overwrite, :515); transient rows are neither alive (never candidates) nor
-  // entered in the ID map.  Staged: the ID map changes are applied at commit.
+  // entered in the ID map.  The ID map is updated here with an undo log, rolled back if
+  // anything below fails before the commit.
   for (uint64_t i = 0; i < n; ++i)
     if (b->ident[i] == kDeadIdent)
       return fail(DK_E_INVALID, "record %llu: identity 0x%llx is reserved", (unsigned long long)i,
                   (unsigned long long)kDeadIdent);
   std::vector<uint8_t> flags(n, 0);
   std::vector<uint32_t> dead;
-  std::unordered_map<uint64_t, uint32_t> batch_row;  // ID -> newest row of this batch
+  std::vector<std::pair<uint64_t, uint32_t>> undo;
+  c->ident_row.plan(row0 + n);
   for (uint64_t i = 0; i < n && !transient; ++i) {
     flags[i] = kAlive | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
     if (c->overwrite) continue;
-    auto bt = batch_row.find(b->ident[i]);
-    if (bt != batch_row.end()) {
-      flags[bt->second - row0] &= (uint8_t)~kAlive;
-      bt->second = (uint32_t)(row0 + i);
-      continue;
+    const uint32_t old = c->ident_row.get(b->ident[i]);
+    if (old != IdentMap::kNoRow) {
+      if (old >= row0) flags[old - row0] &= (uint8_t)~kAlive;  // an older copy in this batch
+      else dead.push_back(old);
     }
-    batch_row.emplace(b->ident[i], (uint32_t)(row0 + i));
-    auto it = c->ident_row.find(b->ident[i]);
-    if (it != c->ident_row.end()) dead.push_back(it->second);
+    undo.emplace_back(b->ident[i], old);
+    c->ident_row.set(b->ident[i], (uint32_t)(row0 + i));
   }
+  struct Rollback {
+    dk_ctx* c;
+    std::vector<std::pair<uint64_t, uint32_t>>* undo;
+    bool armed = true;
+    ~Rollback() {
+      if (!armed) return;
+      for (auto it = undo->rbegin(); it != undo->rend(); ++it) c->ident_row.set(it->first, it->second);
+    }
+  } rollback{c, &undo};
 
   // 2. device space (contents preserved; nothing logical changes on failure)
   HIPCHK(hipSetDevice(c->device));
@@ -968,7 +1085,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     L.npost += ls.pkey.size();
     L.qoff.insert(L.qoff.end(), ls.qoff.begin(), ls.qoff.end());
   }
-  for (const auto& br : batch_row) c->ident_row[br.first] = br.second;
+  rollback.armed = false;
   for (uint32_t r : dead)
     if (c->base_ok && r < c->base_rows) c->base_dead.push_back(r);
   if (nk > 0) c->key_style = style;

@@ -19,6 +19,8 @@
 // Gson parses leniently; this reader takes strict RFC 8259 JSON in UTF-8 and reports
 // anything else -- and any value a cleaner table does not cover -- as DK_E_UNSUPPORTED,
 // so the caller packs that batch on its own (Java / Python) path instead.
+#include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -26,7 +28,7 @@
 #include <memory>
 #include <new>
 #include <string>
-#include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "dk_clean_table.h"
@@ -300,11 +302,11 @@ bool py_isspace(uint32_t c) {  // Python str.isspace (str.split() / strip())
          c == 0x202F || c == 0x205F || c == 0x3000;
 }
 
-void lowercase_normalize(std::u16string& s) {
-  std::u16string out;
-  out.reserve(s.size());
+void lowercase_normalize(std::u16string& s) {  // in place: the output is never longer
+  size_t o = 0;
   bool pending = false;
-  for (char16_t c : s) {
+  for (size_t i = 0; i < s.size(); ++i) {
+    const char16_t c = s[i];
     if (c >= 0x370) fail(DK_E_UNSUPPORTED, "cleaner: character outside the native table");
     const uint16_t m = kCleanTable[c];
     if (m == 0xFFFF) fail(DK_E_UNSUPPORTED, "cleaner: character outside the native table");
@@ -314,11 +316,11 @@ void lowercase_normalize(std::u16string& s) {
       pending = true;
       continue;
     }
-    if (pending && !out.empty()) out.push_back(u' ');
+    if (pending && o) s[o++] = u' ';
     pending = false;
-    out.push_back(x);
+    s[o++] = x;
   }
-  s.swap(out);
+  s.resize(o);
 }
 
 void country_name_clean(std::u16string& s) {
@@ -337,13 +339,18 @@ void capital_clean(std::u16string& s) {
   size_t a = 0, b = s.size();
   while (a < b && py_isspace(s[a])) ++a;
   while (b > a && py_isspace(s[b - 1])) --b;
-  s = s.substr(a, b - a);
+  s.erase(b);
+  s.erase(0, a);
 }
 
 // ---- key functions: dukehip.records.PartsKey (code-point slicing, Python semantics) ----
-std::vector<uint32_t> code_points(const std::u16string& s) {
+struct KeyScratch {  // per worker, reused across records (no allocation per value)
   std::vector<uint32_t> cp;
-  cp.reserve(s.size());
+  std::vector<std::pair<size_t, size_t>> toks;
+};
+
+void code_points(const std::u16string& s, std::vector<uint32_t>& cp) {
+  cp.clear();
   for (size_t i = 0; i < s.size(); ++i) {
     const char16_t c = s[i];
     if (c >= 0xD800 && c <= 0xDBFF && i + 1 < s.size() && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
@@ -353,7 +360,6 @@ std::vector<uint32_t> code_points(const std::u16string& s) {
       cp.push_back(c);
     }
   }
-  return cp;
 }
 
 void append_cp(std::u16string& out, uint32_t c) {
@@ -378,11 +384,14 @@ void py_slice(int64_t n, int32_t start, int32_t end, int64_t* a, int64_t* b) {
   if (*b < *a) *b = *a;
 }
 
-void key_part(const std::u16string* value, const dk_key_part& kp, std::u16string& out) {
+void key_part(const std::u16string* value, const dk_key_part& kp, std::u16string& out, KeyScratch& ks) {
   if (!value) return;  // a missing value contributes ""
-  std::vector<uint32_t> cp = code_points(*value);
+  std::vector<uint32_t>& cp = ks.cp;
+  code_points(*value, cp);
+  size_t lo = 0, hi = cp.size();
   if (kp.token != INT32_MIN) {  // str.split() then toks[token]
-    std::vector<std::pair<size_t, size_t>> toks;
+    auto& toks = ks.toks;
+    toks.clear();
     size_t i = 0;
     while (i < cp.size()) {
       while (i < cp.size() && py_isspace(cp[i])) ++i;
@@ -395,154 +404,287 @@ void key_part(const std::u16string* value, const dk_key_part& kp, std::u16string
     int64_t t = kp.token;
     if (t < -nt || t >= nt) return;
     if (t < 0) t += nt;
-    cp = std::vector<uint32_t>(cp.begin() + toks[t].first, cp.begin() + toks[t].second);
+    lo = toks[t].first;
+    hi = toks[t].second;
   }
   int64_t a, b;
-  py_slice((int64_t)cp.size(), kp.start, kp.end, &a, &b);
-  for (int64_t i = a; i < b; ++i) append_cp(out, cp[i]);
+  py_slice((int64_t)(hi - lo), kp.start, kp.end, &a, &b);
+  for (int64_t i = a; i < b; ++i) append_cp(out, cp[lo + i]);
 }
 
-// ---- packed output ---------------------------------------------------------------------
-struct ColBuild {
-  std::vector<uint32_t> off{0};
-  std::u16string units;
-  std::vector<uint8_t> present;
-  bool any_missing = false;
-  void add(const std::u16string* v) {
-    if (v) units.append(*v);
-    present.push_back(v ? 1 : 0);
-    any_missing = any_missing || !v;
-    off.push_back((uint32_t)units.size());
+// ---- parallel packing ------------------------------------------------------------------
+// A batch is packed in three steps: (1) the top-level array is split into entity spans by a
+// chunk-parallel structural scan (quote parity per chunk, then bracket events outside
+// strings, then one pass over the events); (2) workers parse contiguous runs of entities
+// into slices of every column; (3) the slices are concatenated in parallel and the record
+// IDs interned in batch order.  Strict JSON only: every span goes through the Reader and
+// every gap between spans is checked, so exactly the sequential reader's inputs are taken,
+// and a failure reports the first failing entity (its error, or the split's).
+
+int pack_threads(uint64_t work, uint64_t per_thread) {
+  int t = 16;  // the GPU box's CPU share per GPU; the container's own core count if lower
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (hw && hw < (unsigned)t) t = (int)hw;
+  if (const char* e = getenv("DK_INGEST_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return std::min(v, 64);  // forced (tests exercise the merge on small batches)
   }
+  const uint64_t by_work = work / per_thread;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)t, by_work));
+}
+
+template <typename F>
+void parallel_for(int n, F&& f) {
+  std::vector<std::thread> th;
+  th.reserve(n > 1 ? n - 1 : 0);
+  for (int i = 1; i < n; ++i) th.emplace_back([&f, i] { f(i); });
+  f(0);
+  for (auto& t : th) t.join();
+}
+
+inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+// 8 bytes at a time: does the word hold a '"' or a '\\'?
+inline bool has_quote_or_bs(uint64_t w) {
+  auto zero = [](uint64_t x) { return (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull; };
+  return zero(w ^ 0x2222222222222222ull) | zero(w ^ 0x5C5C5C5C5C5C5C5Cull);
+}
+
+struct Split {
+  std::vector<std::pair<uint64_t, uint64_t>> spans;  // [first byte '{', one past '}')
+  int code = DK_OK;                                    // a structural error after the spans
+  std::string msg;
 };
 
-}  // namespace
-
-
-namespace {
-
-struct Packed {
-  dk_packed pub{};
-  std::vector<dk_column> cols, keys;
-  std::vector<std::vector<uint32_t>> offs;
-  std::vector<std::vector<uint8_t>> units8, present;
-  std::vector<std::u16string> units16;
-  std::vector<uint8_t> deleted, group;
-  std::vector<uint64_t> ident;
+struct Events {  // bracket events outside strings: pos * 4 + {0 '{', 1 '[', 2 '}', 3 ']'}
+  std::vector<uint64_t> ev;
 };
 
-void finish_column(Packed& P, ColBuild& cb, dk_column& out) {
-  P.offs.push_back(std::move(cb.off));
-  bool narrow = true;
-  for (char16_t c : cb.units)
-    if (c > 0xFF) { narrow = false; break; }
-  if (narrow) {
-    std::vector<uint8_t> u(cb.units.size() + 1, 0);
-    for (size_t i = 0; i < cb.units.size(); ++i) u[i] = (uint8_t)cb.units[i];
-    P.units8.push_back(std::move(u));
-    out.units = P.units8.back().data();
-    out.width = 1;
-  } else {
-    cb.units.push_back(0);
-    P.units16.push_back(std::move(cb.units));
-    out.units = P.units16.back().data();
-    out.width = 2;
-  }
-  out.offsets = P.offs.back().data();
-  if (cb.any_missing) {
-    P.present.push_back(std::move(cb.present));
-    out.present = P.present.back().data();
-  } else {
-    out.present = nullptr;
-  }
+// the unescaped-quote parity of [c0, c1) (the escape state at c0 from the backslash run
+// before it: valid JSON has backslashes only inside strings, where they pair up)
+bool chunk_escaped_at(const char* J, uint64_t lo, uint64_t c0) {
+  uint64_t k = 0;
+  while (c0 > lo + k && J[c0 - 1 - k] == '\\') ++k;
+  return k & 1;
 }
 
-}  // namespace
-
-extern "C" {
-
-int dk_interner_create(dk_interner** out) {
-  if (!out) return dk_fail_ingest(DK_E_INVALID, "out is NULL");
-  *out = new (std::nothrow) dk_interner();
-  return *out ? DK_OK : dk_fail_ingest(DK_E_NOMEM, "out of host memory");
-}
-
-void dk_interner_destroy(dk_interner* it) { delete it; }
-
-uint64_t dk_interner_size(const dk_interner* it) { return it ? it->ids.size() : 0; }
-
-int dk_interner_find(const dk_interner* it, const uint16_t* units, uint64_t n, uint64_t* id) {
-  if (!it || !id || (n && !units)) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
-  const auto f = it->ids.find(std::u16string(reinterpret_cast<const char16_t*>(units), n));
-  if (f == it->ids.end()) return dk_fail_ingest(DK_E_INVALID, "ID not interned");
-  *id = f->second;
-  return DK_OK;
-}
-
-int dk_interner_intern(dk_interner* it, const dk_column* col, uint64_t n, uint64_t* out) {
-  if (!it || !col || (n && (!out || !col->offsets || !col->units)))
-    return dk_fail_ingest(DK_E_INVALID, "NULL argument");
-  if (col->width != 1 && col->width != 2) return dk_fail_ingest(DK_E_INVALID, "width 1 or 2");
-  try {
-    std::u16string k;
-    for (uint64_t i = 0; i < n; ++i) {
-      if (col->present && !col->present[i]) return dk_fail_ingest(DK_E_INVALID, "missing ID");
-      const uint32_t a = col->offsets[i], b = col->offsets[i + 1];
-      k.resize(b - a);
-      for (uint32_t j = a; j < b; ++j)
-        k[j - a] = col->width == 1 ? ((const uint8_t*)col->units)[j] : ((const uint16_t*)col->units)[j];
-      const auto f = it->ids.find(k);
-      out[i] = f != it->ids.end() ? f->second : it->add(std::move(k));
+uint32_t quote_parity(const char* J, uint64_t c0, uint64_t c1, bool esc) {
+  uint32_t q = 0;
+  uint64_t i = c0;
+  while (i < c1) {
+    if (!esc && i + 8 <= c1) {
+      uint64_t w;
+      memcpy(&w, J + i, 8);
+      if (!has_quote_or_bs(w)) { i += 8; continue; }
     }
-  } catch (const std::bad_alloc&) {
-    return dk_fail_ingest(DK_E_NOMEM, "out of host memory");
+    const char ch = J[i++];
+    if (esc) { esc = false; continue; }
+    if (ch == '\\') esc = true;
+    else if (ch == '"') q ^= 1;
   }
-  return DK_OK;
+  return q;
 }
 
-int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_interner* ids,
-                 dk_packed** out) {
-  if (!src || !json || !ids || !out) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
-  *out = nullptr;
-  if (src->nprops < 0 || src->nprops > 16 || src->nkeys < 0 || src->nkeys > 8 ||
-      src->ncolumns < 0 || (src->ncolumns && !src->columns) || (src->nkeys && !src->keys) ||
-      !src->dataset_id || src->group_no < 0 || src->group_no > 2)
-    return dk_fail_ingest(DK_E_INVALID, "bad dk_source");
-  for (int c = 0; c < src->ncolumns; ++c) {
-    const dk_source_column& sc = src->columns[c];
-    if (!sc.name || sc.prop < -1 || sc.prop >= src->nprops || sc.cleaner < DK_CLEAN_NONE ||
-        sc.cleaner > DK_CLEAN_CAPITAL)
-      return dk_fail_ingest(DK_E_INVALID, "bad dk_source_column");
+void bracket_events(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr, Events& E) {
+  uint64_t i = c0;
+  while (i < c1) {
+    if (instr && !esc && i + 8 <= c1) {
+      uint64_t w;
+      memcpy(&w, J + i, 8);
+      if (!has_quote_or_bs(w)) { i += 8; continue; }
+    }
+    const char ch = J[i];
+    if (esc) {
+      esc = false;
+    } else if (ch == '\\') {
+      esc = true;
+    } else if (ch == '"') {
+      instr = !instr;
+    } else if (!instr) {
+      int code = -1;
+      if (ch == '{') code = 0;
+      else if (ch == '[') code = 1;
+      else if (ch == '}') code = 2;
+      else if (ch == ']') code = 3;
+      if (code >= 0) E.ev.push_back(i * 4 + (uint64_t)code);
+    }
+    ++i;
   }
-  try {
-    // the member names the data source reads
-    std::vector<std::string> names;
-    for (int c = 0; c < src->ncolumns; ++c) names.emplace_back(src->columns[c].name);
-    const int i_id = (int)names.size(), i_del = i_id + 1;
-    names.emplace_back("_id");
-    names.emplace_back("_deleted");
-    std::unordered_map<std::string, int> slot;
-    for (int i = (int)names.size() - 1; i >= 0; --i) slot[names[i]] = i;
+}
 
-    std::vector<ColBuild> cb(src->nprops), kb(src->nkeys);
-    ColBuild idc, eidc;
-    Packed* P = new Packed();
-    std::unique_ptr<Packed> guard(P);
-    std::u16string ds;
-    decode_string(src->dataset_id, src->dataset_id + strlen(src->dataset_id), ds);
-    std::vector<Val> got(names.size()), side;
-    std::vector<char> has(names.size());
-    std::vector<std::u16string> pv(src->nprops);
-    std::vector<char> pset(src->nprops);
-    std::u16string s, key, mname;
-    Reader R{json, json + len, &side};
-    // the batch: an array of entity objects, or one entity (App.java:955-965)
-    const bool batch = R.peek() == '[';
-    if (batch) ++R.p;
-    bool more = !batch || R.peek() != ']';
-    if (batch && !more) ++R.p;
-    uint64_t r = 0;
-    while (more) {
+// The gap before entity r (after '[' when first, else after the previous entity) up to
+// `to`: whitespace, then (not first) one ',' and whitespace.  `closing`: the gap runs into
+// the array's ']' instead of an entity.  Errors as the sequential reader raises them.
+bool gap_ok(const char* J, uint64_t from, uint64_t to, bool first, bool closing, uint64_t r, Split& S) {
+  uint64_t i = from;
+  while (i < to && is_ws(J[i])) ++i;
+  if (first) {
+    if (i == to) return true;
+    S.code = DK_E_INVALID;  // "[ 5 ..." : the element is not an object
+    S.msg = "entity " + std::to_string(r) + " is not a JSON object";
+    return false;
+  }
+  if (i == to) {
+    if (closing) return true;
+    S.code = DK_E_UNSUPPORTED;
+    S.msg = "JSON: expected ']'";
+    return false;
+  }
+  if (J[i] != ',') {
+    S.code = DK_E_UNSUPPORTED;
+    S.msg = "JSON: expected ']'";
+    return false;
+  }
+  ++i;
+  while (i < to && is_ws(J[i])) ++i;
+  if (i == to && !closing) return true;
+  S.code = DK_E_INVALID;  // after ',': something other than an object (or a trailing comma)
+  S.msg = "entity " + std::to_string(r) + " is not a JSON object";
+  return false;
+}
+
+// Entity spans of the body: an array of entities, or one entity (App.java:955-965)
+void split_entities(const char* J, uint64_t len, Split& S) {
+  uint64_t p = 0;
+  while (p < len && is_ws(J[p])) ++p;
+  if (p >= len) {
+    S.code = DK_E_UNSUPPORTED;
+    S.msg = "JSON: unexpected end of input";
+    return;
+  }
+  if (J[p] != '[') {  // one entity: the worker parses it to the end of the body
+    if (J[p] != '{') {
+      S.code = DK_E_INVALID;
+      S.msg = "entity 0 is not a JSON object";
+      return;
+    }
+    S.spans.emplace_back(p, len);
+    return;
+  }
+  const uint64_t lo = p + 1;
+  const uint64_t body = len - lo;
+  const int T = pack_threads(body, 1u << 20);
+  std::vector<uint64_t> cut(T + 1);
+  for (int t = 0; t <= T; ++t) cut[t] = lo + body * (uint64_t)t / (uint64_t)T;
+  std::vector<uint32_t> par(T);
+  std::vector<char> esc0(T);
+  parallel_for(T, [&](int t) {
+    esc0[t] = chunk_escaped_at(J, lo, cut[t]);
+    par[t] = quote_parity(J, cut[t], cut[t + 1], esc0[t]);
+  });
+  std::vector<Events> E(T);
+  std::vector<char> instr(T);
+  for (int t = 0, q = 0; t < T; ++t) {
+    instr[t] = (char)q;
+    q ^= (int)par[t];
+  }
+  parallel_for(T, [&](int t) { bracket_events(J, cut[t], cut[t + 1], esc0[t], instr[t], E[t]); });
+  // one pass over the events: depth 1 = inside the top-level array
+  int64_t depth = 1;
+  uint64_t last = lo, start = 0;
+  for (int t = 0; t < T; ++t) {
+    for (const uint64_t e : E[t].ev) {
+      const uint64_t pos = e >> 2;
+      const int code = (int)(e & 3);
+      if (code < 2) {
+        if (depth == 1) {
+          if (!gap_ok(J, last, pos, S.spans.empty(), false, S.spans.size(), S)) return;
+          if (code != 0) {
+            S.code = DK_E_INVALID;
+            S.msg = "entity " + std::to_string(S.spans.size()) + " is not a JSON object";
+            return;
+          }
+          start = pos;
+        }
+        ++depth;
+      } else {
+        --depth;
+        if (depth == 1) {
+          S.spans.emplace_back(start, pos + 1);
+          last = pos + 1;
+        } else if (depth == 0) {
+          if (code != 3) {
+            S.code = DK_E_UNSUPPORTED;
+            S.msg = "JSON: expected a value";
+            return;
+          }
+          if (!gap_ok(J, last, pos, S.spans.empty(), true, S.spans.size(), S)) return;
+          uint64_t i = pos + 1;
+          while (i < len && is_ws(J[i])) ++i;
+          if (i != len) {
+            S.code = DK_E_UNSUPPORTED;
+            S.msg = "JSON: trailing characters";
+          }
+          return;
+        }
+      }
+    }
+  }
+  S.code = DK_E_UNSUPPORTED;  // the array never closes (or a string never ends)
+  S.msg = "JSON: unexpected end of input";
+}
+
+// One worker's slice of a column: values back to back, offsets relative to the slice.
+struct ColPart {
+  std::vector<uint32_t> off{0};
+  std::vector<char16_t> u;
+  std::vector<uint8_t> present;
+  bool missing = false;
+  char16_t maxu = 0;
+  void add(const std::u16string& v) {
+    char16_t m = maxu;
+    for (char16_t c : v) m = c > m ? c : m;
+    maxu = m;
+    u.insert(u.end(), v.begin(), v.end());
+    off.push_back((uint32_t)u.size());
+    present.push_back(1);
+  }
+  void add_missing() {
+    off.push_back((uint32_t)u.size());
+    present.push_back(0);
+    missing = true;
+  }
+};
+
+struct Slice {
+  uint64_t e0 = 0, e1 = 0;      // entity range
+  std::vector<ColPart> cols;    // nprops, then nkeys, then the record ID, then the entity id
+  std::vector<uint8_t> deleted;
+  std::vector<uint64_t> hash;   // record-ID hashes (U16Table::hash)
+  int code = DK_OK;
+  uint64_t fail_at = 0;
+  std::string msg;
+};
+
+struct SourceView {
+  const dk_source* src;
+  std::vector<std::string> names;  // data-source columns, then "_id", "_deleted"
+  int i_id, i_del;
+  std::u16string ds;
+};
+
+// IncrementalDataSource.DatasetDataSourceRecordIterator.next for entities [e0, e1)
+void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out) {
+  const dk_source* src = V.src;
+  const int np = src->nprops, nk = src->nkeys;
+  out.cols.assign(np + nk + 2, ColPart());
+  const uint64_t n = out.e1 - out.e0;
+  for (auto& c : out.cols) {
+    c.off.reserve(n + 1);
+    c.present.reserve(n);
+  }
+  out.deleted.reserve(n);
+  out.hash.reserve(n);
+  std::vector<Val> got(V.names.size()), side;
+  std::vector<char> has(V.names.size());
+  std::vector<std::u16string> pv(np);
+  std::vector<char> pset(np);
+  std::u16string s, key, mname, eid, rid;
+  KeyScratch ks;
+  uint64_t r = out.e0;
+  try {
+    for (; r < out.e1; ++r) {
+      Reader R{J + S.spans[r].first, J + S.spans[r].second, &side};
       // one entity: its members in one pass (a repeated name: the last wins, as Gson's
       // JsonObject keeps it); nested containers are skipped
       side.clear();
@@ -559,30 +701,37 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
           R.expect(':');
           Val v;
           R.value(v, 2);
-          // member names compared after unescaping only when they hold an escape
-          std::string nm(ka, kb2);
-          if (nm.find('\\') != std::string::npos) {
+          // the member names read are ASCII; compared after unescaping only when escaped
+          const char* na = ka;
+          size_t nn = (size_t)(kb2 - ka);
+          std::string esc_name;
+          if (memchr(ka, '\\', nn)) {
             mname.clear();
             decode_string(ka, kb2, mname);
-            nm.clear();
             for (char16_t c : mname) {
-              if (c > 0x7F) { nm = "\x01"; break; }  // not one of the (ASCII) names read
-              nm.push_back((char)c);
+              if (c > 0x7F) { esc_name = "\x01"; break; }  // not one of the names read
+              esc_name.push_back((char)c);
             }
+            na = esc_name.data();
+            nn = esc_name.size();
           }
-          const auto f = slot.find(nm);
-          if (f != slot.end()) {
-            got[f->second] = v;
-            has[f->second] = 1;
+          for (size_t i = 0; i < V.names.size(); ++i) {  // the first column of that name
+            if (V.names[i].size() == nn && memcmp(V.names[i].data(), na, nn) == 0) {
+              got[i] = v;
+              has[i] = 1;
+              break;
+            }
           }
           if (R.peek() == ',') { ++R.p; continue; }
           R.expect('}');
           break;
         }
       }
+      R.ws();
+      if (R.p != R.e) fail(DK_E_UNSUPPORTED, "JSON: trailing characters");
       // entity id (IncrementalDataSource.java:54-61)
-      std::u16string eid;
-      if (has[i_id]) as_string(got[i_id], side, eid, "_id");
+      eid.clear();
+      if (has[V.i_id]) as_string(got[V.i_id], side, eid, "_id");
       if (eid.empty()) fail(DK_E_INVALID, "Got an entity with no '_id' attribute!");
       // columns in data-source order, RecordBuilder.addValue: clean, skip empty
       std::fill(pset.begin(), pset.end(), 0);
@@ -608,51 +757,242 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
           pset[sc.prop] = 1;
         }
       }
-      for (int p = 0; p < src->nprops; ++p) cb[p].add(pset[p] ? &pv[p] : nullptr);
+      for (int p = 0; p < np; ++p) {
+        if (pset[p]) out.cols[p].add(pv[p]);
+        else out.cols[p].add_missing();
+      }
       // key functions over the cleaned values
-      for (int k = 0; k < src->nkeys; ++k) {
+      for (int k = 0; k < nk; ++k) {
         key.clear();
         const dk_key_function& kf = src->keys[k];
         for (int i = 0; i < kf.nparts; ++i) {
           const dk_key_part& kp = kf.parts[i];
-          if (kp.prop < 0 || kp.prop >= src->nprops) fail(DK_E_INVALID, "key part property out of range");
-          key_part(pset[kp.prop] ? &pv[kp.prop] : nullptr, kp, key);
+          if (kp.prop < 0 || kp.prop >= np) fail(DK_E_INVALID, "key part property out of range");
+          key_part(pset[kp.prop] ? &pv[kp.prop] : nullptr, kp, key, ks);
         }
-        kb[k].add(&key);
+        out.cols[np + k].add(key);
       }
       // synthetic properties (IncrementalDataSource.java:76-98)
-      std::u16string rid;
+      rid.clear();
       if (src->group_no) {
         rid.push_back((char16_t)(u'0' + src->group_no));
         rid += u"__";
       }
-      rid += ds;
+      rid += V.ds;
       rid += u"__";
       rid += eid;
-      idc.add(&rid);
-      eidc.add(&eid);
-      P->deleted.push_back(has[i_del] && as_boolean(got[i_del], side) ? 1 : 0);
-      if (src->group_no) P->group.push_back((uint8_t)src->group_no);
-      const auto f = ids->ids.find(rid);
-      P->ident.push_back(f != ids->ids.end() ? f->second : ids->add(std::move(rid)));
-      ++r;
-      if (!batch) break;
-      if (R.peek() == ',') {
-        ++R.p;
-      } else {
-        R.expect(']');
-        more = false;
-      }
+      out.cols[np + nk].add(rid);
+      out.cols[np + nk + 1].add(eid);
+      out.hash.push_back(U16Table::hash(rid.data(), rid.size()));
+      out.deleted.push_back(has[V.i_del] && as_boolean(got[V.i_del], side) ? 1 : 0);
     }
-    R.ws();
-    if (R.p != R.e) fail(DK_E_UNSUPPORTED, "JSON: trailing characters");
-    const uint64_t n = r;
-    P->cols.resize(src->nprops);
-    P->keys.resize(src->nkeys);
-    for (int p = 0; p < src->nprops; ++p) finish_column(*P, cb[p], P->cols[p]);
-    for (int k = 0; k < src->nkeys; ++k) finish_column(*P, kb[k], P->keys[k]);
-    finish_column(*P, idc, P->pub.id);
-    finish_column(*P, eidc, P->pub.entity_id);
+  } catch (const Fail& f) {
+    out.code = f.code;
+    out.msg = f.msg;
+    out.fail_at = r;
+  } catch (const std::bad_alloc&) {
+    out.code = DK_E_NOMEM;
+    out.msg = "out of host memory";
+    out.fail_at = r;
+  }
+}
+
+// A packed column (owned by Packed)
+struct FinalCol {
+  std::vector<uint32_t> off;
+  std::vector<uint8_t> u8;
+  std::vector<uint16_t> u16;
+  std::vector<uint8_t> present;
+};
+
+struct Packed {
+  dk_packed pub{};
+  std::vector<dk_column> cols, keys;
+  std::vector<FinalCol> store;  // sized once: the dk_column pointers stay valid
+  std::vector<uint8_t> deleted, group;
+  std::vector<uint64_t> ident;
+};
+
+// slices -> packed columns: sizes and widths first, then one parallel pass in which each
+// worker copies its slice of every column into place
+struct ColPlan {
+  std::vector<uint64_t> ubase;  // per slice: first unit
+  bool missing = false, narrow = true;
+};
+
+void merge_columns(std::vector<Slice>& sl, uint64_t n, std::vector<FinalCol>& F, std::vector<dk_column*>& out) {
+  const int T = (int)sl.size(), NC = (int)F.size();
+  std::vector<ColPlan> plan(NC);
+  for (int c = 0; c < NC; ++c) {
+    ColPlan& L = plan[c];
+    L.ubase.assign(T + 1, 0);
+    char16_t maxu = 0;
+    for (int t = 0; t < T; ++t) {
+      const ColPart& P = sl[t].cols[c];
+      L.ubase[t + 1] = L.ubase[t] + P.u.size();
+      L.missing = L.missing || P.missing;
+      maxu = std::max(maxu, P.maxu);
+    }
+    if (L.ubase[T] >= (1ull << 32)) fail(DK_E_UNSUPPORTED, "a column of over 4G units in one batch");
+    L.narrow = maxu <= 0xFF;
+    F[c].off.resize(n + 1);
+    F[c].off[0] = 0;
+    if (L.narrow) F[c].u8.resize(L.ubase[T] + 1);
+    else F[c].u16.resize(L.ubase[T] + 1);
+    if (L.missing) F[c].present.resize(n);
+  }
+  parallel_for(T, [&](int t) {
+    const uint64_t r0 = sl[t].e0, m = sl[t].e1 - sl[t].e0;
+    for (int c = 0; c < NC; ++c) {
+      const ColPart& P = sl[t].cols[c];
+      const ColPlan& L = plan[c];
+      const uint32_t b = (uint32_t)L.ubase[t];
+      uint32_t* o = F[c].off.data() + r0 + 1;
+      for (uint64_t i = 0; i < m; ++i) o[i] = P.off[i + 1] + b;
+      const size_t nu = P.u.size();
+      if (L.narrow) {
+        uint8_t* d = F[c].u8.data() + L.ubase[t];
+        const char16_t* u = P.u.data();
+        for (size_t i = 0; i < nu; ++i) d[i] = (uint8_t)u[i];
+        if (t == T - 1) F[c].u8[L.ubase[T]] = 0;
+      } else {
+        if (nu) memcpy(F[c].u16.data() + L.ubase[t], P.u.data(), nu * 2);
+        if (t == T - 1) F[c].u16[L.ubase[T]] = 0;
+      }
+      if (L.missing && m) memcpy(F[c].present.data() + r0, P.present.data(), m);
+    }
+  });
+  for (int c = 0; c < NC; ++c) {
+    out[c]->offsets = F[c].off.data();
+    out[c]->units = plan[c].narrow ? (const void*)F[c].u8.data() : (const void*)F[c].u16.data();
+    out[c]->width = plan[c].narrow ? 1 : 2;
+    out[c]->present = plan[c].missing ? F[c].present.data() : nullptr;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int dk_interner_create(dk_interner** out) {
+  if (!out) return dk_fail_ingest(DK_E_INVALID, "out is NULL");
+  *out = new (std::nothrow) dk_interner();
+  return *out ? DK_OK : dk_fail_ingest(DK_E_NOMEM, "out of host memory");
+}
+
+void dk_interner_destroy(dk_interner* it) { delete it; }
+
+uint64_t dk_interner_size(const dk_interner* it) { return it ? it->size() : 0; }
+
+int dk_interner_find(const dk_interner* it, const uint16_t* units, uint64_t n, uint64_t* id) {
+  if (!it || !id || (n && !units)) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
+  if (!it->find(reinterpret_cast<const char16_t*>(units), n, id))
+    return dk_fail_ingest(DK_E_INVALID, "ID not interned");
+  return DK_OK;
+}
+
+int dk_interner_intern(dk_interner* it, const dk_column* col, uint64_t n, uint64_t* out) {
+  if (!it || !col || (n && (!out || !col->offsets || !col->units)))
+    return dk_fail_ingest(DK_E_INVALID, "NULL argument");
+  if (col->width != 1 && col->width != 2) return dk_fail_ingest(DK_E_INVALID, "width 1 or 2");
+  for (uint64_t i = 0; i < n; ++i) {
+    if (col->present && !col->present[i]) return dk_fail_ingest(DK_E_INVALID, "missing ID");
+    if (col->offsets[i + 1] < col->offsets[i]) return dk_fail_ingest(DK_E_INVALID, "offsets not monotone");
+  }
+  try {
+    it->reserve(n, n ? col->offsets[n] - col->offsets[0] : 0);
+    std::u16string k;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint32_t a = col->offsets[i], b = col->offsets[i + 1];
+      k.resize(b - a);
+      for (uint32_t j = a; j < b; ++j)
+        k[j - a] = col->width == 1 ? ((const uint8_t*)col->units)[j] : ((const uint16_t*)col->units)[j];
+      out[i] = it->find_or_add(k.data(), k.size());
+    }
+  } catch (const std::bad_alloc&) {
+    return dk_fail_ingest(DK_E_NOMEM, "out of host memory");
+  }
+  return DK_OK;
+}
+
+int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_interner* ids,
+                 dk_packed** out) {
+  if (!src || !json || !ids || !out) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
+  *out = nullptr;
+  if (src->nprops < 0 || src->nprops > 16 || src->nkeys < 0 || src->nkeys > 8 ||
+      src->ncolumns < 0 || (src->ncolumns && !src->columns) || (src->nkeys && !src->keys) ||
+      !src->dataset_id || src->group_no < 0 || src->group_no > 2)
+    return dk_fail_ingest(DK_E_INVALID, "bad dk_source");
+  for (int c = 0; c < src->ncolumns; ++c) {
+    const dk_source_column& sc = src->columns[c];
+    if (!sc.name || sc.prop < -1 || sc.prop >= src->nprops || sc.cleaner < DK_CLEAN_NONE ||
+        sc.cleaner > DK_CLEAN_CAPITAL)
+      return dk_fail_ingest(DK_E_INVALID, "bad dk_source_column");
+  }
+  try {
+    SourceView V;
+    V.src = src;
+    for (int c = 0; c < src->ncolumns; ++c) V.names.emplace_back(src->columns[c].name);
+    V.i_id = (int)V.names.size();
+    V.i_del = V.i_id + 1;
+    V.names.emplace_back("_id");
+    V.names.emplace_back("_deleted");
+    decode_string(src->dataset_id, src->dataset_id + strlen(src->dataset_id), V.ds);
+
+    auto T0 = std::chrono::steady_clock::now();
+    static const bool timing = getenv("DK_INGEST_TIMING") != nullptr;  // phase times to stderr
+    auto lap = [&](const char* w) {
+      if (!timing) return;
+      const auto t1 = std::chrono::steady_clock::now();
+      fprintf(stderr, "dk_pack_json %s %.2f ms\n", w, std::chrono::duration<double, std::milli>(t1 - T0).count());
+      T0 = t1;
+    };
+    // 1. entity spans
+    Split S;
+    split_entities(json, len, S);
+    const uint64_t n = S.spans.size();
+    lap("split");
+    // 2. entity slices, parsed in parallel
+    const int T = pack_threads(n, 4096);
+    std::vector<Slice> sl(T);
+    for (int t = 0; t < T; ++t) {
+      sl[t].e0 = n * (uint64_t)t / (uint64_t)T;
+      sl[t].e1 = n * (uint64_t)(t + 1) / (uint64_t)T;
+    }
+    parallel_for(T, [&](int t) { parse_slice(V, json, S, sl[t]); });
+    lap("parse");
+    for (const Slice& x : sl)  // the first failing entity, else the split's own error
+      if (x.code != DK_OK) return dk_fail_ingest(x.code, x.msg.c_str());
+    if (S.code != DK_OK) return dk_fail_ingest(S.code, S.msg.c_str());
+    // 3. concatenated columns, interned record IDs
+    Packed* P = new Packed();
+    std::unique_ptr<Packed> guard(P);
+    const int np = src->nprops, nk = src->nkeys;
+    P->store.resize(np + nk + 2);
+    P->cols.resize(np);
+    P->keys.resize(nk);
+    std::vector<dk_column*> dst;
+    for (int p = 0; p < np; ++p) dst.push_back(&P->cols[p]);
+    for (int k = 0; k < nk; ++k) dst.push_back(&P->keys[k]);
+    dst.push_back(&P->pub.id);
+    dst.push_back(&P->pub.entity_id);
+    merge_columns(sl, n, P->store, dst);
+    P->deleted.resize(n);
+    for (const Slice& x : sl)
+      if (!x.deleted.empty()) memcpy(P->deleted.data() + x.e0, x.deleted.data(), x.deleted.size());
+    if (src->group_no) P->group.assign(n, (uint8_t)src->group_no);
+    lap("merge");
+    // record IDs in batch order: new ids are dense in first-appearance order
+    P->ident.resize(n);
+    uint64_t rid_units = 0;
+    for (const Slice& x : sl) rid_units += x.cols[np + nk].u.size();
+    ids->reserve(n, rid_units);
+    for (const Slice& x : sl) {
+      const ColPart& C = x.cols[np + nk];
+      for (uint64_t i = 0; i < x.e1 - x.e0; ++i)
+        P->ident[x.e0 + i] = ids->find_or_add(C.u.data() + C.off[i], C.off[i + 1] - C.off[i], x.hash[i]);
+    }
+    lap("intern");
     P->pub.n = n;
     P->pub.columns = P->cols.data();
     P->pub.key_columns = P->keys.data();

@@ -59,7 +59,7 @@ struct dk_linkdb {
 
   // Link's ID order: String.compareTo of the two record IDs (UTF-16 code units)
   std::pair<uint64_t, uint64_t> key(uint64_t a, uint64_t b) const {
-    return *ids->strs[a] <= *ids->strs[b] ? std::make_pair(a, b) : std::make_pair(b, a);
+    return ids->compare(a, b) <= 0 ? std::make_pair(a, b) : std::make_pair(b, a);
   }
 
   // SinceAwareInMemoryLinkDatabase.assertLink, then InMemoryLinkDatabase.assertLink
@@ -87,9 +87,9 @@ extern "C" {
 
 int dk_interner_string(const dk_interner* it, uint64_t id, const uint16_t** units, uint64_t* n) {
   if (!it || !units || !n) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
-  if (id >= it->strs.size()) return dk_fail_ingest(DK_E_INVALID, "id not interned");
-  *units = reinterpret_cast<const uint16_t*>(it->strs[id]->data());
-  *n = it->strs[id]->size();
+  if (id >= it->size()) return dk_fail_ingest(DK_E_INVALID, "id not interned");
+  *units = reinterpret_cast<const uint16_t*>(it->str(id));
+  *n = it->len(id);
   return DK_OK;
 }
 
@@ -111,7 +111,7 @@ int dk_linkdb_apply(dk_linkdb* db, const dk_link_batch* b, int64_t timestamp, dk
   const uint64_t nq = b->nqueries;
   const uint64_t ne = nq ? b->first[nq] : 0;
   if (ne && (!b->candidate_ident || !b->prob || !b->kind)) return dk_fail_ingest(DK_E_INVALID, "NULL arrays");
-  const uint64_t nid = db->ids->strs.size();
+  const uint64_t nid = db->ids->size();
   for (uint64_t i = 0; i < nq; ++i) {
     if (b->first[i] > b->first[i + 1]) return dk_fail_ingest(DK_E_INVALID, "first[] not monotone");
     if (b->query_ident[i] >= nid) return dk_fail_ingest(DK_E_INVALID, "query ident not interned");
