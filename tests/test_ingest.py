@@ -160,3 +160,67 @@ def test_second_value_for_a_property_declines():
         ns.pack('[{"_id": "1", "a": "x", "b": "y"}]', I.Interner())
     pk = ns.pack('[{"_id": "1", "a": "x", "b": ""}]', I.Interner())   # empty: skipped
     assert pk.values(0) == ["x"]
+
+
+def tricky_entities(rng, n):
+    """Values full of JSON structure characters (brackets, quotes, backslashes) and ignored
+    members holding nested containers: the chunk-parallel split must see them as data."""
+    alpha = list('ab {}[]",\\:') + ["\\u005d", "é", "\U0001F600"]
+    ents = []
+    for i in range(n):
+        e = {"_id": str(i) + rng.choice(["", "{", "]", '"', "\\"]),
+             "raw": "".join(rng.choice(alpha) for _ in range(rng.randint(0, 12))),
+             "nested": {"x": [1, {"y": "]}"}], "z": "[{"} if rng.random() < 0.5 else ["}", "]"]}
+        if rng.random() < 0.7:
+            e["area"] = rng.choice([[3], rng.randint(0, 9), "4"])
+        ents.append(e)
+    return ents
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_pack_json_parallel_split_matches_python_path(threads, monkeypatch):
+    monkeypatch.setenv("DK_INGEST_THREADS", str(threads))
+    rng = random.Random(100 + threads)
+    src = source()
+    ns = I.NativeSource(src, PROPS, KEYS)
+    body = json.dumps(tricky_entities(rng, 400), ensure_ascii=threads == 3)
+    # odd whitespace between entities and around the array
+    body = "\n [ " + body[1:-1].replace("}, {", "} ,\n\t{") + " ] \n"
+    recs, vals, keys = reference(body, src)
+    pk = ns.pack(body, I.Interner())
+    assert pk.n == len(recs)
+    for p in range(len(PROPS)):
+        assert pk.values(p) == vals[p], PROPS[p]
+    for k in range(len(KEYS)):
+        assert pk.keys(k) == keys[k]
+    assert pk.ids() == [r.get_value("ID") for r in recs]
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+@pytest.mark.parametrize("body,code", [
+    ('[{"_id": "1"}, {"_id": "2"},]', A.DK_E_INVALID),      # trailing comma: not an object
+    ('[{"_id": "1"} {"_id": "2"}]', A.DK_E_UNSUPPORTED),    # missing comma
+    ('[{"_id": "1"}, {"_id": "2"]', A.DK_E_UNSUPPORTED),    # mismatched bracket
+    ('[{"_id": "1"}, {"_id": "2}]', A.DK_E_UNSUPPORTED),    # unterminated string
+    ('[{"_id": "1"}, 7, {"_id": "3"}]', A.DK_E_INVALID),    # a non-object element
+    ('[{"_id": "1"}, {"name": "x"}, {"_id": "3"', A.DK_E_INVALID),  # entity 1 fails first
+    ('[{"_id": "1"}] x', A.DK_E_UNSUPPORTED),              # trailing characters
+    ('  ', A.DK_E_UNSUPPORTED),
+    ('5', A.DK_E_INVALID),
+])
+def test_pack_json_errors_parallel(body, code, threads, monkeypatch):
+    monkeypatch.setenv("DK_INGEST_THREADS", str(threads))
+    ns = I.NativeSource(source(), PROPS, KEYS)
+    if code == A.DK_E_UNSUPPORTED:   # declined: the caller's own packing path takes it
+        with pytest.raises(I.NativeUnsupported):
+            ns.pack(body, I.Interner())
+        return
+    with pytest.raises(A.DukeHipError) as e:
+        ns.pack(body, I.Interner())
+    assert e.value.code == code
+
+
+def test_pack_json_empty_array():
+    ns = I.NativeSource(source(), PROPS, KEYS)
+    pk = ns.pack(" [ \n ] ", I.Interner())
+    assert pk.n == 0
