@@ -572,7 +572,7 @@ def warm_batch(eng, w, n, queries, torch):
                       deleted=w.get("deleted"), key_columns=kcols)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    res = eng.match(rows[queries])   # the re-posted records' new rows
+    res = eng.match(rows[queries], on_device=True)   # the re-posted records' new rows
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     res.close()

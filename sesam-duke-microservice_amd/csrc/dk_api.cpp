@@ -860,11 +860,14 @@ static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, std::vector
   });
   if (kc.width == 1) units = wide.data();
   auto& tab = c->intern[k];
-  tab.reserve(n, tot);
+  if (tab.size() + n >= (1ull << 31)) return fail(DK_E_UNSUPPORTED, "key function %d: over 2^31 keys", k);
+  std::vector<const char16_t*> ptr(n);
+  std::vector<uint32_t> ln(n);
   for (uint64_t i = 0; i < n; ++i) {
-    const uint64_t a = kc.offsets[i] - base, e = kc.offsets[i + 1] - base;
-    dst[i] = tab.find_or_add(units + a, e - a, h[i]);
+    ptr[i] = units + (kc.offsets[i] - base);
+    ln[i] = kc.offsets[i + 1] - kc.offsets[i];
   }
+  tab.intern_batch(n, ptr.data(), ln.data(), h.data(), dst, n >= (1u << 16) ? 4 : 1);
   return DK_OK;
 }
 

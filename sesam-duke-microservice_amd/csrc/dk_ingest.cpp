@@ -456,10 +456,6 @@ struct Split {
   std::string msg;
 };
 
-struct Events {  // bracket events outside strings: pos * 4 + {0 '{', 1 '[', 2 '}', 3 ']'}
-  std::vector<uint64_t> ev;
-};
-
 // the unescaped-quote parity of [c0, c1) (the escape state at c0 from the backslash run
 // before it: valid JSON has backslashes only inside strings, where they pair up)
 bool chunk_escaped_at(const char* J, uint64_t lo, uint64_t c0) {
@@ -485,7 +481,10 @@ uint32_t quote_parity(const char* J, uint64_t c0, uint64_t c1, bool esc) {
   return q;
 }
 
-void bracket_events(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr, Events& E) {
+// Brackets outside strings in [c0, c1): f(pos, ch) for each of '{' '[' '}' ']'; f returns
+// false to stop the scan.
+template <typename F>
+void for_brackets(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr, F&& f) {
   uint64_t i = c0;
   while (i < c1) {
     if (instr && !esc && i + 8 <= c1) {
@@ -500,50 +499,100 @@ void bracket_events(const char* J, uint64_t c0, uint64_t c1, bool esc, bool inst
       esc = true;
     } else if (ch == '"') {
       instr = !instr;
-    } else if (!instr) {
-      int code = -1;
-      if (ch == '{') code = 0;
-      else if (ch == '[') code = 1;
-      else if (ch == '}') code = 2;
-      else if (ch == ']') code = 3;
-      if (code >= 0) E.ev.push_back(i * 4 + (uint64_t)code);
+    } else if (!instr && (ch == '{' || ch == '[' || ch == '}' || ch == ']')) {
+      if (!f(i, ch)) return;
     }
     ++i;
   }
 }
 
-// The gap before entity r (after '[' when first, else after the previous entity) up to
-// `to`: whitespace, then (not first) one ',' and whitespace.  `closing`: the gap runs into
-// the array's ']' instead of an entity.  Errors as the sequential reader raises them.
-bool gap_ok(const char* J, uint64_t from, uint64_t to, bool first, bool closing, uint64_t r, Split& S) {
-  uint64_t i = from;
-  while (i < to && is_ws(J[i])) ++i;
-  if (first) {
-    if (i == to) return true;
-    S.code = DK_E_INVALID;  // "[ 5 ..." : the element is not an object
-    S.msg = "entity " + std::to_string(r) + " is not a JSON object";
-    return false;
-  }
-  if (i == to) {
-    if (closing) return true;
-    S.code = DK_E_UNSUPPORTED;
-    S.msg = "JSON: expected ']'";
-    return false;
-  }
-  if (J[i] != ',') {
-    S.code = DK_E_UNSUPPORTED;
-    S.msg = "JSON: expected ']'";
-    return false;
-  }
-  ++i;
-  while (i < to && is_ws(J[i])) ++i;
-  if (i == to && !closing) return true;
-  S.code = DK_E_INVALID;  // after ',': something other than an object (or a trailing comma)
-  S.msg = "entity " + std::to_string(r) + " is not a JSON object";
-  return false;
+// One chunk of the top-level array, its depth at the start known: entity starts ('{' at
+// depth 1) and ends (one past the '}' back to depth 1), the array's closing ']', or the
+// first bracket that cannot be there.
+struct ChunkScan {
+  std::vector<uint64_t> starts, ends;
+  uint64_t close = UINT64_MAX;  // the top-level ']'
+  uint64_t bad = UINT64_MAX;    // a non-object element's '[' or a stray closer
+};
+
+void scan_chunk(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr, int64_t depth, ChunkScan& C) {
+  for_brackets(J, c0, c1, esc, instr, [&](uint64_t pos, char ch) {
+    if (ch == '{' || ch == '[') {
+      if (depth == 1) {
+        if (ch != '{') { C.bad = pos; return false; }
+        C.starts.push_back(pos);
+      }
+      ++depth;
+      return true;
+    }
+    --depth;
+    if (depth == 1) {
+      C.ends.push_back(pos + 1);
+    } else if (depth == 0) {
+      if (ch == ']') C.close = pos;
+      else C.bad = pos;
+      return false;
+    } else if (depth < 0) {
+      C.bad = pos;
+      return false;
+    }
+    return true;
+  });
 }
 
-// Entity spans of the body: an array of entities, or one entity (App.java:955-965)
+// The text between two elements of the top-level array: whitespace only, one ',' in
+// whitespace, a ',' followed by something else, or something else.
+enum Gap { kEmpty, kComma, kCommaOther, kOther };
+
+Gap classify_gap(const char* J, uint64_t from, uint64_t to) {
+  uint64_t i = from;
+  while (i < to && is_ws(J[i])) ++i;
+  if (i == to) return kEmpty;
+  if (J[i] != ',') return kOther;
+  ++i;
+  while (i < to && is_ws(J[i])) ++i;
+  return i == to ? kComma : kCommaOther;
+}
+
+// What follows the gap before element r: an entity '{', the array's ']', a misplaced
+// bracket, or the end of the body.  True when well formed; otherwise S gets the error the
+// sequential reader raises there (Reader.peek / expect, "entity r is not a JSON object").
+enum Next { kEntity, kClose, kBad, kEnd };
+
+bool element_check(Gap g, uint64_t r, Next nx, Split& S) {
+  auto invalid = [&] {
+    S.code = DK_E_INVALID;
+    S.msg = "entity " + std::to_string(r) + " is not a JSON object";
+    return false;
+  };
+  auto unsup = [&](const char* m) {
+    S.code = DK_E_UNSUPPORTED;
+    S.msg = m;
+    return false;
+  };
+  if (r == 0) {  // right after '['
+    if (g != kEmpty) return invalid();
+    if (nx == kEntity || nx == kClose) return true;
+    return nx == kEnd ? unsup("JSON: unexpected end of input") : invalid();
+  }
+  switch (g) {  // after entity r - 1
+    case kEmpty:
+      if (nx == kClose) return true;
+      return unsup(nx == kEnd ? "JSON: unexpected end of input" : "JSON: expected ']'");
+    case kComma:
+      if (nx == kEntity) return true;
+      return nx == kEnd ? unsup("JSON: unexpected end of input") : invalid();
+    case kCommaOther:
+      return invalid();
+    default:
+      return unsup("JSON: expected ']'");
+  }
+}
+
+// Entity spans of the body: an array of entities, or one entity (App.java:955-965).  Four
+// passes over chunks of the array on pack_threads() threads: unescaped-quote parity (so
+// each chunk knows whether it starts inside a string), bracket depth change, then the
+// entity starts / ends at the chunk's now known depth; the gaps between entities last.
 void split_entities(const char* J, uint64_t len, Split& S) {
   uint64_t p = 0;
   while (p < len && is_ws(J[p])) ++p;
@@ -567,61 +616,82 @@ void split_entities(const char* J, uint64_t len, Split& S) {
   std::vector<uint64_t> cut(T + 1);
   for (int t = 0; t <= T; ++t) cut[t] = lo + body * (uint64_t)t / (uint64_t)T;
   std::vector<uint32_t> par(T);
-  std::vector<char> esc0(T);
+  std::vector<char> esc0(T), instr(T);
+  std::vector<int64_t> delta(T), d0(T);
+  std::vector<ChunkScan> CS(T);
   parallel_for(T, [&](int t) {
     esc0[t] = chunk_escaped_at(J, lo, cut[t]);
     par[t] = quote_parity(J, cut[t], cut[t + 1], esc0[t]);
   });
-  std::vector<Events> E(T);
-  std::vector<char> instr(T);
   for (int t = 0, q = 0; t < T; ++t) {
     instr[t] = (char)q;
     q ^= (int)par[t];
   }
-  parallel_for(T, [&](int t) { bracket_events(J, cut[t], cut[t + 1], esc0[t], instr[t], E[t]); });
-  // one pass over the events: depth 1 = inside the top-level array
-  int64_t depth = 1;
-  uint64_t last = lo, start = 0;
+  parallel_for(T, [&](int t) {
+    int64_t d = 0;
+    for_brackets(J, cut[t], cut[t + 1], esc0[t], instr[t], [&](uint64_t, char ch) {
+      d += (ch == '{' || ch == '[') ? 1 : -1;
+      return true;
+    });
+    delta[t] = d;
+  });
+  for (int t = 0; t < T; ++t) d0[t] = t ? d0[t - 1] + delta[t - 1] : 1;
+  parallel_for(T, [&](int t) {
+    if (d0[t] > 0) scan_chunk(J, cut[t], cut[t + 1], esc0[t], instr[t], d0[t], CS[t]);
+  });
+  // the chunks up to the first that closes the array or holds a misplaced bracket
+  uint64_t stop = len, close = UINT64_MAX, bad = UINT64_MAX;
+  int tl = T - 1;
   for (int t = 0; t < T; ++t) {
-    for (const uint64_t e : E[t].ev) {
-      const uint64_t pos = e >> 2;
-      const int code = (int)(e & 3);
-      if (code < 2) {
-        if (depth == 1) {
-          if (!gap_ok(J, last, pos, S.spans.empty(), false, S.spans.size(), S)) return;
-          if (code != 0) {
-            S.code = DK_E_INVALID;
-            S.msg = "entity " + std::to_string(S.spans.size()) + " is not a JSON object";
-            return;
-          }
-          start = pos;
-        }
-        ++depth;
-      } else {
-        --depth;
-        if (depth == 1) {
-          S.spans.emplace_back(start, pos + 1);
-          last = pos + 1;
-        } else if (depth == 0) {
-          if (code != 3) {
-            S.code = DK_E_UNSUPPORTED;
-            S.msg = "JSON: expected a value";
-            return;
-          }
-          if (!gap_ok(J, last, pos, S.spans.empty(), true, S.spans.size(), S)) return;
-          uint64_t i = pos + 1;
-          while (i < len && is_ws(J[i])) ++i;
-          if (i != len) {
-            S.code = DK_E_UNSUPPORTED;
-            S.msg = "JSON: trailing characters";
-          }
-          return;
-        }
-      }
-    }
+    if (CS[t].bad != UINT64_MAX) { bad = stop = CS[t].bad; tl = t; break; }
+    if (CS[t].close != UINT64_MAX) { close = stop = CS[t].close; tl = t; break; }
   }
-  S.code = DK_E_UNSUPPORTED;  // the array never closes (or a string never ends)
-  S.msg = "JSON: unexpected end of input";
+  std::vector<uint64_t> so(tl + 2, 0), eo(tl + 2, 0);
+  for (int t = 0; t <= tl; ++t) {
+    so[t + 1] = so[t] + CS[t].starts.size();
+    eo[t + 1] = eo[t] + CS[t].ends.size();
+  }
+  std::vector<uint64_t> starts(so[tl + 1]), ends(eo[tl + 1]);
+  parallel_for(tl + 1, [&](int t) {
+    std::copy(CS[t].starts.begin(), CS[t].starts.end(), starts.begin() + so[t]);
+    std::copy(CS[t].ends.begin(), CS[t].ends.end(), ends.begin() + eo[t]);
+  });
+  const uint64_t ns = starts.size(), ne = ends.size();  // ne == ns or ns - 1
+  // the first entity whose gap is malformed (gaps in parallel; the first one found wins)
+  std::vector<uint64_t> first_bad(T, UINT64_MAX);
+  parallel_for(T, [&](int t) {
+    const uint64_t k0 = ns * (uint64_t)t / (uint64_t)T, k1 = ns * (uint64_t)(t + 1) / (uint64_t)T;
+    for (uint64_t k = k0; k < k1; ++k) {
+      const Gap g = classify_gap(J, k ? ends[k - 1] : lo, starts[k]);
+      if (g != (k ? kComma : kEmpty)) { first_bad[t] = k; break; }
+    }
+  });
+  uint64_t kbad = UINT64_MAX;
+  for (int t = 0; t < T && kbad == UINT64_MAX; ++t) kbad = first_bad[t];
+  const uint64_t nspans = kbad != UINT64_MAX ? kbad : ne;
+  S.spans.resize(nspans);
+  parallel_for(T, [&](int t) {
+    const uint64_t k0 = nspans * (uint64_t)t / (uint64_t)T, k1 = nspans * (uint64_t)(t + 1) / (uint64_t)T;
+    for (uint64_t k = k0; k < k1; ++k) S.spans[k] = {starts[k], ends[k]};
+  });
+  if (kbad != UINT64_MAX) {  // entity kbad follows a malformed gap
+    element_check(classify_gap(J, kbad ? ends[kbad - 1] : lo, starts[kbad]), kbad, kEntity, S);
+    return;
+  }
+  if (ns > ne) {  // an entity still open where the scan stopped (its gap was fine)
+    S.code = DK_E_UNSUPPORTED;
+    S.msg = "JSON: unexpected end of input";
+    return;
+  }
+  const uint64_t last = nspans ? ends[nspans - 1] : lo;
+  const Next nx = bad != UINT64_MAX ? kBad : (close != UINT64_MAX ? kClose : kEnd);
+  if (!element_check(classify_gap(J, last, stop), nspans, nx, S)) return;
+  uint64_t i = close + 1;  // kClose: whitespace only after the array
+  while (i < len && is_ws(J[i])) ++i;
+  if (i != len) {
+    S.code = DK_E_UNSUPPORTED;
+    S.msg = "JSON: trailing characters";
+  }
 }
 
 // One worker's slice of a column: values back to back, offsets relative to the slice.
@@ -900,7 +970,6 @@ int dk_interner_intern(dk_interner* it, const dk_column* col, uint64_t n, uint64
     if (col->offsets[i + 1] < col->offsets[i]) return dk_fail_ingest(DK_E_INVALID, "offsets not monotone");
   }
   try {
-    it->reserve(n, n ? col->offsets[n] - col->offsets[0] : 0);
     std::u16string k;
     for (uint64_t i = 0; i < n; ++i) {
       const uint32_t a = col->offsets[i], b = col->offsets[i + 1];
@@ -983,14 +1052,25 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
     if (src->group_no) P->group.assign(n, (uint8_t)src->group_no);
     lap("merge");
     // record IDs in batch order: new ids are dense in first-appearance order
+    if (ids->size() + n >= (1ull << 31)) fail(DK_E_UNSUPPORTED, "over 2^31 record IDs");
     P->ident.resize(n);
-    uint64_t rid_units = 0;
-    for (const Slice& x : sl) rid_units += x.cols[np + nk].u.size();
-    ids->reserve(n, rid_units);
-    for (const Slice& x : sl) {
-      const ColPart& C = x.cols[np + nk];
-      for (uint64_t i = 0; i < x.e1 - x.e0; ++i)
-        P->ident[x.e0 + i] = ids->find_or_add(C.u.data() + C.off[i], C.off[i + 1] - C.off[i], x.hash[i]);
+    {
+      PodVec<const char16_t*> ptr;  // filled by the slices' workers (first touch in parallel)
+      PodVec<uint32_t> ln;
+      PodVec<uint64_t> hs;
+      ptr.reset_uninit(n);
+      ln.reset_uninit(n);
+      hs.reset_uninit(n);
+      parallel_for((int)sl.size(), [&](int t) {
+        const Slice& x = sl[t];
+        const ColPart& C = x.cols[np + nk];
+        for (uint64_t i = 0; i < x.e1 - x.e0; ++i) {
+          ptr[x.e0 + i] = C.u.data() + C.off[i];
+          ln[x.e0 + i] = C.off[i + 1] - C.off[i];
+          hs[x.e0 + i] = x.hash[i];
+        }
+      });
+      ids->intern_batch(n, ptr.data(), ln.data(), hs.data(), P->ident.data(), pack_threads(n, 4096));
     }
     lap("intern");
     P->pub.n = n;

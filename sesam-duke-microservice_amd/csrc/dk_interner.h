@@ -1,23 +1,88 @@
 // dk_interner.h — exact UTF-16 string interning for the host-side units: record IDs (native
 // ingestion, the link database) and blocking-key strings (dk_upsert).  Not part of the ABI.
 //
-// One open-addressing table over a string arena: ids are dense in first-insertion order, a
-// slot holds the hash's high half as a tag plus id + 1, so a probe touches one cache line of
-// slots and compares units only on a tag hit.  Hashes are computed by the caller (ingestion
-// workers hash their records in parallel; the ordered insert is then one sequential pass).
+// An open-addressing table over a string arena: ids are dense in first-insertion order.
+// The slot array is split into kShards shards by the hash's top bits, so a batch is
+// interned shard-parallel (intern_batch): each worker probes / inserts the batch's strings
+// of its shards in batch order under provisional ids, one sequential pass over the batch
+// then numbers the new strings in first-appearance order, and the workers patch their
+// slots and copy the new strings into the arena.  A slot holds the hash's high half as a
+// tag plus id + 1, so a probe compares units only on a tag hit.
 #pragma once
 
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
+// A growable array of trivially copyable T whose growth leaves the new tail unwritten, so
+// the workers that fill it also take its first-touch page faults, in parallel.
+template <typename T>
+struct PodVec {
+  T* p = nullptr;
+  uint64_t n = 0, cap = 0;
+  PodVec() = default;
+  PodVec(const PodVec&) = delete;
+  PodVec& operator=(const PodVec&) = delete;
+  PodVec(PodVec&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
+  PodVec& operator=(PodVec&& o) noexcept {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+    return *this;
+  }
+  ~PodVec() { delete[] p; }
+  uint64_t size() const { return n; }
+  T* data() { return p; }
+  const T* data() const { return p; }
+  T& operator[](uint64_t i) { return p[i]; }
+  const T& operator[](uint64_t i) const { return p[i]; }
+  void clear() { n = 0; }
+  void reserve(uint64_t c) {  // geometric: streams of small batches stay linear
+    if (c <= cap) return;
+    c = std::max<uint64_t>(c, 2 * cap);
+    T* q = new T[c];  // default-initialised: no writes
+    if (n) memcpy(q, p, n * sizeof(T));
+    delete[] p;
+    p = q;
+    cap = c;
+  }
+  void resize_uninit(uint64_t m) {
+    reserve(m);
+    n = m;
+  }
+  void reset_uninit(uint64_t m) {  // m elements, old contents dropped, nothing written
+    if (m > cap) {
+      delete[] p;
+      p = new T[m];
+      cap = m;
+    }
+    n = m;
+  }
+  void push_back(const T& v) {
+    reserve(n + 1);
+    p[n++] = v;
+  }
+  void append(const T* v, uint64_t m) {
+    reserve(n + m);
+    if (m) memcpy(p + n, v, m * sizeof(T));
+    n += m;
+  }
+};
+
 struct U16Table {
-  std::vector<char16_t> arena;
-  std::vector<uint64_t> start{0};  // id -> [start[id], start[id + 1]) in the arena
-  std::vector<uint64_t> hashes;    // id -> its hash (rehash without re-reading strings)
-  std::vector<uint64_t> slots;     // (tag << 32) | (id + 1); 0 = empty
-  uint64_t mask = 0;
+  static constexpr int kShardBits = 4, kShards = 1 << kShardBits;
+  static constexpr uint32_t kProv = 0x80000000u;  // slot id field: batch index of a new string
+
+  PodVec<char16_t> arena;
+  PodVec<uint64_t> start;          // id -> [start[id], start[id + 1]) in the arena
+  PodVec<uint64_t> hashes;         // id -> its hash (rehash without re-reading strings)
+  PodVec<uint64_t> slots;          // kShards x shard_cap: (tag << 32) | (id + 1); 0 = empty
+  uint64_t shard_cap = 0;          // power of two
+  uint64_t fill[kShards] = {};
+
+  U16Table() { start.push_back(0); }
 
   static uint64_t hash(const char16_t* s, uint64_t n) {
     // 8-byte words, multiply-xorshift mixing; the length seeds it ("" != "\0")
@@ -36,34 +101,27 @@ struct U16Table {
     h *= 0x9E3779B97F4A7C15ull;
     return h ^ (h >> 29);
   }
+  static int shard_of(uint64_t h) { return (int)(h >> (64 - kShardBits)); }
 
   uint64_t size() const { return hashes.size(); }
   const char16_t* str(uint64_t id) const { return arena.data() + start[id]; }
   uint64_t len(uint64_t id) const { return start[id + 1] - start[id]; }
   void clear() {
     arena.clear();
-    start.assign(1, 0);
+    start.clear();
+    start.push_back(0);
     hashes.clear();
     slots.clear();
-    mask = 0;
-  }
-  // room for nstrings more strings of nunits units in total (geometric, so a stream of small
-  // batches into a large table does not copy the arena each time)
-  void reserve(uint64_t nstrings, uint64_t nunits) {
-    auto room = [](auto& v, uint64_t add) {
-      if (v.capacity() < v.size() + add) v.reserve(std::max<uint64_t>(v.size() + add, 2 * v.capacity()));
-    };
-    room(arena, nunits);
-    room(start, nstrings);
-    room(hashes, nstrings);
-    grow_to(size() + nstrings);
+    shard_cap = 0;
+    std::fill(fill, fill + kShards, 0);
   }
 
   bool find(const char16_t* s, uint64_t n, uint64_t h, uint64_t* id) const {
-    if (slots.empty()) return false;
-    const uint64_t tag = h >> 32;
-    for (uint64_t i = h & mask;; i = (i + 1) & mask) {
-      const uint64_t e = slots[i];
+    if (!shard_cap) return false;
+    const uint64_t* sh = slots.data() + (uint64_t)shard_of(h) * shard_cap;
+    const uint64_t m = shard_cap - 1, tag = h >> 32;
+    for (uint64_t i = h & m;; i = (i + 1) & m) {
+      const uint64_t e = sh[i];
       if (!e) return false;
       if ((e >> 32) == tag) {
         const uint64_t x = (uint32_t)e - 1;
@@ -76,19 +134,157 @@ struct U16Table {
   }
   bool find(const char16_t* s, uint64_t n, uint64_t* id) const { return find(s, n, hash(s, n), id); }
 
-  // the id of s, interned if new (ids < 2^32 - 1; the callers bound their tables far below)
+  // the id of s, interned if new
   uint64_t find_or_add(const char16_t* s, uint64_t n, uint64_t h) {
     uint64_t id;
     if (find(s, n, h, &id)) return id;
     id = size();
-    grow_to(id + 1);
-    arena.insert(arena.end(), s, s + n);
+    const int sh = shard_of(h);
+    ensure_shard(sh, fill[sh] + 1);
+    arena.append(s, n);
     start.push_back(arena.size());
     hashes.push_back(h);
     place(h, id);
     return id;
   }
   uint64_t find_or_add(const char16_t* s, uint64_t n) { return find_or_add(s, n, hash(s, n)); }
+
+  // out[i] = id of string i (ptr[i], n[i], hash h[i]); new strings get ids in the order of
+  // their first appearance in the batch, exactly as n sequential find_or_add calls would
+  void intern_batch(uint64_t cnt, const char16_t* const* ptr, const uint32_t* n, const uint64_t* h,
+                    uint64_t* out, int threads) {
+    if (cnt < 4096 || threads <= 1) {
+      for (uint64_t i = 0; i < cnt; ++i) out[i] = find_or_add(ptr[i], n[i], h[i]);
+      return;
+    }
+    const int T = std::min(threads, kShards);
+    // the batch's indices per shard, in batch order (parallel counting sort)
+    std::vector<uint64_t> cnts((size_t)T * kShards, 0);
+    run(T, [&](int t) {
+      uint64_t* c = cnts.data() + (size_t)t * kShards;
+      for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) ++c[shard_of(h[i])];
+    });
+    std::vector<uint64_t> base((size_t)T * kShards), shard_lo(kShards + 1, 0);
+    uint64_t acc = 0;
+    for (int s = 0; s < kShards; ++s) {
+      shard_lo[s] = acc;
+      for (int t = 0; t < T; ++t) {
+        base[(size_t)t * kShards + s] = acc;
+        acc += cnts[(size_t)t * kShards + s];
+      }
+    }
+    shard_lo[kShards] = acc;
+    std::vector<uint32_t> order(cnt);
+    run(T, [&](int t) {
+      uint64_t* b = base.data() + (size_t)t * kShards;
+      for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) order[b[shard_of(h[i])]++] = (uint32_t)i;
+    });
+    // room for the batch's new strings (load <= 1/2 per shard): bounded by the batch's count
+    // per shard, or -- when that bound would grow the table -- by a read-only lookup pass
+    // first (a re-posted batch then never grows it)
+    uint64_t need = 0;
+    for (int s = 0; s < kShards; ++s) need = std::max(need, fill[s] + (shard_lo[s + 1] - shard_lo[s]));
+    std::vector<char> known;  // per order position: found by the lookup pass (out[] set)
+    if (shard_cap && 2 * need > shard_cap) {
+      known.assign(cnt, 0);
+      std::vector<uint64_t> miss(kShards, 0);
+      run(T, [&](int t) {
+        for (int s = t; s < kShards; s += T)
+          for (uint64_t k = shard_lo[s]; k < shard_lo[s + 1]; ++k) {
+            const uint32_t i = order[k];
+            uint64_t id;
+            if (find(ptr[i], n[i], h[i], &id)) {
+              out[i] = id;
+              known[k] = 1;
+            } else {
+              ++miss[s];
+            }
+          }
+      });
+      need = 0;
+      for (int s = 0; s < kShards; ++s) need = std::max(need, fill[s] + miss[s]);
+    }
+    ensure_all(need, T);
+    // per shard, in batch order: existing id, or provisional (kProv | first index)
+    std::vector<std::vector<uint64_t>> placed(kShards);  // slot positions of new strings
+    run(T, [&](int t) {
+      for (int s = t; s < kShards; s += T) {
+        uint64_t* sh = slots.data() + (uint64_t)s * shard_cap;
+        const uint64_t m = shard_cap - 1;
+        for (uint64_t k = shard_lo[s]; k < shard_lo[s + 1]; ++k) {
+          if (!known.empty() && known[k]) continue;
+          const uint32_t i = order[k];
+          const uint64_t hh = h[i], tag = hh >> 32;
+          uint64_t pos = hh & m;
+          for (;; pos = (pos + 1) & m) {
+            const uint64_t e = sh[pos];
+            if (!e) {
+              sh[pos] = (tag << 32) | (kProv | i);
+              placed[s].push_back(pos);
+              out[i] = kProv | (uint64_t)i;
+              ++fill[s];
+              break;
+            }
+            if ((e >> 32) != tag) continue;
+            const uint32_t v = (uint32_t)e;
+            if (v & kProv) {
+              const uint32_t j = v & ~kProv;
+              if (n[j] == n[i] && (n[i] == 0 || memcmp(ptr[j], ptr[i], (size_t)n[i] * 2) == 0)) {
+                out[i] = kProv | (uint64_t)j;
+                break;
+              }
+            } else {
+              const uint64_t x = v - 1;
+              if (len(x) == n[i] && (n[i] == 0 || memcmp(str(x), ptr[i], (size_t)n[i] * 2) == 0)) {
+                out[i] = x;
+                break;
+              }
+            }
+          }
+        }
+      }
+    });
+    // number the new strings in first-appearance order
+    const uint64_t id0 = size();
+    uint64_t nid = id0, units = 0;
+    std::vector<uint32_t> fresh;
+    for (uint64_t i = 0; i < cnt; ++i) {
+      const uint64_t v = out[i];
+      if (!(v & kProv)) continue;
+      const uint64_t j = v & ~(uint64_t)kProv;
+      if (j == i) {
+        out[i] = nid++;
+        fresh.push_back((uint32_t)i);
+        units += n[i];
+      } else {
+        out[i] = out[j];
+      }
+    }
+    // slots, ids -> strings, arena
+    const uint64_t a0 = arena.size();
+    arena.resize_uninit(a0 + units);
+    start.resize_uninit(start.size() + fresh.size());
+    hashes.resize_uninit(id0 + fresh.size());
+    uint64_t at = a0;
+    for (size_t f = 0; f < fresh.size(); ++f) {
+      at += n[fresh[f]];
+      start[id0 + 1 + f] = at;
+    }
+    run(T, [&](int t) {
+      for (int s = t; s < kShards; s += T) {
+        uint64_t* sh = slots.data() + (uint64_t)s * shard_cap;
+        for (uint64_t pos : placed[s]) {
+          const uint32_t i = (uint32_t)sh[pos] & ~kProv;
+          sh[pos] = (sh[pos] & ~0xFFFFFFFFull) | (out[i] + 1);
+        }
+      }
+      for (size_t f = fresh.size() * t / T; f < fresh.size() * (t + 1) / T; ++f) {
+        const uint32_t i = fresh[f];
+        hashes[id0 + f] = h[i];
+        if (n[i]) memcpy(arena.data() + start[id0 + f], ptr[i], (size_t)n[i] * 2);
+      }
+    });
+  }
 
   // String.compareTo order of two ids (UTF-16 units, unsigned)
   int compare(uint64_t a, uint64_t b) const {
@@ -100,18 +296,46 @@ struct U16Table {
   }
 
  private:
-  void place(uint64_t h, uint64_t id) {
-    uint64_t i = h & mask;
-    while (slots[i]) i = (i + 1) & mask;
-    slots[i] = ((h >> 32) << 32) | (id + 1);
+  template <typename F>
+  static void run(int T, F&& f) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back([&f, t] { f(t); });
+    f(0);
+    for (auto& x : th) x.join();
   }
-  void grow_to(uint64_t n) {  // load factor <= 1/2
-    if (!slots.empty() && 2 * n <= slots.size()) return;
-    uint64_t cap = slots.empty() ? 64 : slots.size();
+  void place(uint64_t h, uint64_t id) {
+    const int s = shard_of(h);
+    uint64_t* sh = slots.data() + (uint64_t)s * shard_cap;
+    const uint64_t m = shard_cap - 1;
+    uint64_t i = h & m;
+    while (sh[i]) i = (i + 1) & m;
+    sh[i] = ((h >> 32) << 32) | (id + 1);
+    ++fill[s];
+  }
+  void ensure_shard(int, uint64_t n) { ensure_all(n, 1); }
+  // every shard holds n entries at load <= 1/2 (all shards share one capacity)
+  void ensure_all(uint64_t n, int T) {
+    if (shard_cap && 2 * n <= shard_cap) return;
+    uint64_t cap = shard_cap ? shard_cap : 64;
     while (cap < 2 * n) cap *= 2;
-    slots.assign(cap, 0);
-    mask = cap - 1;
-    for (uint64_t id = 0; id < size(); ++id) place(hashes[id], id);
+    slots.reset_uninit((uint64_t)kShards * cap);
+    shard_cap = cap;
+    std::fill(fill, fill + kShards, 0);
+    // zero and refill the shards in parallel (each worker owns whole shards)
+    const uint64_t nid = size();
+    const int TT = std::max(1, std::min(T, kShards));
+    run(TT, [&](int t) {
+      for (int s = t; s < kShards; s += TT) memset(slots.data() + (uint64_t)s * cap, 0, cap * 8);
+      for (uint64_t id = 0; id < nid; ++id) {
+        const int s = shard_of(hashes[id]);
+        if (s % TT != t) continue;
+        uint64_t* sh = slots.data() + (uint64_t)s * cap;
+        uint64_t i = hashes[id] & (cap - 1);
+        while (sh[i]) i = (i + 1) & (cap - 1);
+        sh[i] = ((hashes[id] >> 32) << 32) | (id + 1);
+        ++fill[s];
+      }
+    });
   }
 };
 

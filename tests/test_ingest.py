@@ -207,6 +207,17 @@ def test_pack_json_parallel_split_matches_python_path(threads, monkeypatch):
     ('[{"_id": "1"}] x', A.DK_E_UNSUPPORTED),              # trailing characters
     ('  ', A.DK_E_UNSUPPORTED),
     ('5', A.DK_E_INVALID),
+    ('[ , ]', A.DK_E_INVALID),
+    ('[{"_id": "1"}, "x"]', A.DK_E_INVALID),
+    ('[{"_id": "1"} "x"]', A.DK_E_UNSUPPORTED),
+    ('[ ', A.DK_E_UNSUPPORTED),
+    ('[{"_id": "1"},', A.DK_E_UNSUPPORTED),
+    ('[{"_id": "1"}, 5', A.DK_E_INVALID),
+    ('[[1]]', A.DK_E_INVALID),
+    ('[{"_id": "1"}, [1]]', A.DK_E_INVALID),
+    ('[{"_id": "1"} [1]]', A.DK_E_UNSUPPORTED),
+    ('[}', A.DK_E_INVALID),
+    ('[{"_id": "1"}}]', A.DK_E_UNSUPPORTED),
 ])
 def test_pack_json_errors_parallel(body, code, threads, monkeypatch):
     monkeypatch.setenv("DK_INGEST_THREADS", str(threads))
@@ -224,3 +235,34 @@ def test_pack_json_empty_array():
     ns = I.NativeSource(source(), PROPS, KEYS)
     pk = ns.pack(" [ \n ] ", I.Interner())
     assert pk.n == 0
+
+
+def test_parallel_interning_equals_sequential(monkeypatch):
+    """Record IDs interned shard-parallel (large batches) get the ids sequential interning
+    gives: dense, in first-appearance order, re-posted IDs keep theirs; across batches that
+    grow the table and batches that only look up."""
+    rng = random.Random(7)
+    src = DataSource("ds", [DataSourceColumn("raw", "RAW", None)])
+    ns = I.NativeSource(src, ["RAW"], [])
+    bodies = []
+    for b, (n, span) in enumerate([(9000, 6000), (20000, 30000), (12000, 30000), (9000, 40000)]):
+        ents = [{"_id": f"id{rng.randrange(span)}" + ("é" if rng.random() < 0.05 else ""), "raw": "x"}
+                for _ in range(n)]
+        bodies.append(json.dumps(ents))
+    got = {}
+    for threads in ("1", "8"):
+        monkeypatch.setenv("DK_INGEST_THREADS", threads)
+        it = I.Interner()
+        packs = [ns.pack(body, it) for body in bodies]   # the idents live in their batches
+        got[threads] = [[int(x) for x in pk.ident] for pk in packs]
+        ids = [r for body in bodies for r in (f"ds__{e['_id']}" for e in json.loads(body))]
+        flat = [x for batch in got[threads] for x in batch]
+        assert [it.find(r) for r in ids] == flat
+        assert len(it) == len(set(ids))
+    assert got["1"] == got["8"]
+    # first-appearance numbering
+    seen = {}
+    for r in (f"ds__{e['_id']}" for body in bodies for e in json.loads(body)):
+        seen.setdefault(r, len(seen))
+    assert [x for batch in got["8"] for x in batch] == [seen[f"ds__{e['_id']}"] for body in bodies
+                                                        for e in json.loads(body)]
