@@ -425,7 +425,10 @@ def main():
         achieved = prof["score_bytes"] / score_s if score_s > 0 else 0.0
         traffic = None
         valu = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_k_score.json")
+        # the kept PMC summary of this workload's scoring kernel (scripts/summarize_profiles.py)
+        pmc = os.path.join(ROOT, "profiles", f"pmc_k_score_{w['name']}.json")
+        if not os.path.exists(pmc):
+            pmc = os.path.join(ROOT, "profiles", "pmc_k_score.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pj = json.load(f)
@@ -442,7 +445,7 @@ def main():
                 rate = ipp * prof["pairs_scored"] / score_s if score_s > 0 else 0.0
                 valu = {"insts_per_pair": ipp, "achieved": rate / 1e9, "peak": VALU_PEAK / 1e9,
                         "unit": "G wave-instructions/s", "frac": rate / VALU_PEAK,
-                        "source": "profiles/pmc_k_score.json (" + pj.get("commit", "?") + ")"}
+                        "source": os.path.relpath(pmc, ROOT) + " (" + pj.get("commit", "?") + ")"}
         out = {
             "metric": METRIC,
             "value": value,

@@ -120,6 +120,19 @@ static int run_tasks(int n, bool parallel, F&& task) {
   return DK_OK;
 }
 
+// DK_HOST_TIMING=1: host phase times of dk_upsert on stderr (diagnostics)
+struct HostLap {
+  bool on;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  HostLap() : on(getenv("DK_HOST_TIMING") != nullptr) {}
+  void operator()(const char* what) {
+    if (!on) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "dk_upsert %s %.2f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+    t0 = t1;
+  }
+};
+
 // f(lo, hi) over [0, n) in `parts` contiguous ranges on their own threads
 template <typename F>
 static void parallel_ranges(uint64_t n, int parts, F&& f) {
@@ -949,6 +962,7 @@ static int stage_lucene(dk_ctx* c, const dk_batch* b, uint64_t n, uint64_t row0,
 }
 
 static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool transient) {
+  HostLap lap;
   if (!c || !b) return fail(DK_E_INVALID, "NULL argument");
   if (!transient && c->transient)
     return fail(DK_E_STATE, "transient rows present: dk_drop_transient before indexing");
@@ -991,6 +1005,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     });
     if (rc) return rc;
   }
+  lap("stage");
   // identity + tombstones: delete-by-ID then add (IncrementalLuceneDatabase.java:516-517;
   // skipped with overwrite, :515); transient rows are neither alive (never candidates) nor
   // entered in the ID map.  The ID map is updated here with an undo log, rolled back if
@@ -1024,6 +1039,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     }
   } rollback{c, &undo};
 
+  lap("ident");
   // 2. device space (contents preserved; nothing logical changes on failure)
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = c->stream;
@@ -1042,6 +1058,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     HIPCHK(L.qterm.reserve((nqt + ls.qterm.size()) * 4 + 4, nqt * 4, s));
   }
 
+  lap("reserve");
   // 3. commit
   c->index_gen++;
   if (transient && !c->transient) {
@@ -1084,6 +1101,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
                           hipMemcpyHostToDevice, s));
   }
   HIPCHK(hipStreamSynchronize(s));  // host staging goes out of scope
+  lap("copy");
   if (L.on) {
     L.npost += ls.pkey.size();
     L.qoff.insert(L.qoff.end(), ls.qoff.begin(), ls.qoff.end());
