@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 #include <rocprim/rocprim.hpp>
 
 #include "dk_internal.h"
@@ -510,6 +511,14 @@ __device__ __forceinline__ uint32_t wl_class(uint32_t ch) {
   return 0u;
 }
 
+// max of two weights (finite, positive: no NaN ordering to honour), one v_max_f64 -- fmax
+// would first canonicalise the operand the compiler cannot prove canonical
+__device__ __forceinline__ double max_weight(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ double wl_class_weight(uint32_t cls) {
   return cls == 1u ? 2.0 : (cls == 2u ? 0.1 : 1.0);
 }
@@ -528,6 +537,16 @@ __device__ __forceinline__ double wl_class_weight(uint32_t cls) {
 // Out of line: the stream's registers (column, weights, units, ring cursor) get an
 // allocation of their own instead of competing with the fused kernel's live state, which
 // spilled the weights and units inside the cell loop.
+// f(integral_constant<int, i>) for i = 0 .. N-1, unrolled at compile time
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 template <int G, int R, bool WL, typename CT>
 __device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1p, int n1, int nneed) {
   uint64_t* lds = g_wave_tables[threadIdx.x >> 6];
@@ -603,9 +622,16 @@ __device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1
   load_block();
   wave_lds_sync();
 
-  T col[R];
+  // The lane's DP column.  In the steady state logical row r lives in col[(r + rho) %
+  // (R + 1)], rho = -t mod (R + 1): a step writes row r's new value into the slot row r-1
+  // vacated (row r-1's old value was row r's diagonal), so the column rotates one slot per
+  // step instead of being moved back (a register move per cell), and the steady-state loop
+  // is unrolled R + 1 steps, which makes every slot index a constant.  The pipeline fill
+  // (t < G: lane k starts its first column at step k) runs in place, rho = 0.
+  T col[R + 1];
 #pragma unroll
   for (int r = 0; r < R; ++r) col[r] = (T)(k * R + r + 1);  // D(i, 0) = i
+  col[R] = (T)0;
   T prev = (T)(k * R);                                      // D(k*R, j-1)
   T bot = col[R - 1];
   int m = 0, j = 1 - k;  // this lane's candidate and its column at this step
@@ -616,7 +642,9 @@ __device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1
     srcc = (int)(x >> 16);
   }
   uint32_t lu = ring[(0 - k) & 127];  // the unit of stream column t - k, read a step ahead
-  for (int t = 0; t < tend; ++t) {
+  auto step = [&](auto rho_c, int t, auto fill_c) {
+    constexpr int rho = decltype(rho_c)::value;
+    constexpr bool FILL = decltype(fill_c)::value;
     if ((t & 63) == 32) {  // block b+1 into the half block b-1 held, then load block b+2
       write_block(((t >> 6) + 1) & 1);
       load_block();
@@ -630,7 +658,8 @@ __device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1
         uint64_t bits = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const uint64_t b = WL ? (uint64_t)__double_as_longlong((double)col[r]) : (uint64_t)(uint32_t)(int)col[r];
+          const T x = col[(r + rho) % (R + 1)];
+          const uint64_t b = WL ? (uint64_t)__double_as_longlong((double)x) : (uint64_t)(uint32_t)(int)x;
           bits |= b & (0ull - (uint64_t)(r + 1 == rstar));
         }
         rbits[srcc] = bits;
@@ -645,43 +674,47 @@ __device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1
       int kb = k * R;
       asm volatile("" : "+v"(kb));
 #pragma unroll
-      for (int r = 0; r < R; ++r) col[r] = (T)(kb + r + 1);
+      for (int r = 0; r < R; ++r) col[(r + rho) % (R + 1)] = (T)(kb + r + 1);
       prev = (T)kb;
     }
     // lane 0's row above: the matrix's top boundary D(0, j)
     T top;
-    if (WL) top = n1 == 1 ? col[0] : (T)(j == 1 ? n1 : j);
+    if (WL) top = n1 == 1 ? col[rho % (R + 1)] : (T)(j == 1 ? n1 : j);
     else top = (T)j;
     const T recv = from_left<G>(top, bot, k);  // D(k*R, j)
-    if (j >= 1 && m < cnt) {
+    // the fill computes only lanes that have started (in place); the steady state computes
+    // every lane (finished lanes produce values no running lane reads: a lane only takes
+    // its left neighbour's column while that neighbour was still running)
+    if (FILL ? (j >= 1 && m < cnt) : true) {
       T up = recv, dg = prev;
-      if (WL) {
-        const double w2 = wl_class_weight(u >> 16);
+      const double w2 = WL ? wl_class_weight(u >> 16) : 0.0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const double old = col[r];
-          const double cost = c1[r] == u ? 0.0 : fmax(w1[r], w2);
+      for (int r = 0; r < R; ++r) {
+        const T old = col[(r + rho) % (R + 1)];
+        T v;
+        if (WL) {
+          const double cost = c1[r] == u ? 0.0 : max_weight(w1[r], w2);
           // Math.min(left, Math.min(above, aboveleft)) on non-negative values
-          const double v = fmin((double)up + w1[r], fmin(old + w2, (double)dg + cost));
-          col[r] = (T)v;
-          dg = (T)old;
-          up = (T)v;
+          v = (T)fmin((double)up + w1[r], fmin((double)old + w2, (double)dg + cost));
+        } else {
+          v = (T)(imin3((int)up, (int)dg, (int)old) + (c1[r] == u ? 0 : 1));
         }
-      } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int old = (int)col[r];
-          const int v = imin3((int)up, (int)dg, old) + (c1[r] == u ? 0 : 1);
-          col[r] = (T)v;
-          dg = (T)old;
-          up = (T)v;
-        }
+        col[FILL ? (r + rho) % (R + 1) : (r + rho + R) % (R + 1)] = v;
+        dg = old;
+        up = v;
       }
       prev = recv;
-      bot = col[R - 1];
+      bot = up;
     }
     ++j;
-  }
+  };
+  const int tfill = min(tend, G);
+  for (int t = 0; t < tfill; ++t) step(std::integral_constant<int, 0>{}, t, std::true_type{});
+  for (int t = tfill; t < tend; t += R + 1)
+    static_for<R + 1>([&](auto q) {
+      constexpr int qq = decltype(q)::value;
+      if (t + qq < tend) step(std::integral_constant<int, (R + 1 - qq) % (R + 1)>{}, t + qq, std::false_type{});
+    });
 }
 
 // Similarity of every lane with `need` set (the others keep `sim`) through long_dp.
