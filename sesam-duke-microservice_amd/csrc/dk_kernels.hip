@@ -511,14 +511,6 @@ __device__ __forceinline__ uint32_t wl_class(uint32_t ch) {
   return 0u;
 }
 
-// max of two weights (finite, positive: no NaN ordering to honour), one v_max_f64 -- fmax
-// would first canonicalise the operand the compiler cannot prove canonical
-__device__ __forceinline__ double max_weight(double a, double b) {
-  double r;
-  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-
 __device__ __forceinline__ double wl_class_weight(uint32_t cls) {
   return cls == 1u ? 2.0 : (cls == 2u ? 0.1 : 1.0);
 }
@@ -693,7 +685,7 @@ __device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1
         const T old = col[(r + rho) % (R + 1)];
         T v;
         if (WL) {
-          const double cost = c1[r] == u ? 0.0 : max_weight(w1[r], w2);
+          const double cost = c1[r] == u ? 0.0 : fmax(w1[r], w2);
           // Math.min(left, Math.min(above, aboveleft)) on non-negative values
           v = (T)fmin((double)up + w1[r], fmin((double)old + w2, (double)dg + cost));
         } else {
