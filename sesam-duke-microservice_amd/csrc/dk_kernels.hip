@@ -373,145 +373,13 @@ __device__ __forceinline__ int compact_distance_pk(const uint64_t* peq, int n1, 
   return result;
 }
 
-// ------------------------------------------------------------------------------------
-// The packed DP with the bottom half two columns behind (skew 2) and two columns per loop
-// iteration.  With skew 1 the bottom half's row H+1 of column t-1 needs the top half's row
-// H of column t-1, computed at the end of step t-1, so every step's chain waits for the
-// whole previous step: one dependent chain of 2 instructions per row through the column.
-// With skew 2 the bottom half of step t+1 (column t-1) needs top row H of column t-1 from
-// step t-1 only, so step t+1's row i depends on step t's rows i-1 and i and nothing later:
-// the loop computes step t row i and step t+1 row i-1 together -- two independent chains
-// in flight, the same instructions.  Register pair i holds top row i of column t and
-// bottom row H+i of column t-2; the cutoff test of column t-2 (top half from step t-2,
-// bottom half from step t) and D(n1, n2-1) at step n2-1 (top) / n2+1 (bottom) as before.
-// ------------------------------------------------------------------------------------
-template <int R, typename CT>
-__device__ __forceinline__ int compact_distance_pk2(const uint64_t* peq, int n1, const Str<CT>& s2,
-                                                    int n2, bool act) {
-  constexpr int UPW = Str<CT>::UPW;
-  static_assert(UPW >= 2, "two columns per word at least");
-  constexpr int H = R / 2;
-  constexpr int TAIL = R <= 32 ? 4 : 8;  // rows past n1 lie in (R - TAIL, R]
-  constexpr int NC = (H + 15) / 16;      // cost words
-  constexpr int KT = TAIL < H ? TAIL : H;  // pairs that can hold row n1: (H - KT, H]
-  constexpr uint32_t BIG = 0x7000u;
-  const int maxdist = min(n1, n2) >> 1;
-  const uint32_t B = 0x4000u - (uint32_t)(maxdist + 1);
-  uint32_t P[H + 1];
-#pragma unroll
-  for (int i = 1; i <= H; ++i) P[i] = ((uint32_t)i + B) | (BIG << 16);  // top col -1, bottom "col -3"
-  uint32_t tm[H + 1];
-#pragma unroll
-  for (int i = 1; i <= H; ++i)
-    tm[i] = (i > n1 ? 0x4000u : 0u) | (H + i > n1 ? 0x40000000u : 0u);
-  const bool bottom_result = n1 > H;
-  int result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
-  bool live = act && n2 > 1;
-  const int fin = n2 - 1 + (bottom_result ? 2 : 0);  // step at which D(n1, n2-1) is known
-  auto extract = [&](const uint32_t* Q) {  // Q[k] = pair H - KT + 1 + k of the step
-    uint32_t r = 0;
-#pragma unroll
-    for (int row = R - TAIL + 1; row <= R; ++row)
-      if (row == n1) r = row <= H ? (Q[row - (H - KT + 1)] & 0xFFFFu) : (Q[row - H - (H - KT + 1)] >> 16);
-    return (int)(r - B);
-  };
-
-  uint32_t w = act ? s2.word(0) : 0u;  // the word holding column t
-  uint32_t wn = s2.word_any(1);
-  uint64_t ne0 = ~peq_eq<CT>(peq, Str<CT>::unit(w, 0));  // cost masks of columns t, t+1
-  uint64_t ne1 = ~peq_eq<CT>(peq, Str<CT>::unit(w, 1));
-  uint64_t nem2 = ~0ull, nem1 = ~0ull;                    // columns t-2, t-1 (bottom halves)
-  uint32_t hm1 = (uint32_t)H + B, hm2 = BIG, hm3 = BIG;   // top row H of columns t-1, t-2, t-3
-  uint32_t accm1 = 0, accm2 = 0;                          // cutoff ANDs of steps t-1, t-2
-  for (int t = 0; live; t += 2) {
-    // columns t+2, t+3 for the next iteration (t is even and wave-uniform: scalar branch)
-    if ((t + 2) % UPW == 0) {
-      w = wn;
-      wn = s2.word_any((t + 2) / UPW + 1);
-    }
-    const uint64_t ne2 = ~peq_eq<CT>(peq, Str<CT>::unit(w, (t + 2) % UPW));
-    const uint64_t ne3 = ~peq_eq<CT>(peq, Str<CT>::unit(w, (t + 3) % UPW));
-    uint32_t Ca[NC], Cb[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      Ca[c] = ((uint32_t)(ne0 >> (16 * c)) & 0xFFFFu) | ((uint32_t)(nem2 >> (H + 16 * c)) << 16);
-      Cb[c] = ((uint32_t)(ne1 >> (16 * c)) & 0xFFFFu) | ((uint32_t)(nem1 >> (H + 16 * c)) << 16);
-    }
-    // step a = t (top column t, bottom column t-2); step b = t+1 (top t+1, bottom t-1)
-    uint32_t va_prev = ((uint32_t)t + 1u + B) | (hm2 << 16);  // row 0 of step a = diag of step b row 1
-    uint32_t pd = ((uint32_t)t + B) | (hm3 << 16);
-    uint32_t vb_prev = ((uint32_t)t + 2u + B) | (hm1 << 16);
-    uint32_t va_pp = va_prev;
-    uint32_t acc_a = 0xFFFFFFFFu, acc_b = 0xFFFFFFFFu;
-    uint32_t QA[KT];  // step a's pairs that can hold row n1
-#pragma unroll
-    for (int i = 1; i <= H; ++i) {
-      const uint32_t left = P[i];
-      const uint32_t ca = (Ca[(i - 1) >> 4] >> ((i - 1) & 15)) & 0x10001u;
-      const uint32_t va = pk_min3_u16(va_prev, pd, left) + ca;
-      if (H + i > R - TAIL) acc_a &= va | tm[i];
-      else acc_a &= va;
-      if (i > H - KT) QA[i - (H - KT + 1)] = va;
-      if (i >= 2) {  // step b, row i-1
-        const uint32_t cb = (Cb[(i - 2) >> 4] >> ((i - 2) & 15)) & 0x10001u;
-        const uint32_t vb = pk_min3_u16(vb_prev, va_pp, va_prev) + cb;
-        P[i - 1] = vb;
-        vb_prev = vb;
-        if (H + i - 1 > R - TAIL) acc_b &= vb | tm[i - 1];
-        else acc_b &= vb;
-      }
-      pd = left;
-      va_pp = va_prev;
-      va_prev = va;
-    }
-    {  // step b, row H
-      const uint32_t cb = (Cb[(H - 1) >> 4] >> ((H - 1) & 15)) & 0x10001u;
-      const uint32_t vb = pk_min3_u16(vb_prev, va_pp, va_prev) + cb;
-      P[H] = vb;
-      if (2 * H > R - TAIL) acc_b &= vb | tm[H];
-      else acc_b &= vb;
-    }
-    hm3 = hm1;
-    hm2 = va_prev & 0xFFFFu;  // top row H of column t
-    hm1 = P[H] & 0xFFFFu;     // of column t+1
-    // column t-2 cut off (top half: step t-2, bottom half: step t), then column t-1
-    if (t >= 3 && (accm2 & 0x4000u) && (acc_a & 0x40000000u)) {
-      result = maxdist + 1;
-      live = false;
-    } else if (t == fin) {
-      result = extract(QA);
-      live = false;
-    } else if (t + 1 >= 3 && (accm1 & 0x4000u) && (acc_b & 0x40000000u)) {
-      result = maxdist + 1;
-      live = false;
-    } else if (t + 1 == fin) {
-      result = extract(P + (H - KT + 1));
-      live = false;
-    }
-    accm2 = acc_a;
-    accm1 = acc_b;
-    nem2 = ne0;
-    nem1 = ne1;
-    ne0 = ne2;
-    ne1 = ne3;
-  }
-  return result;
-}
-
 // [Duke 1.2] comparators.Levenshtein.compare.  RMAX: the largest row bucket this kernel
 // variant instantiates (the host picks the variant from the longest Levenshtein value),
 // which bounds the VGPRs of the whole fused kernel and so its occupancy.
-// Row buckets up to 16 take the skew-1 DP (measured faster there: the per-iteration work of
-// the two-column loop does not pay for short columns), longer ones the skew-2 two-column DP.
-#if defined(DK_LEV_SCALAR)
+#ifdef DK_LEV_SCALAR
 #define DK_LEV_DP compact_distance_peq
-#define DK_LEV_DP_LONG compact_distance_peq
-#elif defined(DK_LEV_SKEW1)
-#define DK_LEV_DP compact_distance_pk
-#define DK_LEV_DP_LONG compact_distance_pk
 #else
 #define DK_LEV_DP compact_distance_pk
-#define DK_LEV_DP_LONG compact_distance_pk2
 #endif
 
 template <int RMAX, typename CT>
@@ -534,14 +402,14 @@ __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str
     case 2: d = DK_LEV_DP<8>(peq, n1, s2, n2, run); break;
     case 3: d = DK_LEV_DP<12>(peq, n1, s2, n2, run); break;
     case 4: d = DK_LEV_DP<16>(peq, n1, s2, n2, run); break;
-    case 5: d = DK_LEV_DP_LONG<20>(peq, n1, s2, n2, run); break;
-    case 6: d = DK_LEV_DP_LONG<24>(peq, n1, s2, n2, run); break;
-    case 7: d = DK_LEV_DP_LONG<28>(peq, n1, s2, n2, run); break;
-    case 8: d = DK_LEV_DP_LONG<32>(peq, n1, s2, n2, run); break;
-    case 9: case 10: d = DK_LEV_DP_LONG<(RMAX < 40 ? 4 : 40)>(peq, n1, s2, n2, run); break;
-    case 11: case 12: d = DK_LEV_DP_LONG<(RMAX < 48 ? 4 : 48)>(peq, n1, s2, n2, run); break;
-    case 13: case 14: d = DK_LEV_DP_LONG<(RMAX < 56 ? 4 : 56)>(peq, n1, s2, n2, run); break;
-    default: d = DK_LEV_DP_LONG<(RMAX < 64 ? 4 : 64)>(peq, n1, s2, n2, run); break;
+    case 5: d = DK_LEV_DP<20>(peq, n1, s2, n2, run); break;
+    case 6: d = DK_LEV_DP<24>(peq, n1, s2, n2, run); break;
+    case 7: d = DK_LEV_DP<28>(peq, n1, s2, n2, run); break;
+    case 8: d = DK_LEV_DP<32>(peq, n1, s2, n2, run); break;
+    case 9: case 10: d = DK_LEV_DP<(RMAX < 40 ? 4 : 40)>(peq, n1, s2, n2, run); break;
+    case 11: case 12: d = DK_LEV_DP<(RMAX < 48 ? 4 : 48)>(peq, n1, s2, n2, run); break;
+    case 13: case 14: d = DK_LEV_DP<(RMAX < 56 ? 4 : 56)>(peq, n1, s2, n2, run); break;
+    default: d = DK_LEV_DP<(RMAX < 64 ? 4 : 64)>(peq, n1, s2, n2, run); break;
   }
   if (run) {
     const int dist = min(d, len);
