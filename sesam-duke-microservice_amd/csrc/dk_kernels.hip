@@ -1296,8 +1296,8 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   const uint64_t s = slot0 + min(idx, nslots - 1);
   uint32_t qi = 0, g = 0;
   bool mirror = false;  // SYM: the candidate is a query too (the reverse pair is owned here)
-  int ksel = 0;         // SYM: key function of the slot and its bucket record
-  uint4 rsel = make_uint4(0, 0, 0, 0);
+  int ksel = 0;         // SYM: key function of the slot, and the query's offset in the
+  uint32_t moff = 0;    // candidate's mirror run (its own bucket position - the run's start)
   if (S.allpairs) {
     // slots of a query: [qi * mpad, qi * mpad + m), mpad = m rounded up to 64
     qi = (uint32_t)(s / S.mpad);
@@ -1329,7 +1329,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
             g = (uint32_t)(S.segoff[kk] + x);
             mirror = in_t;
             ksel = kk;
-            rsel = r;
+            moff = r.w - r.z;
           } else {
             t -= len;
           }
@@ -1413,7 +1413,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     // an entry -- the rest of that segment keeps its NaN fill
     if (in_launch) S.ores[s] = valid ? prob : __builtin_nan("");
     if (mirror && decide(prob2, P.threshold, P.maybe) != 0u)
-      S.mres[S.mbase[(uint64_t)ksel * S.nq + (crow - S.r0)] + (rsel.w - rsel.z)] = prob2;
+      S.mres[S.mbase[(uint64_t)ksel * S.nq + (crow - S.r0)] + moff] = prob2;
     block_emit(out, 0u, 0.0, 0u, qi, valid ? (mirror ? 2u : 1u) : 0u, bytes);  // operands read once
   } else {
     const uint32_t kind = valid ? decide(prob, P.threshold, P.maybe) : 0u;
