@@ -678,7 +678,8 @@ struct ColStage {
   int maxlen = 0, maxgrams = 0;
   std::vector<uint32_t> off;        // relative to the arena's current fill
   std::vector<uint16_t> len;
-  std::vector<uint8_t> bytes;       // the batch's units at the arena width
+  PodVec<uint8_t> bytes;            // the batch's units at the arena width (uninitialised:
+                                    // the fill writes every byte, padding included)
   std::vector<double> num;
   std::vector<uint8_t> numok;
   std::vector<uint32_t> goff;       // relative to the code list's current fill
@@ -734,17 +735,19 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
     return fail(DK_E_UNSUPPORTED, "property %d: arena over 4G units", pidx);
   S.units = cur;
   // pass 2: the units at the arena width (row ranges in parallel for large batches)
-  S.bytes.assign(cur * W, 0);
+  S.bytes.reset_uninit(cur * W);
   const uint8_t* u8 = (const uint8_t*)col->units;
   const uint16_t* u16 = (const uint16_t*)col->units;
   parallel_ranges(n, n >= (1u << 16) ? 4 : 1, [&](uint64_t lo, uint64_t hi) {
     for (uint64_t i = lo; i < hi; ++i) {
       if (S.len[i] == kMissing) continue;
       const uint64_t a = col->offsets[i], L = S.len[i];
+      const uint64_t padded = (L + align - 1) / align * align;
       uint8_t* d = S.bytes.data() + (uint64_t)S.off[i] * W;
       if (col->width == W) memcpy(d, (const uint8_t*)col->units + a * W, L * W);
       else  // u8 input into a u16 arena
         for (uint64_t k = 0; k < L; ++k) reinterpret_cast<uint16_t*>(d)[k] = u8[a + k];
+      memset(d + L * W, 0, (padded - L) * W);  // zero padding to the 4-byte boundary
     }
   });
   if (!is_num && !is_qg) return DK_OK;
@@ -837,9 +840,9 @@ static int commit_column(dk_ctx* c, int pidx, ColStage& S, uint64_t n, uint64_t 
 
 // Key ids of the batch for key function k (u64 keys as given, or key strings interned
 // exactly).  Interning a key of a batch that is later rejected only adds an unused id.
-static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, std::vector<uint64_t>& kv) {
+static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, uint64_t* kv) {
   const uint64_t n = b->n;
-  uint64_t* dst = kv.data() + (uint64_t)k * n;
+  uint64_t* dst = kv + (uint64_t)k * n;
   if (style == 1) {
     memcpy(dst, b->keys + (uint64_t)k * n, n * 8);
     return DK_OK;
@@ -855,10 +858,11 @@ static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, std::vector
   // the key strings as UTF-16 and their hashes (row ranges in parallel), then the ordered
   // insert into the key function's table
   const uint64_t base = n ? kc.offsets[0] : 0, tot = n ? kc.offsets[n] - base : 0;
-  std::vector<char16_t> wide;
+  PodVec<char16_t> wide;  // uninitialised: filled by the range workers
   const char16_t* units = reinterpret_cast<const char16_t*>(kc.units) + (kc.width == 2 ? base : 0);
-  std::vector<uint64_t> h(n);
-  if (kc.width == 1) wide.resize(tot);
+  PodVec<uint64_t> h;
+  h.reset_uninit(n);
+  if (kc.width == 1) wide.reset_uninit(tot);
   const uint8_t* u8 = (const uint8_t*)kc.units + base;
   parallel_ranges(n, n >= (1u << 16) ? 4 : 1, [&](uint64_t lo, uint64_t hi) {
     for (uint64_t i = lo; i < hi; ++i) {
@@ -874,8 +878,10 @@ static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, std::vector
   if (kc.width == 1) units = wide.data();
   auto& tab = c->intern[k];
   if (tab.size() + n >= (1ull << 31)) return fail(DK_E_UNSUPPORTED, "key function %d: over 2^31 keys", k);
-  std::vector<const char16_t*> ptr(n);
-  std::vector<uint32_t> ln(n);
+  PodVec<const char16_t*> ptr;
+  PodVec<uint32_t> ln;
+  ptr.reset_uninit(n);
+  ln.reset_uninit(n);
   for (uint64_t i = 0; i < n; ++i) {
     ptr[i] = units + (kc.offsets[i] - base);
     ln[i] = kc.offsets[i + 1] - kc.offsets[i];
@@ -994,13 +1000,14 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   // 1. validate + pack on the host (no index state changes): one task per property, key
   // function and the Lucene source, on their own threads for large batches
   std::vector<ColStage> cols(c->schema.nprops);
-  std::vector<uint64_t> kv((uint64_t)nk * n);
+  PodVec<uint64_t> kv;  // every entry written by its key function's task
+  kv.reset_uninit((uint64_t)nk * n);
   LuceneStage ls;
   const int np = c->schema.nprops, ntask = np + nk + (c->luc.on ? 1 : 0);
   {
     int rc = run_tasks(ntask, n >= 8192, [&](int t) {
       if (t < np) return stage_column(c, t, &b->columns[t], n, cols[t]);
-      if (t < np + nk) return stage_key(c, b, style, t - np, kv);
+      if (t < np + nk) return stage_key(c, b, style, t - np, kv.data());
       return stage_lucene(c, b, n, row0, transient, ls);
     });
     if (rc) return rc;

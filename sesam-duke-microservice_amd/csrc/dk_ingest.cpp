@@ -739,10 +739,14 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
   const int np = src->nprops, nk = src->nkeys;
   out.cols.assign(np + nk + 2, ColPart());
   const uint64_t n = out.e1 - out.e0;
+  // a value is at most as long as its JSON text (keys and IDs: their parts' lengths): the
+  // slice's bytes bound every column's units, so the buffers never grow and copy
+  const uint64_t bytes = n ? S.spans[out.e1 - 1].second - S.spans[out.e0].first : 0;
   for (auto& c : out.cols) {
     c.off.reserve(n + 1);
     c.present.reserve(n);
   }
+  for (int p = 0; p < np; ++p) out.cols[p].u.reserve(bytes / 2 + 64);
   out.deleted.reserve(n);
   out.hash.reserve(n);
   std::vector<Val> got(V.names.size()), side;
@@ -868,11 +872,11 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
 }
 
 // A packed column (owned by Packed)
-struct FinalCol {
-  std::vector<uint32_t> off;
-  std::vector<uint8_t> u8;
-  std::vector<uint16_t> u16;
-  std::vector<uint8_t> present;
+struct FinalCol {  // uninitialised storage: the merge workers first-touch their own slices
+  PodVec<uint32_t> off;
+  PodVec<uint8_t> u8;
+  PodVec<uint16_t> u16;
+  PodVec<uint8_t> present;
 };
 
 struct Packed {
@@ -905,11 +909,11 @@ void merge_columns(std::vector<Slice>& sl, uint64_t n, std::vector<FinalCol>& F,
     }
     if (L.ubase[T] >= (1ull << 32)) fail(DK_E_UNSUPPORTED, "a column of over 4G units in one batch");
     L.narrow = maxu <= 0xFF;
-    F[c].off.resize(n + 1);
+    F[c].off.reset_uninit(n + 1);
     F[c].off[0] = 0;
-    if (L.narrow) F[c].u8.resize(L.ubase[T] + 1);
-    else F[c].u16.resize(L.ubase[T] + 1);
-    if (L.missing) F[c].present.resize(n);
+    if (L.narrow) F[c].u8.reset_uninit(L.ubase[T] + 1);
+    else F[c].u16.reset_uninit(L.ubase[T] + 1);
+    if (L.missing) F[c].present.reset_uninit(n);
   }
   parallel_for(T, [&](int t) {
     const uint64_t r0 = sl[t].e0, m = sl[t].e1 - sl[t].e0;
