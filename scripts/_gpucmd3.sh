@@ -1,4 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-nproc > gpurun_out/ingest.log; cat /sys/fs/cgroup/cpu.max >> gpurun_out/ingest.log 2>&1
-timeout -k 10 300 python -u scripts/bench_ingest.py >> gpurun_out/ingest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gputest.log 2>&1

@@ -625,3 +625,34 @@ def test_link_database_written_in_bulk_equals_callbacks():
     assert got == want
     assert any(v[0] == R.RETRACTED for v in want.values())
     db.close()
+
+
+@pytest.mark.gpu
+def test_deduplicate_json_parallel_host_paths(monkeypatch):
+    """Batches large enough for every parallel host path (chunked split, slice parse, merge,
+    shard-parallel ID and key interning, parallel upsert staging): the POSTed-body path
+    equals the Record path, including a second batch that re-posts half the IDs."""
+    monkeypatch.setenv("DK_INGEST_THREADS", "8")
+    with open(os.path.join(GOLDEN, "testdukeconfig_schema.json")) as f:
+        cfg_d = json.load(f)["pipelines"]["Deduplication/countries-dbpedia-mondial"]
+    kf = [dh.PartsKey(("NAME", None, 0, 4)), dh.PartsKey(("CAPITAL", None, 0, 3))]
+    procs = []
+    for _ in range(2):
+        cfg = DukeConfig.from_dict(cfg_d)
+        procs.append(dh.GpuProcessor(cfg, dh.GpuBlockingDatabase(cfg, kf)))
+    first = stress_entities(36000, 21)
+    second = stress_entities(36000, 22)
+    for i, e in enumerate(second):
+        if i % 2 == 0:
+            e["_id"] = first[(i * 7) % len(first)]["_id"]   # re-posted IDs
+    for ents in (first, second):
+        body = json.dumps(ents)
+        src0 = procs[0].config.data_sources[0]
+        src1 = procs[1].config.data_sources[0]
+        ref = procs[0].deduplicate(dh.records_from_entities(dh.parse_entities(body)[0], src0))
+        got = procs[1].deduplicate_json(body, src1)
+        assert got.n == ref.n and got.pairs_scored == ref.pairs_scored and got.n > 0
+        for k in ("first", "candidate", "prob", "kind"):
+            assert np.array_equal(getattr(got, k), getattr(ref, k)), k
+    for p in procs:
+        p.database.close()
