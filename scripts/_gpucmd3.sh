@@ -1,3 +1,4 @@
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gputest.log 2>&1
+mkdir -p gpurun_out/trace
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace -o tr -- python3 bench.py --cpu-seconds 0 --pcie-steps 0 --no-warm-batch --no-json-batch > gpurun_out/trace/bench.log 2>&1
