@@ -1305,7 +1305,11 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     valid = valid && t < S.m;
     g = valid ? (uint32_t)t : 0u;
   } else {
-    qi = S.wq[s >> 6];  // one query per wave by construction (padded slot layout)
+    // one query per wave by construction (padded slot layout): the wave's first slot,
+    // computed wave-uniformly, so the map read is a scalar load at the head of the chain
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t sw = slot0 + min((uint64_t)blockIdx.x * blockDim.x + (uint64_t)wave * 64u, nslots - 1);
+    qi = S.wq[sw >> 6];
   }
   qi = __builtin_amdgcn_readfirstlane(qi);
   const uint32_t q = __builtin_amdgcn_readfirstlane(S.queries[qi]);
@@ -1316,9 +1320,22 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     // query's keys are wave-uniform.
     uint64_t t = s - S.qoff[qi];
     int k = -1;
-    for (int kk = 0; kk < S.nseg; ++kk) {
+    // the first kPre segments' ranges issued together (clamped: no branch around the loads);
+    // the loop is unrolled, so each segment's range is a register, not a serial load + wait
+    constexpr int kPre = 4;
+    uint4 pre4[kPre];
+    uint2 pre2[kPre];
+#pragma unroll
+    for (int kk = 0; kk < kPre; ++kk) {
+      const uint64_t at = (uint64_t)min(kk, S.nseg - 1) * S.nq + qi;
+      if (SYM) pre4[kk] = S.sranges[at];
+      else pre2[kk] = S.ranges[at];
+    }
+#pragma unroll
+    for (int kk = 0; kk < kMaxSegs; ++kk) {
+      if (kk >= S.nseg) break;  // wave-uniform
       if (SYM) {  // owned candidates: [lo, qa) then (pq, hi)
-        const uint4 r = S.sranges[(uint64_t)kk * S.nq + qi];
+        const uint4 r = kk < kPre ? pre4[kk < kPre ? kk : 0] : S.sranges[(uint64_t)kk * S.nq + qi];
         const bool in_t = r.w != kNoPos;
         const uint64_t nlow = r.z - r.x;
         const uint64_t len = nlow + (in_t ? (uint64_t)(r.y - r.w - 1) : 0);
@@ -1335,7 +1352,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
           }
         }
       } else {
-        const uint2 r = S.ranges[(uint64_t)kk * S.nq + qi];
+        const uint2 r = kk < kPre ? pre2[kk < kPre ? kk : 0] : S.ranges[(uint64_t)kk * S.nq + qi];
         const uint64_t len = (uint64_t)(r.y - r.x);
         if (k < 0) {
           if (t < len) {
