@@ -156,6 +156,28 @@ __device__ __forceinline__ void peq_set(uint64_t* peq, const CT* s, int n, bool 
   wave_lds_sync();
 }
 
+// the same with this lane's query unit already in a register (prefetched by the caller)
+template <typename CT>
+__device__ __forceinline__ void peq_set_unit(uint64_t* peq, uint32_t ch, int n, bool on) {
+  const int lane = (int)lane_id();
+  if (lane < n) {
+    const uint64_t bit = 1ull << lane;
+    if (sizeof(CT) == 1) {
+      if (on) atomicOr((unsigned long long*)&peq[ch], (unsigned long long)bit);
+      else peq[ch] = 0;
+    } else {
+      if (on) {
+        atomicOr((unsigned long long*)&peq[ch & 0xFF], (unsigned long long)bit);
+        atomicOr((unsigned long long*)&peq[256 + (ch >> 8)], (unsigned long long)bit);
+      } else {
+        peq[ch & 0xFF] = 0;
+        peq[256 + (ch >> 8)] = 0;
+      }
+    }
+  }
+  wave_lds_sync();
+}
+
 template <typename CT>
 __device__ __forceinline__ uint64_t peq_eq(const uint64_t* peq, uint32_t x) {
   if (sizeof(CT) == 1) return peq[x];
@@ -1112,7 +1134,7 @@ __device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool o
 template <int RMAX, int LR, typename CT, bool SYM>
 __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
-                                             int lc, bool cmp, double& rev) {
+                                             int lc, bool cmp, double& rev, uint32_t qch) {
   const CT* base = reinterpret_cast<const CT*>(D.units);
   const Str<CT> s1{reinterpret_cast<const uint32_t*>(base + D.off[q]), 1, 1 << 30};
   const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + g, rstride,
@@ -1143,7 +1165,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
     case DK_CMP_JAROWINKLER: {
       const bool table = lq <= 64 && (D.op == DK_CMP_LEVENSHTEIN || __ballot(cmp && lc > 64) == 0);
       if (table) {
-        peq_set(peq, base + D.off[q], lq, true);
+        peq_set_unit<CT>(peq, qch, lq, true);
         if (D.op == DK_CMP_LEVENSHTEIN) {
           sim = levenshtein_peq<RMAX>(peq, s1, lq, s2, lc, cmp);
         } else {
@@ -1152,7 +1174,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
                                    : jarowinkler_peq<uint64_t, CT, SYM>(peq, s1, lq, s2, lc, cmp, &r);
           if (SYM) rev = r;
         }
-        peq_set(peq, base + D.off[q], lq, false);
+        peq_set_unit<CT>(peq, qch, lq, false);
       } else if (cmp) {
         sim = jarowinkler(s1, lq, s2, lc);
         if (SYM) rev = lq == lc ? jarowinkler(s2, lc, s1, lq) : sim;
@@ -1383,11 +1405,32 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   double prob = P.raw_prop < 0 ? 0.5 : __builtin_nan("");
   double prob2 = 0.5;  // SYM: Processor.compare(candidate, query)
   uint32_t bytes = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
+  // property p+1's query length, this lane's query unit (its Peq bit) and the candidate's
+  // length are loaded while property p computes: a property then starts without the
+  // length -> offset -> unit chain of dependent loads
+  auto prefetch = [&](int pp, int& lq_, uint32_t& ch_, int& lc_) {
+    const DevProp& E = P.props[pp];
+    lq_ = (int)__builtin_amdgcn_readfirstlane((uint32_t)E.len[q]);
+    const int lane = (int)lane_id();
+    ch_ = 0u;
+    const bool table = E.op == DK_CMP_LEVENSHTEIN || E.op == DK_CMP_JAROWINKLER;  // Peq users
+    if (table && lq_ != (int)kMissing && lane < lq_ && lane < 64) {
+      const uint32_t o = __builtin_amdgcn_readfirstlane(E.off[q]);
+      ch_ = E.width == 1 ? (uint32_t)reinterpret_cast<const uint8_t*>(E.units)[o + lane]
+                         : (uint32_t)reinterpret_cast<const uint16_t*>(E.units)[o + lane];
+    }
+    lc_ = valid ? (int)__hip_atomic_load(E.rlen + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (int)kMissing;
+  };
+  int lq_n = 0, lc_n = (int)kMissing;
+  uint32_t qch_n = 0u;
+  if (P.nprops > 0) prefetch(0, lq_n, qch_n, lc_n);
   for (int p = 0; p < P.nprops; ++p) {
     const DevProp& D = P.props[p];
-    const int lq = (int)__builtin_amdgcn_readfirstlane((uint32_t)D.len[q]);
+    const int lq = lq_n;
+    const int lc = lc_n;
+    const uint32_t qch = qch_n;
+    if (p + 1 < P.nprops) prefetch(p + 1, lq_n, qch_n, lc_n);
     if (lq == (int)kMissing) continue;  // r1 has no value: property skipped for the wave
-    const int lc = valid ? (int)D.rlen[g] : (int)kMissing;
     const bool present = lc != (int)kMissing;
     const bool cmp = present && lq > 0 && lc > 0;
     double sim = 0.0, rev = 0.0;
@@ -1400,8 +1443,8 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       rev = sim;
     } else if (D.op != DK_CMP_NONE) {
       rev = __builtin_nan("");  // marks "same as sim" unless the comparator sets it
-      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev)
-                         : string_sim<RMAX, LR, uint16_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev);
+      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch)
+                         : string_sim<RMAX, LR, uint16_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch);
       if (!SYM || rev != rev) rev = sim;
       if (cmp) {
         if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2)
