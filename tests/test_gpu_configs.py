@@ -269,18 +269,22 @@ def upsert_slice(eng, vals, keys, ident, a, b, deleted=None):
                       key_columns=[dh.Column.from_strings(k[a:b]) for k in keys])
 
 
-def test_failed_upsert_leaves_index_unchanged():
+@pytest.mark.parametrize("sparse", [False, True])
+def test_failed_upsert_leaves_index_unchanged(sparse):
     """A batch rejected by dk_upsert (a Levenshtein value over 256 units) that re-posts
     already indexed IDs must not tombstone them; a valid re-post of those IDs in shuffled
-    positions afterwards supersedes them exactly once (Lucene delete-then-add)."""
+    positions afterwards supersedes them exactly once (Lucene delete-then-add).  sparse:
+    64-bit identities far above the row count (the ID map's hash side and its undo log)."""
     p, props, vals, keys = persons_case(600, 200, 31)
     n = len(vals[0])
     eng = dh.GpuEngine(schema_of(props, 0.9, 0.7, "dedup", 2))
-    ident = np.arange(n, dtype=np.uint64)
+    big = np.random.default_rng(5).choice(2 ** 62, size=n, replace=False).astype(np.uint64) + 2 ** 40
+    idmap = (lambda a: big[np.asarray(a, dtype=np.int64)]) if sparse else (lambda a: np.asarray(a, np.uint64))
+    ident = idmap(np.arange(n))
     upsert_slice(eng, vals, keys, ident, 0, 500)
     # batch 2: IDs 0..59 again + new ones, and one over-long ADDRESS value
     perm = np.random.default_rng(1).permutation(60)
-    b_ident = np.r_[perm, np.arange(500, n)].astype(np.uint64)
+    b_ident = idmap(np.r_[perm, np.arange(500, n)])
     b_vals = [[v[i] for i in perm] + v[500:] for v in vals]
     b_keys = [[k[i] for i in perm] + k[500:] for k in keys]
     bad = [list(col) for col in b_vals]
