@@ -20,10 +20,13 @@ already resident in HBM (its blocking tables are built by the first match after 
 upsert, in the warmup) and the match list left in HBM: `value` is that rate.  The boundary
 hands the MatchListener its list in host memory, so the same step with the list copied to
 pinned host memory is timed after it and reported as `pcie_inclusive` (never `value`).
-N>1: one process per GPU (torchrun), replicated index, query records split into contiguous
-tiles per rank; every rank keeps its list in HBM and the per-rank counts are all-gathered
-over RCCL (--gather none, default); --gather shm also copies each tile's list into its
-slice of one shared host mapping, --gather rccl gathers the lists to GPU 0 over xGMI.
+N>1: one process per GPU -- started by torch.distributed.run, or by this script itself when
+`--gpus N` is given without a launcher (WORLD_SIZE unset) -- replicated index, query records
+split into contiguous cost-weighted tiles per rank.  The result gather is inside the timed
+step: by default (--gather shm) every GPU copies its tile's list into its slice
+of one shared host mapping over its own host link, overlapped with scoring, and the per-rank
+counts are all-gathered over RCCL, after which rank 0 holds the node list; --gather rccl
+gathers the lists to GPU 0 over xGMI, --gather none leaves them in each rank's HBM.
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -64,15 +67,16 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the oracle baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="threads of the CPU baseline (0 = every host core, os.cpu_count())")
+                    help="threads of the CPU baseline (0 = the CPUs this job may use: the "
+                         "smaller of its affinity set and its cgroup CPU quota)")
     ap.add_argument("--cpu-single-seconds", type=float, default=6.0,
                     help="target CPU time of the single-core baseline sample (0 = skip)")
-    ap.add_argument("--gather", default="none", choices=["none", "shm", "rccl"],
-                    help="N>1 result path inside the timed steps: none = each rank's match "
-                         "list stays in its HBM and only the per-rank counts are all-gathered "
-                         "(the device-resident `value`); shm = every GPU also copies its "
-                         "tile's list into its slice of one shared host mapping (rank 0 reads "
-                         "it in place); rccl = device lists gathered to GPU 0 over xGMI")
+    ap.add_argument("--gather", default=None, choices=["none", "shm", "rccl"],
+                    help="N>1 result path inside the timed steps (default shm): shm = every "
+                         "GPU copies its tile's list into its slice of one shared host mapping "
+                         "(rank 0 reads the node list in place: SURVEY §8d's result gather); "
+                         "rccl = device lists gathered to GPU 0 over xGMI; none = each rank's "
+                         "list stays in its HBM, only the per-rank counts are all-gathered")
     ap.add_argument("--pcie-steps", type=int, default=3,
                     help="N=1: extra steps with the match list copied to pinned host memory "
                          "(the PCIe-inclusive rate, reported beside `value`; 0 = skip)")
@@ -211,15 +215,101 @@ def make_schema(w):
     return s
 
 
+def bpair_s8d(w, counts):
+    """SURVEY §8(d)'s algorithmic bytes per scored pair (the unamortised operand stream):
+    B_pair = 8 (two u32 row ids) + 1 (decision) + per string property 2·(4 + L̄·w)
+           + per numeric property 2·8 + per q-gram property 2·(4 + Ḡ·g),
+    L̄ / Ḡ the mean units / unique grams per value over the scored pairs (here: the query
+    side weighted by each query's candidate count -- both sides of a pair come from the same
+    generator in every config), w the stored unit width (1 Latin-1, 2 UTF-16), g the packed
+    gram bytes (u32 codes for q <= 2, u64 above).  Returns (B_pair, per-property detail)."""
+    from dukehip import _abi as A
+    qs = np.asarray(w["queries"], dtype=np.int64)
+    wt = np.asarray(counts, dtype=np.float64)
+    tot = wt.sum()
+    if tot <= 0:
+        return None, {}
+    b, detail = 9.0, {}
+    for p in w["props"]:
+        vals = w["values"][p["name"]]
+        sel = [vals[i] for i in qs]
+        if p["comparator"] == A.CMP_NUMERIC:
+            b += 16.0
+            detail[p["name"]] = {"bytes": 16.0}
+            continue
+        lens = np.fromiter((len(s) if s else 0 for s in sel), np.float64, len(sel))
+        wid = 2 if any(s and max(map(ord, s)) > 255 for s in sel[:20000]) else 1
+        if p["comparator"] == A.CMP_QGRAM:
+            qq = int(p.get("q", 2))
+            g = np.fromiter((len({s[i:i + qq] for i in range(len(s) - qq + 1)}) if s else 0
+                             for s in sel), np.float64, len(sel))
+            gbar = float((g * wt).sum() / tot)
+            gb = 4 if qq <= 2 else 8
+            pb = 2.0 * (4 + gbar * gb)
+            detail[p["name"]] = {"grams": gbar, "gram_bytes": gb, "bytes": pb}
+        else:
+            lbar = float((lens * wt).sum() / tot)
+            pb = 2.0 * (4 + lbar * wid)
+            detail[p["name"]] = {"units": lbar, "width": wid, "bytes": pb}
+        b += pb
+    return b, detail
+
+
 CMP_NAMES = {1: "Levenshtein", 2: "JaroWinkler", 3: "QGramComparator", 4: "ExactComparator",
              5: "NumericComparator", 6: "WeightedLevenshtein", 7: "DiceCoefficientComparator",
              8: "JaccardIndexComparator"}
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nranks, argv=None, port=None, script=None):
+    """`bench.py --gpus N` started without a launcher: start the N ranks here, one child
+    process per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), the
+    same environment torch.distributed.run gives them.  This process never touches the GPU
+    (no torch import, no HIP call), so the children start clean; rank 0 prints the line.
+    Returns the first non-zero child exit status (the others are then stopped), else 0."""
+    import signal
+    import subprocess
+    argv = sys.argv[1:] if argv is None else argv
+    port = port or free_port()
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__),
+                                       *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for o in live:            # one rank failed: the collectives would hang
+                    o.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
+    if args.gather is None:
+        args.gather = "shm" if world > 1 else "none"
     heartbeat(rank)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -422,7 +512,17 @@ def main():
     if rank == 0:
         launches = max(1, prof["score_launches"])
         score_s = prof["ms_score"] / 1e3
-        achieved = prof["score_bytes"] / score_s if score_s > 0 else 0.0
+        # roofline.achieved: SURVEY §8(d)'s B_pair x the pairs one k_score launch scores, over
+        # the launch's HIP-event time on the ctx stream
+        if world == 1:
+            counts = eng.candidate_counts(allq)
+        bpair, bdetail = bpair_s8d(w, counts)
+        pairs_launch = prof["pairs_scored"] / launches
+        avg_launch_s = score_s / launches
+        achieved = bpair * pairs_launch / avg_launch_s if avg_launch_s > 0 and bpair else 0.0
+        # the kernel's own operand bytes (the query side LDS-resident, the symmetric schedule's
+        # candidate operands read once per pair): what the schedule actually has to move
+        sched = prof["score_bytes"] / score_s if score_s > 0 else 0.0
         traffic = None
         valu = None
         # the kept PMC summary of this workload's scoring kernel (scripts/summarize_profiles.py)
@@ -478,10 +578,17 @@ def main():
             "index_build_s": t_index,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                         "frac_s8d": achieved / HBM_PEAK,
                          "traffic": traffic,
                          "kernel": "k_score", "launches": prof["score_launches"],
                          "avg_launch_ms": prof["ms_score"] / launches,
-                         "bytes_per_launch": prof["score_bytes"] / launches,
+                         "pairs_per_launch": pairs_launch,
+                         "b_pair_s8d": bpair, "b_pair_detail": bdetail,
+                         "bytes_per_launch": bpair * pairs_launch if bpair else None,
+                         # the same B_pair over the whole step (every kernel + the gather)
+                         "frac_step": (bpair * value / (HBM_PEAK * world)) if bpair else None,
+                         "operand_bytes_per_launch": prof["score_bytes"] / launches,
+                         "frac_operand_bytes": sched / HBM_PEAK,
                          "limiter": "valu" if valu else None, "valu": valu},
             "pcie_inclusive": pcie,
             # per-rank pairs scored of the last step (tile balance; N>1)
@@ -597,7 +704,9 @@ def cpu_baseline(w, gpu_res, args):
     ot = O.OracleTable(props, [w["values"][p["name"]] for p in w["props"]], keys=w["keys"],
                        group=w["group"], threshold=w["threshold"], maybe=w["maybe"], mode=mode)
     nproc = os.cpu_count() or 1
-    threads = args.cpu_threads or nproc
+    affinity, quota = host_cpus()
+    effective = max(1, min(affinity or nproc, int(-(-quota // 1)) if quota else nproc))
+    threads = args.cpu_threads or effective
     allq = w["queries"]
 
     def sample(nthreads, seconds):
@@ -627,6 +736,27 @@ def cpu_baseline(w, gpu_res, args):
             cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except OSError:
         pass
+    out = {"value": r["pairs_scored"] / (r["ms_score"] / 1e3), "unit": "pairs/s",
+           # the CPUs the threads actually ran on: min(threads, affinity, cgroup quota)
+           "cores": min(threads, effective), "threads": threads,
+           "kind": "port",
+           "sample": f"first {s} of {len(allq)} query records ({r['pairs_scored']} pairs), "
+                     f"scoring loop timed, blocking-index build excluded ({r['ms_index']:.0f} ms)",
+           "seconds": r["ms_score"] / 1e3, "cpu_model": cpu, "host_nproc": nproc,
+           "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+           "matches_identical_to_gpu": bool(ok), "single_core": single}
+    if single:
+        # EXTRAPOLATION, not a measurement: the single-core rate x every hardware thread the
+        # host reports (linear scaling, an upper bound of the whole node's CPU rate; this job
+        # may only use `cores` of them)
+        out["extrapolated_all_host_threads"] = {
+            "value": single["value"] * nproc, "threads": nproc,
+            "note": "single-core rate x host_nproc, linear (extrapolated, not measured)"}
+    return out
+
+
+def host_cpus():
+    """(CPUs in this process's affinity set, cgroup v2 CPU quota in CPUs or None)."""
     try:
         affinity = len(os.sched_getaffinity(0))
     except OSError:
@@ -638,18 +768,7 @@ def cpu_baseline(w, gpu_res, args):
             quota = None if q == "max" else float(q) / float(per)
     except (OSError, ValueError):
         pass
-    out = {"value": r["pairs_scored"] / (r["ms_score"] / 1e3), "unit": "pairs/s", "cores": threads,
-           "kind": "port",
-           "sample": f"first {s} of {len(allq)} query records ({r['pairs_scored']} pairs), "
-                     f"scoring loop timed, blocking-index build excluded ({r['ms_index']:.0f} ms)",
-           "seconds": r["ms_score"] / 1e3, "cpu_model": cpu, "host_nproc": nproc,
-           "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
-           "matches_identical_to_gpu": bool(ok), "single_core": single}
-    if single:
-        # what nproc cores would reach at the single-core rate (linear scaling: an upper
-        # bound of the host's all-core rate, the conservative denominator for GPU/CPU)
-        out["all_core_linear_bound"] = single["value"] * nproc
-    return out
+    return affinity, quota
 
 
 def cpu_baseline_lucene(w, gpu_res, O):

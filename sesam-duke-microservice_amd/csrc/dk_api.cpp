@@ -45,6 +45,22 @@ static int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// The exception barrier of every C-ABI entry and host task: nothing C++ crosses the boundary
+// (an escaping exception would std::terminate the JVM / Python host).  Out of host memory is
+// DK_E_NOMEM; RAII undo logs (dk_upsert's Rollback) have run by the time it is returned.
+template <typename F>
+static int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return fail(DK_E_NOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(DK_E_DEVICE, "internal error: %s", e.what());
+  } catch (...) {
+    return fail(DK_E_DEVICE, "internal error");
+  }
+}
+
 #define HIPCHK(expr)                                                                 \
   do {                                                                               \
     hipError_t e_ = (expr);                                                          \
@@ -98,7 +114,7 @@ static int run_tasks(int n, bool parallel, F&& task) {
   std::vector<int> rc(n, DK_OK);
   std::vector<std::string> msg(n);
   auto one = [&](int i) {
-    rc[i] = task(i);
+    rc[i] = guarded([&] { return task(i); });
     if (rc[i] != DK_OK) msg[i] = g_err;
   };
   if (!parallel || n <= 1) {
@@ -108,10 +124,7 @@ static int run_tasks(int n, bool parallel, F&& task) {
     }
     return DK_OK;
   }
-  std::vector<std::thread> th;
-  for (int i = 1; i < n; ++i) th.emplace_back(one, i);
-  one(0);
-  for (auto& t : th) t.join();
+  dk_run_parts(n, one);  // `one` does not throw
   for (int i = 0; i < n; ++i)
     if (rc[i] != DK_OK) {
       g_err = msg[i];
@@ -134,16 +147,14 @@ struct HostLap {
 };
 
 // f(lo, hi) over [0, n) in `parts` contiguous ranges on their own threads
+// (an exception of any range is rethrown on the caller once every thread has joined)
 template <typename F>
 static void parallel_ranges(uint64_t n, int parts, F&& f) {
   if (parts <= 1 || n < 2u * (uint64_t)parts) {
     f((uint64_t)0, n);
     return;
   }
-  std::vector<std::thread> th;
-  for (int t = 1; t < parts; ++t) th.emplace_back([&f, n, parts, t] { f(n * t / parts, n * (t + 1) / parts); });
-  f((uint64_t)0, n / parts);
-  for (auto& x : th) x.join();
+  dk_run_parts(parts, [&](int t) { f(n * t / parts, n * (t + 1) / parts); });
 }
 
 // ----------------------------------------------------------------------------------------
@@ -564,7 +575,7 @@ extern "C" int dk_fail_ingest(int code, const char* msg) { return fail(code, "%s
 
 int dk_abi_version(void) { return DK_ABI_VERSION; }
 
-int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
+static int create_impl(const dk_schema* schema, int device, dk_ctx** out) {
   if (!out) return fail(DK_E_INVALID, "out is NULL");
   *out = nullptr;
   int rc = validate_schema(schema);
@@ -610,6 +621,10 @@ int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
   }
   *out = c;
   return DK_OK;
+}
+
+int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
+  return guarded([&] { return create_impl(schema, device, out); });
 }
 
 void dk_destroy(dk_ctx* c) {
@@ -997,6 +1012,19 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   if (row0 + n >= (1ull << 29))
     return fail(DK_E_UNSUPPORTED, "index would exceed %u rows", 1u << 29);
 
+  // 0. the columns' structure, before any task reads them: the staging tasks run
+  // concurrently, and the Lucene task reads the lookup columns that a column task is still
+  // validating (a NULL or non-monotone offsets array must be DK_E_INVALID, not a crash)
+  for (int p = 0; p < c->schema.nprops; ++p) {
+    const dk_column& col = b->columns[p];
+    if (!col.offsets || (!col.units && col.offsets[n] != col.offsets[0]))
+      return fail(DK_E_INVALID, "property %d: offsets/units missing", p);
+    if (col.width != 1 && col.width != 2)
+      return fail(DK_E_INVALID, "property %d: width %d (1 or 2)", p, col.width);
+    for (uint64_t i = 0; i < n; ++i)
+      if (col.offsets[i + 1] < col.offsets[i])
+        return fail(DK_E_INVALID, "property %d: offsets not monotone at %llu", p, (unsigned long long)i);
+  }
   // 1. validate + pack on the host (no index state changes): one task per property, key
   // function and the Lucene source, on their own threads for large batches
   std::vector<ColStage> cols(c->schema.nprops);
@@ -1036,15 +1064,27 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     undo.emplace_back(b->ident[i], old);
     c->ident_row.set(b->ident[i], (uint32_t)(row0 + i));
   }
+  struct Mark {
+    uint64_t units, grams;
+    int maxlen, maxgrams, width;
+  };
   struct Rollback {
     dk_ctx* c;
     std::vector<std::pair<uint64_t, uint32_t>>* undo;
+    std::vector<Mark> marks;  // per property, taken before the commit
     bool armed = true;
     ~Rollback() {
       if (!armed) return;
       for (auto it = undo->rbegin(); it != undo->rend(); ++it) c->ident_row.set(it->first, it->second);
+      for (size_t p = 0; p < marks.size(); ++p) {
+        c->P[p].units_used = marks[p].units;
+        c->P[p].grams_used = marks[p].grams;
+        c->P[p].maxlen = marks[p].maxlen;
+        c->P[p].maxgrams = marks[p].maxgrams;
+        c->P[p].width = marks[p].width;
+      }
     }
-  } rollback{c, &undo};
+  } rollback{c, &undo, {}};
 
   lap("ident");
   // 2. device space (contents preserved; nothing logical changes on failure)
@@ -1079,10 +1119,8 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     HIPCHK(hipMemcpyAsync(c->group.as<uint8_t>() + row0, b->group, n, hipMemcpyHostToDevice, s));
   else
     HIPCHK(hipMemsetAsync(c->group.as<uint8_t>() + row0, 0, n, s));
-  if (!dead.empty()) {
-    HIPCHK(hipMemcpyAsync(d_dead.p, dead.data(), dead.size() * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_clear_flag(c->flags.as<uint8_t>(), d_dead.as<uint32_t>(), dead.size(), kAlive, s));
-  }
+  // the arena fill marks are restored if a device step below fails (Rollback)
+  for (auto& p : c->P) rollback.marks.push_back({p.units_used, p.grams_used, p.maxlen, p.maxgrams, p.width});
   for (int p = 0; p < c->schema.nprops; ++p) {
     int rc = commit_column(c, p, cols[p], n, row0);
     if (rc) return rc;
@@ -1107,6 +1145,12 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     HIPCHK(hipMemcpyAsync(L.qoff_d.as<uint64_t>() + row0 + 1, ls.qoff.data(), n * 8,
                           hipMemcpyHostToDevice, s));
   }
+  // last device step: the superseded versions stop being alive (their identities already
+  // map to the new rows); nothing after it can fail but the synchronisation itself
+  if (!dead.empty()) {
+    HIPCHK(hipMemcpyAsync(d_dead.p, dead.data(), dead.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_clear_flag(c->flags.as<uint8_t>(), d_dead.as<uint32_t>(), dead.size(), kAlive, s));
+  }
   HIPCHK(hipStreamSynchronize(s));  // host staging goes out of scope
   lap("copy");
   if (L.on) {
@@ -1126,17 +1170,17 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
 }
 
 int dk_upsert(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
-  return upsert_rows(c, b, rows_out, false);
+  return guarded([&] { return upsert_rows(c, b, rows_out, false); });
 }
 
 // IncrementalLuceneDatabase.setIndexingIsDisabled(true) (:95-96, :498-512) around the
 // httptransform batch (App.java:1130-1132, 1174-1175): the batch is matched against the
 // index without entering it.
 int dk_upsert_transient(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
-  return upsert_rows(c, b, rows_out, true);
+  return guarded([&] { return upsert_rows(c, b, rows_out, true); });
 }
 
-int dk_drop_transient(dk_ctx* c) {
+static int drop_transient_impl(dk_ctx* c) {
   if (!c) return fail(DK_E_INVALID, "NULL argument");
   if (!c->transient) return DK_OK;
   HIPCHK(hipSetDevice(c->device));
@@ -1153,6 +1197,10 @@ int dk_drop_transient(dk_ctx* c) {
   }
   c->transient = false;
   return DK_OK;
+}
+
+int dk_drop_transient(dk_ctx* c) {
+  return guarded([&] { return drop_transient_impl(c); });
 }
 
 // ----------------------------------------------------------------------------------------
@@ -2123,7 +2171,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   return DK_OK;
 }
 
-int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out) {
+static int match_impl(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out) {
   if (!c || !out) return fail(DK_E_INVALID, "NULL argument");
   *out = nullptr;
   if (nq && !query_rows) return fail(DK_E_INVALID, "query_rows is NULL");
@@ -2156,10 +2204,14 @@ int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_r
   return DK_OK;
 }
 
+int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out) {
+  return guarded([&] { return match_impl(c, query_rows, nq, flags, out); });
+}
+
 // Per-query candidate counts of the blocking contract (the sum of the query's bucket
 // sizes over the key functions, before the isSameAs / duplicate filters): the cost model
 // of the multi-GPU query tiles.  ALLPAIRS: every query gets the usable rows.
-int dk_candidate_counts(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, uint64_t* counts) {
+static int candidate_counts_impl(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, uint64_t* counts) {
   if (!c || (nq && (!query_rows || !counts))) return fail(DK_E_INVALID, "NULL argument");
   for (uint64_t i = 0; i < nq; ++i)
     if (query_rows[i] >= c->nrows)
@@ -2186,6 +2238,10 @@ int dk_candidate_counts(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, uint
   HIPCHK(hipMemcpyAsync(counts, c->counts.p, nq * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return DK_OK;
+}
+
+int dk_candidate_counts(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, uint64_t* counts) {
+  return guarded([&] { return candidate_counts_impl(c, query_rows, nq, counts); });
 }
 
 int dk_result_copy_to_device(const dk_result* r, uint64_t* first, uint32_t* candidate,
@@ -2219,7 +2275,7 @@ int dk_result_region_layout(uint64_t bytes, uint64_t max_queries, dk_region_layo
   return DK_OK;
 }
 
-int dk_set_result_region(dk_ctx* c, void* base, uint64_t bytes, uint64_t max_queries) {
+static int set_result_region_impl(dk_ctx* c, void* base, uint64_t bytes, uint64_t max_queries) {
   if (!c) return fail(DK_E_INVALID, "ctx is NULL");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->copy_stream));
@@ -2246,6 +2302,10 @@ int dk_set_result_region(dk_ctx* c, void* base, uint64_t bytes, uint64_t max_que
   return DK_OK;
 }
 
+int dk_set_result_region(dk_ctx* c, void* base, uint64_t bytes, uint64_t max_queries) {
+  return guarded([&] { return set_result_region_impl(c, base, bytes, max_queries); });
+}
+
 void dk_free_result(dk_result* r) {
   if (!r) return;
   ResultHolder* R = reinterpret_cast<ResultHolder*>(r);  // dk_result is the first member
@@ -2259,17 +2319,25 @@ void dk_free_result(dk_result* r) {
 // replica and the result pools are untouched, so dk_match after a compare reuses them.
 static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double* prob);
 
-int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
+static int compare_rows_impl(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
   return compare_one(c, r1, r2, -1, prob);
+}
+
+int dk_compare_rows(dk_ctx* c, uint32_t r1, uint32_t r2, double* prob) {
+  return guarded([&] { return compare_rows_impl(c, r1, r2, prob); });
 }
 
 // Comparator.compare(v1, v2) of property `prop` (the raw similarity PropertyImpl maps to a
 // probability) for two indexed rows, through the production scoring kernel.
-int dk_property_similarity(dk_ctx* c, int prop, uint32_t r1, uint32_t r2, double* sim) {
+static int property_similarity_impl(dk_ctx* c, int prop, uint32_t r1, uint32_t r2, double* sim) {
   if (!c || !sim) return fail(DK_E_INVALID, "NULL argument");
   if (prop < 0 || prop >= c->schema.nprops)
     return fail(DK_E_INVALID, "property %d out of range [0, %d)", prop, c->schema.nprops);
   return compare_one(c, r1, r2, prop, sim);
+}
+
+int dk_property_similarity(dk_ctx* c, int prop, uint32_t r1, uint32_t r2, double* sim) {
+  return guarded([&] { return property_similarity_impl(c, prop, r1, r2, sim); });
 }
 
 static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double* prob) {
@@ -2334,7 +2402,7 @@ static void clear_index(dk_ctx* c) {
   }
 }
 
-int dk_compare_values(dk_ctx* c, const dk_batch* pair, double* prob) {
+static int compare_values_impl(dk_ctx* c, const dk_batch* pair, double* prob) {
   if (!c || !pair || !prob) return fail(DK_E_INVALID, "NULL argument");
   if (pair->n != 2) return fail(DK_E_INVALID, "dk_compare_values takes a batch of 2 records (r1, r2)");
   if (!c->pair_ctx) {
@@ -2359,6 +2427,10 @@ int dk_compare_values(dk_ctx* c, const dk_batch* pair, double* prob) {
   int rc = upsert_rows(pc, &b, nullptr, false);
   if (rc) return rc;
   return dk_compare_rows(pc, 0, 1, prob);
+}
+
+int dk_compare_values(dk_ctx* c, const dk_batch* pair, double* prob) {
+  return guarded([&] { return compare_values_impl(c, pair, prob); });
 }
 
 int dk_set_overwrite(dk_ctx* c, int on) {

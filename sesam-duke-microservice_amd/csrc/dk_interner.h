@@ -16,9 +16,43 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <new>
 #include <thread>
 #include <vector>
+
+// f(i) for i < n, parts 1.. on their own threads and part 0 on the caller's.  Exception-safe:
+// a thread that cannot be started runs its part on the caller instead, every started thread
+// is joined, and the first exception any part threw is rethrown on the caller afterwards (an
+// exception escaping a std::thread would std::terminate the host process -- the JVM).
+template <typename F>
+inline void dk_run_parts(int n, F&& f) {
+  if (n <= 1) {
+    if (n == 1) f(0);
+    return;
+  }
+  std::vector<std::exception_ptr> err((size_t)n);
+  auto part = [&](int i) {
+    try {
+      f(i);
+    } catch (...) {
+      err[(size_t)i] = std::current_exception();
+    }
+  };
+  std::vector<std::thread> th;
+  int started = 1;
+  try {
+    th.reserve((size_t)n - 1);
+    for (; started < n; ++started) th.emplace_back(part, started);
+  } catch (...) {
+    // no more threads: the remaining parts run here
+  }
+  part(0);
+  for (int i = started; i < n; ++i) part(i);
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
 
 // A growable array of trivially copyable T whose growth leaves the new tail unwritten, so
 // the workers that fill it also take its first-touch page faults, in parallel.
@@ -72,9 +106,9 @@ struct PodVec {
   }
   void reset_uninit(uint64_t m) {  // m elements, old contents dropped, nothing written
     if (m > cap) {
+      T* q = alloc(m);  // first: a failed allocation leaves the vector as it was
       free(p);
-      p = nullptr;
-      p = alloc(m);
+      p = q;
       cap = m;
     }
     n = m;
@@ -224,8 +258,19 @@ struct U16Table {
       for (int s = 0; s < kShards; ++s) need = std::max(need, fill[s] + miss[s]);
     }
     ensure_all(need, T);
-    // per shard, in batch order: existing id, or provisional (kProv | first index)
+    // Every allocation happens before the first provisional slot is written (the workers
+    // and the numbering pass below allocate nothing): a std::bad_alloc leaves the table as
+    // it was.  Worst case: every string of the batch is new.
     std::vector<std::vector<uint64_t>> placed(kShards);  // slot positions of new strings
+    uint64_t units_max = 0;
+    for (int s = 0; s < kShards; ++s) placed[s].reserve(shard_lo[s + 1] - shard_lo[s]);
+    for (uint64_t i = 0; i < cnt; ++i) units_max += n[i];
+    arena.reserve(arena.size() + units_max);
+    start.reserve(start.size() + cnt);
+    hashes.reserve(hashes.size() + cnt);
+    std::vector<uint32_t> fresh;
+    fresh.reserve(cnt);
+    // per shard, in batch order: existing id, or provisional (kProv | first index)
     run(T, [&](int t) {
       for (int s = t; s < kShards; s += T) {
         uint64_t* sh = slots.data() + (uint64_t)s * shard_cap;
@@ -266,7 +311,6 @@ struct U16Table {
     // number the new strings in first-appearance order
     const uint64_t id0 = size();
     uint64_t nid = id0, units = 0;
-    std::vector<uint32_t> fresh;
     for (uint64_t i = 0; i < cnt; ++i) {
       const uint64_t v = out[i];
       if (!(v & kProv)) continue;
@@ -317,10 +361,7 @@ struct U16Table {
  private:
   template <typename F>
   static void run(int T, F&& f) {
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back([&f, t] { f(t); });
-    f(0);
-    for (auto& x : th) x.join();
+    dk_run_parts(T, f);
   }
   void place(uint64_t h, uint64_t id) {
     const int s = shard_of(h);

@@ -158,3 +158,43 @@ def test_reference_pipeline_on_lucene_semantics():
         total += res.n
     assert total > 100
     db.close()
+
+
+@pytest.mark.parametrize("defect", ["nonmonotone", "null_offsets"])
+def test_malformed_large_batch_rejected(defect):
+    """A batch of >= 8192 rows stages its columns and the Lucene source on concurrent
+    threads; a malformed lookup column (offsets running backwards, or no offsets at all) must
+    be DK_E_INVALID with the index unchanged -- not a crash in the Lucene task."""
+    p = synth.persons(9000, 1000, seed=63)
+    vals = [p["name"], p["address"], p["dob"]]
+    n = len(vals[0])
+    ident = np.arange(n, dtype=np.uint64)
+    sch = schema_of(PROPS, 0.9, 0.7, "dedup", 0)
+    A.lucene_source(sch, [0, 1], 10, 0.9)
+    eng = dh.GpuEngine(sch)
+    upsert(eng, vals, ident, 0, 500)
+    cols = [dh.Column.from_strings(v) for v in vals]
+    bad = cols[0]
+    if defect == "nonmonotone":
+        bad.offsets = bad.offsets.copy()
+        bad.offsets[5000] = bad.offsets[5001] + 7    # offsets[5001] < offsets[5000]
+        raw = [c.c() for c in cols]
+    else:
+        raw = [c.c() for c in cols]
+        raw[0].offsets = None
+    arr = (A.dk_column * len(raw))(*raw)
+    b = A.dk_batch()
+    b.n = n
+    b.ident = ident.ctypes.data
+    b.columns = arr
+    rc = eng.lib.dk_upsert(eng.ctx, A.C.byref(b), None)
+    assert rc == A.DK_E_INVALID, (rc, eng.lib.dk_last_error())
+    assert eng.num_rows == 500
+    q = np.arange(500, dtype=np.uint32)
+    in_index = np.ones(500, bool)
+    want, scored = expected(PROPS, [v[:500] for v in vals], [0, 1], ident[:500], in_index,
+                            np.zeros(500, np.uint8), None, q, 0.9, 0.7, 10, 0.9, "dedup")
+    res = eng.match(q)
+    check(res, want, scored)
+    res.close()
+    eng.close()
