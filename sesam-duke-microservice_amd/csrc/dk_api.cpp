@@ -340,7 +340,14 @@ struct PropState {
   int maxlen = 0;
   int maxgrams = 0;        // longest code list of a value
   DevBuf off, len, units, num, numok, goff, gcnt, grams;
+  DevBuf gseed;            // Latin-1 bigram sets: per-row perfect-hash seed (DevProp::g16)
 };
+
+// QGram q = 2 without positions: its codes are bigrams, which a width-1 (Latin-1) arena packs
+// as 16-bit keys with a per-row perfect hash (DevProp::g16)
+static bool bigram_prop(const dk_property& p) {
+  return p.comparator == DK_CMP_QGRAM && p.qgram_q == 2 && p.qgram_tokenizer != DK_QGRAM_POSITIONAL;
+}
 
 // One property's candidate replica (see dk_internal.h): values in replica-position order.
 // The blocking tables own one set (index state); dk_compare_rows builds its own one-position
@@ -348,6 +355,7 @@ struct PropState {
 struct Replica {
   int rlmax = 0;
   int rgmax = 0;
+  int g16 = 0, rgrows = 0;  // bigram-key replica: u64 word rows per position
   int width = 0;
   uint64_t npos = 0;  // positions the buffers are laid out for (the transposed stride)
   DevBuf rlen, runits, rnum, rnumok, rgoff, rgcnt, rgrams;
@@ -502,6 +510,7 @@ static hipError_t grow_rows(dk_ctx* c, uint64_t need) {
       GROW(p.goff, uint32_t);
       GROW(p.gcnt, uint16_t);
     }
+    if (bigram_prop(p.cfg)) GROW(p.gseed, uint16_t);
   }
 #undef GROW
   c->cap = nc;
@@ -1124,6 +1133,12 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   for (int p = 0; p < c->schema.nprops; ++p) {
     int rc = commit_column(c, p, cols[p], n, row0);
     if (rc) return rc;
+    // a Latin-1 bigram property: the new rows' perfect-hash seeds (once the arena is wide,
+    // bigram keys are never used again, and neither are seeds)
+    PropState& P = c->P[p];
+    if (bigram_prop(P.cfg) && P.width == 1)
+      HIPCHK(launch_gram_seed(P.grams.as<uint64_t>(), P.goff.as<uint32_t>(), P.gcnt.as<uint16_t>(),
+                              P.len.as<uint16_t>(), row0, n, P.gseed.as<uint16_t>(), s));
   }
   for (int k = 0; k < nk; ++k)
     HIPCHK(hipMemcpyAsync(c->keys[k].as<uint64_t>() + row0, kv.data() + (uint64_t)k * n, n * 8,
@@ -1311,6 +1326,9 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
     D.rgrams = R.rgrams.p;
     D.rgmax = R.rgmax;
     D.rg32 = 16 * S.cfg.qgram_q + (S.cfg.qgram_tokenizer == DK_QGRAM_POSITIONAL ? 16 : 0) <= 32;
+    D.g16 = R.g16;
+    D.rgrows = R.rgrows;
+    D.gseed = S.gseed.as<uint16_t>();
   }
   return P;
 }
@@ -1318,7 +1336,7 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
 // Candidate replica: every property's candidate-side values in replica order, units
 // transposed ([unit][position]) for values of at most kMaxReplicaUnits units.  The layout
 // (units / codes per value, width) follows the index's current longest values.
-struct ReplicaShape { int rlmax, rgmax, width, rgw; };
+struct ReplicaShape { int rlmax, rgmax, width, rgw, rgrows; };
 
 static ReplicaShape replica_shape(const PropState& S) {
   const int op = S.cfg.comparator;
@@ -1331,6 +1349,12 @@ static ReplicaShape replica_shape(const PropState& S) {
   // codes pack 16 bits per unit (+16 for the POSITIONAL index): q <= 2 fits in a u32
   const int gram_bits = 16 * S.cfg.qgram_q + (S.cfg.qgram_tokenizer == DK_QGRAM_POSITIONAL ? 16 : 0);
   sh.rgw = gram_bits <= 32 ? 4 : 8;
+  // Latin-1 bigrams: 16-bit keys, four per u64 word, an even number of word rows (k_score
+  // reads two word rows per step)
+  if (sh.rgmax && bigram_prop(S.cfg) && sh.width == 1) {
+    sh.rgw = 2;
+    sh.rgrows = std::max(2, ((sh.rgmax + 3) / 4 + 1) & ~1);
+  }
   return sh;
 }
 
@@ -1339,7 +1363,9 @@ static bool replica_fits(const dk_ctx* c, const std::vector<Replica>& rep) {
   if (rep.size() != c->P.size()) return false;
   for (size_t i = 0; i < c->P.size(); ++i) {
     const ReplicaShape sh = replica_shape(c->P[i]);
-    if (sh.rlmax != rep[i].rlmax || sh.rgmax != rep[i].rgmax || sh.width != rep[i].width) return false;
+    if (sh.rlmax != rep[i].rlmax || sh.rgmax != rep[i].rgmax || sh.width != rep[i].width ||
+        sh.rgrows != rep[i].rgrows || (sh.rgw == 2) != (rep[i].g16 != 0))
+      return false;
   }
   return true;
 }
@@ -1355,6 +1381,8 @@ static int layout_replica(dk_ctx* c, std::vector<Replica>& rep, uint64_t npos) {
     R.rlmax = sh.rlmax;
     R.rgmax = sh.rgmax;
     R.width = sh.width;
+    R.g16 = sh.rgw == 2;
+    R.rgrows = sh.rgrows;
     R.npos = npos;
     HIPCHK(R.rlen.reserve(npos * 2 + 8, 0, s));
     if (R.rlmax) HIPCHK(R.runits.reserve(npos * (uint64_t)R.rlmax * sh.width + 64, 0, s));
@@ -1366,7 +1394,8 @@ static int layout_replica(dk_ctx* c, std::vector<Replica>& rep, uint64_t npos) {
       HIPCHK(R.rgoff.reserve(npos * 4 + 8, 0, s));
       HIPCHK(R.rgcnt.reserve(npos * 2 + 8, 0, s));
     }
-    if (R.rgmax) HIPCHK(R.rgrams.reserve(npos * (uint64_t)R.rgmax * sh.rgw + 64, 0, s));
+    if (R.rgmax)
+      HIPCHK(R.rgrams.reserve(npos * (R.g16 ? (uint64_t)R.rgrows * 8 : (uint64_t)R.rgmax * sh.rgw) + 64, 0, s));
   }
   return DK_OK;
 }
@@ -1400,6 +1429,8 @@ static int fill_replica(dk_ctx* c, std::vector<Replica>& rep, const uint32_t* ro
     J.rgcnt = R.rgcnt.as<uint16_t>();
     J.rgmax = R.rgmax;
     J.rg32 = replica_shape(S).rgw == 4;
+    J.g16 = R.g16;
+    J.rgrows = R.rgrows;
     J.grams = S.grams.as<uint64_t>();
     J.rgrams = R.rgrams.p;
     HIPCHK(launch_replicate(J, rowof, pos0, n, s));

@@ -19,6 +19,22 @@ constexpr int kMaxReplicaUnits = 64;   // longer columns are read in place (cano
 constexpr int kMaxReplicaGrams = 64;   // QGram sets with more grams are read in place
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // filtered candidate slot
 
+// Latin-1 bigram keys and their per-row perfect hash (DevProp::g16).  A QGram q = 2 code is
+// (u0 << 16) | u1 (16 bits per UTF-16 unit); with both units < 256 the 16-bit bigram
+// (u0 << 8) | u1 is injective, and key = bigram + 1 (mod 2^16) is never 0 except for the
+// bigram U+00FF U+00FF, whose rows get no seed -- so a zero key is padding.  A row's seed
+// s = (lt - 8) << 8 | i names the table size 2^lt (lt 8..10) and multiplier gram_mult(i)
+// under which slot(key) = low32(key * mult) >> (32 - lt) is injective on the row's keys.
+constexpr uint16_t kGramSeedNone = 0xFFFF;
+constexpr int kGramSeedTries = 256;
+constexpr int kGramPerfectMax = 128;  // grams of a set that get a seed (table <= 1024 u32)
+__host__ __device__ inline uint32_t gram_key(uint64_t code) {
+  return ((((uint32_t)(code >> 8) & 0xFF00u) | ((uint32_t)code & 0xFFu)) + 1u) & 0xFFFFu;
+}
+__host__ __device__ inline uint32_t gram_mult(uint32_t i) {  // odd, < 2^24 (v_mul_u32_u24)
+  return ((0x9E3779u ^ (i * 0x5851F5u)) & 0xFFFFFFu) | 1u;
+}
+
 // comparators whose values carry a precomputed sorted code list (goff/gcnt/grams):
 // QGram sets (sorted unique packed grams) and the token comparators (sorted token ids,
 // duplicates kept)
@@ -75,6 +91,13 @@ struct DevProp {
   const void* rgrams;      // QGram: [k * rstride + g], k < rgmax (0 = read grams in place)
   int32_t rgmax;
   int32_t rg32;            // replica codes are u32 (every code of the property < 2^32)
+  // Latin-1 bigrams (QGram q = 2, BASIC / ENDS, a width-1 arena): rgrams holds per position
+  // rgrows u64 words [j * rstride + g], word j = the gram keys 4j .. 4j+3 (16 bits each,
+  // gram_key(), 0 past the set), and gseed[row] is the row's perfect-hash seed of its own
+  // gram set (kGramSeedNone: none) -- the query side's LDS table is then collision-free.
+  int32_t g16;
+  int32_t rgrows;
+  const uint16_t* gseed;
 };
 
 struct ScoreParams {
@@ -212,6 +235,8 @@ struct ReplicaJob {
   int32_t has_qgram;
   int32_t rgmax;      // QGram replica rows (0: none)
   int32_t rg32;       // u32 replica codes
+  int32_t g16;        // Latin-1 bigram keys, 4 per u64 word, rgrows words (DevProp::g16)
+  int32_t rgrows;
   uint64_t stride;    // replica positions
   const uint32_t* off;
   const uint16_t* len;
@@ -279,6 +304,10 @@ hipError_t launch_select_rows(const uint8_t* flags, const uint8_t* group, uint64
                               uint64_t nrows, int want_group, uint32_t* flag_out, hipStream_t s);
 hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64_t row0,
                                uint64_t nrows, uint32_t base, uint32_t* rows_out, hipStream_t s);
+// rows [row0, row0 + n): seed[row] = the perfect-hash seed of the row's bigram keys
+hipError_t launch_gram_seed(const uint64_t* grams, const uint32_t* goff, const uint16_t* gcnt,
+                            const uint16_t* len, uint64_t row0, uint64_t n, uint16_t* seed,
+                            hipStream_t s);
 // replica positions [pos0, pos0 + npos)
 hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t pos0, uint64_t npos,
                             hipStream_t s);

@@ -1104,6 +1104,74 @@ __device__ __forceinline__ int qgram_common_hashed(uint64_t* tab, const uint64_t
   return common;
 }
 
+// |Q ∩ C| for Latin-1 bigram sets (DevProp::g16).  The query's keys go to their slots of a
+// per-wave LDS table under the query row's perfect-hash seed, so each candidate key is ONE
+// table read and compare -- no probe chain, no divergence.  Each lane streams its
+// candidate's key words (four keys per u64: the wave's 64 lanes read one 512-B row per word)
+// two words at a time, the next two in flight.  Lanes past their own set read padding keys
+// (0); slot 0 -- where key 0 hashes -- is never left 0, so padding never counts, and empty
+// slots hold 0, which no real key equals.  Wave-uniform call; the table is left zero.
+__device__ __forceinline__ int qgram_common_perfect(uint32_t* tab, const uint64_t* __restrict__ g1, int m1,
+                                                    uint32_t seed, const uint64_t* __restrict__ rg,
+                                                    uint64_t rstride, uint32_t g, int m2) {
+  const int lt = 8 + (int)(seed >> 8);
+  const uint32_t mult = gram_mult(seed & 0xFFu);
+  const int sh = 32 - lt;
+  const int lane = (int)lane_id();
+  if (lane == 0) tab[0] = ~0u;  // a real key landing in slot 0 overwrites the sentinel below
+  uint32_t s0 = 0u, s1 = 0u;    // this lane's query slots (m1 <= kGramPerfectMax = 128)
+  if (lane < m1) {
+    const uint32_t key = gram_key(g1[lane]);
+    s0 = (uint32_t)__umul24(key, mult) >> sh;
+    tab[s0] = key;
+  }
+  if (lane + 64 < m1) {
+    const uint32_t key = gram_key(g1[lane + 64]);
+    s1 = (uint32_t)__umul24(key, mult) >> sh;
+    tab[s1] = key;
+  }
+  wave_lds_sync();
+  int njw = (m2 + 3) >> 2;  // word rows: this lane's, then the wave's most (the trip count)
+  for (int o = 32; o > 0; o >>= 1) njw = max(njw, __shfl_xor(njw, o));
+  njw = (int)__builtin_amdgcn_readfirstlane((uint32_t)njw);
+  // the word row's base is wave-uniform, the lane adds a 32-bit byte offset
+  const char* base = reinterpret_cast<const char*>(rg);
+  const uint32_t boff = g * 8u;
+  const uint64_t rowb = rstride * 8u;
+  auto ld = [&](int j) -> uint64_t {
+    return __hip_atomic_load(reinterpret_cast<const uint64_t*>(base + (uint64_t)j * rowb + boff),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  int common = 0;
+  auto probe = [&](uint64_t w) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t key = (uint32_t)(w >> (16 * e)) & 0xFFFFu;
+      common += tab[(uint32_t)__umul24(key, mult) >> sh] == key ? 1 : 0;
+    }
+  };
+  if (njw > 0) {
+    uint64_t c0 = ld(0), c1 = ld(1);  // rgrows is even and >= 2
+    for (int j = 0; j < njw; j += 2) {
+      uint64_t n0 = 0, n1 = 0;
+      if (j + 2 < njw) {  // wave-uniform; j + 3 < rgrows
+        n0 = ld(j + 2);
+        n1 = ld(j + 3);
+      }
+      probe(c0);
+      probe(c1);
+      c0 = n0;
+      c1 = n1;
+    }
+  }
+  wave_lds_sync();
+  if (lane < m1) tab[s0] = 0u;
+  if (lane + 64 < m1) tab[s1] = 0u;
+  if (lane == 0) tab[0] = 0u;
+  wave_lds_sync();
+  return common;
+}
+
 __device__ __forceinline__ int intersect_sorted(const uint64_t* __restrict__ g1, int m1,
                                                 const uint64_t* __restrict__ g2, int m2) {
   int i = 0, j = 0, common = 0;
@@ -1185,15 +1253,29 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
       if (cmp) sim = str_equal(s1, lq, s2, lc) ? 1.0 : 0.0;
       break;
     case DK_CMP_QGRAM: {
-      const bool same = cmp && str_equal(s1, lq, s2, lc);
       const int m1 = (int)__builtin_amdgcn_readfirstlane((uint32_t)D.gcnt[q]);
       const uint64_t* g1 = D.grams + D.goff[q];
+      if (D.g16) {
+        const uint32_t sd = __builtin_amdgcn_readfirstlane((uint32_t)D.gseed[q]);
+        if (m1 > 0 && sd != kGramSeedNone) {  // wave-uniform
+          // no string compare: equal values have equal non-empty gram sets, for which every
+          // formula is exactly 1.0
+          const int m2 = cmp ? (int)D.rgcnt[g] : 0;
+          const int common = qgram_common_perfect(reinterpret_cast<uint32_t*>(peq), g1, m1, sd,
+                                                  reinterpret_cast<const uint64_t*>(D.rgrams),
+                                                  rstride, g, m2);
+          if (m2 > 0) sim = qgram_formula(common, m1, m2, D.formula);
+          break;
+        }
+      }
+      const bool same = cmp && str_equal(s1, lq, s2, lc);
       if (m1 > 0 && m1 <= kQgramHashMax && g1[m1 - 1] != ~0ull) {  // wave-uniform
         sim = same ? 1.0 : 0.0;
         const int m2 = cmp && !same ? (int)D.rgcnt[g] : 0;
-        // candidate codes: the transposed replica (coalesced), or in place
+        // candidate codes: the transposed replica (coalesced), or in place (no replica, or
+        // a bigram-key replica and a query without a perfect hash)
         const int common =
-            !D.rgmax ? qgram_common_hashed(peq, g1, m1, D.grams + D.rgoff[g], 1, max(m2 - 1, 0), m2)
+            !D.rgmax || D.g16 ? qgram_common_hashed(peq, g1, m1, D.grams + D.rgoff[g], 1, max(m2 - 1, 0), m2)
             : D.rg32 ? qgram_common_hashed(peq, g1, m1, reinterpret_cast<const uint32_t*>(D.rgrams) + g,
                                            rstride, D.rgmax - 1, m2)
                      : qgram_common_hashed(peq, g1, m1, reinterpret_cast<const uint64_t*>(D.rgrams) + g,
@@ -1447,8 +1529,9 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
                          : string_sim<RMAX, LR, uint16_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch);
       if (!SYM || rev != rev) rev = sim;
       if (cmp) {
-        if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2)
-          bytes += 6u + (D.rg32 && D.rgmax ? 4u : 8u) * (uint32_t)D.rgcnt[g];
+        if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2,
+                                   // 16-bit keys for Latin-1 bigrams)
+          bytes += 6u + (D.g16 ? 2u : D.rg32 && D.rgmax ? 4u : 8u) * (uint32_t)D.rgcnt[g];
         else if (uses_codes(D.op))  // token ids
           bytes += 6u + 8u * (uint32_t)D.rgcnt[g];
         else
@@ -1641,6 +1724,48 @@ __device__ __forceinline__ void replicate_units(const ReplicaJob& J, uint64_t g,
   for (int k = 0; k < rw; ++k) dst[(uint64_t)k * J.stride] = k < nw ? src[k] : 0u;
 }
 
+// Per-row perfect hash of a Latin-1 bigram set (DevProp::g16): the first multiplier of
+// gram_mult's sequence under which the set's keys land in distinct slots of a 2^lt table
+// (one thread per row, its occupancy bitmap in its own LDS words).  Rows of more than
+// kGramPerfectMax grams, with the key-0 bigram, or without a seed in kGramSeedTries tries
+// get kGramSeedNone (k_score then reads the candidate sets in place).
+__global__ __launch_bounds__(256) void k_gram_seed(const uint64_t* __restrict__ grams,
+                                                   const uint32_t* __restrict__ goff,
+                                                   const uint16_t* __restrict__ gcnt,
+                                                   const uint16_t* __restrict__ len, uint64_t row0,
+                                                   uint64_t n, uint16_t* __restrict__ seed) {
+  __shared__ uint32_t occ[256][33];  // 1024 bits per thread (+1 word: rows spread over banks)
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t row = row0 + i;
+  const int m = len[row] == kMissing ? 0 : (int)gcnt[row];
+  uint16_t out = kGramSeedNone;
+  if (m > 0 && m <= kGramPerfectMax) {
+    const uint64_t* g = grams + goff[row];
+    const int lt = m <= 32 ? 8 : (m <= 64 ? 9 : 10);
+    const int words = 1 << (lt - 5);
+    uint32_t* bits = occ[threadIdx.x];
+    bool zero = false;
+    for (int k = 0; k < m; ++k) zero = zero || gram_key(g[k]) == 0u;
+    for (int t = 0; t < kGramSeedTries && !zero; ++t) {
+      const uint32_t mult = gram_mult((uint32_t)t);
+      for (int w = 0; w < words; ++w) bits[w] = 0u;
+      bool ok = true;
+      for (int k = 0; k < m && ok; ++k) {
+        const uint32_t h = (gram_key(g[k]) * mult) >> (32 - lt);
+        const uint32_t b = 1u << (h & 31u);
+        ok = (bits[h >> 5] & b) == 0u;
+        bits[h >> 5] |= b;
+      }
+      if (ok) {
+        out = (uint16_t)(((lt - 8) << 8) | t);
+        break;
+      }
+    }
+  }
+  seed[row] = out;
+}
+
 __global__ __launch_bounds__(256) void k_replicate(const ReplicaJob J, const uint32_t* __restrict__ rowof,
                                                    uint64_t pos0, uint64_t npos) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1663,7 +1788,16 @@ __global__ __launch_bounds__(256) void k_replicate(const ReplicaJob J, const uin
     if (J.rgmax) {  // codes transposed: the 64 lanes of a score wave read row k as 512 B
       const uint64_t* src = J.grams + J.goff[row];
       const int m = l == (int)kMissing ? 0 : (int)J.gcnt[row];
-      if (J.rg32) {
+      if (J.g16) {  // four bigram keys per word, the wave's 64 lanes read a word row as 512 B
+        uint64_t* dst = reinterpret_cast<uint64_t*>(J.rgrams);
+        for (int j = 0; j < J.rgrows; ++j) {
+          uint64_t w = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * j + e < m) w |= (uint64_t)gram_key(src[4 * j + e]) << (16 * e);
+          dst[(uint64_t)j * J.stride + g] = w;
+        }
+      } else if (J.rg32) {
         uint32_t* dst = reinterpret_cast<uint32_t*>(J.rgrams);
         for (int k = 0; k < J.rgmax; ++k) dst[(uint64_t)k * J.stride + g] = k < m ? (uint32_t)src[k] : 0u;
       } else {
@@ -2126,6 +2260,14 @@ hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64
                                uint64_t nrows, uint32_t base, uint32_t* rows_out, hipStream_t s) {
   DK_LAUNCH_GUARD(nrows);
   k_scatter_rows<<<grid1d(nrows), 256, 0, s>>>(flag, pos, row0, nrows, base, rows_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_seed(const uint64_t* grams, const uint32_t* goff, const uint16_t* gcnt,
+                            const uint16_t* len, uint64_t row0, uint64_t n, uint16_t* seed,
+                            hipStream_t s) {
+  DK_LAUNCH_GUARD(n);
+  k_gram_seed<<<grid1d(n), 256, 0, s>>>(grams, goff, gcnt, len, row0, n, seed);
   return hipGetLastError();
 }
 

@@ -256,8 +256,8 @@ class RowStore:
         self.segs.append((self.n, len(recs), list(recs)))
         self.n += len(recs)
 
-    def append_packed(self, packed, group_no=None):
-        self.segs.append((self.n, packed.n, (packed, group_no)))
+    def append_packed(self, packed, group_no=None, dataset_id=None):
+        self.segs.append((self.n, packed.n, (packed, group_no, dataset_id)))
         self.n += packed.n
 
     def truncate(self, n):
@@ -292,7 +292,7 @@ class RowStore:
         return self._materialise(pay, row - r0)
 
     def _materialise(self, pay, i):
-        packed, group_no = pay
+        packed, group_no, dataset_id = pay
         cache = getattr(packed, "_cols", None)
         if cache is None:
             cache = packed._cols = ([packed.values(p) for p in range(len(self.props))],
@@ -303,8 +303,9 @@ class RowStore:
             rec.add_value(GROUP_NO_PROPERTY_NAME, str(group_no))
         rec.add_value(ID_PROPERTY, ids[i])
         rec.add_value(ORIGINAL_ENTITY_ID_PROPERTY_NAME, eids[i])
-        ds = ids[i].split("__", 2)[1 if group_no else 0]
-        rec.add_value(DATASET_ID_PROPERTY_NAME, ds)
+        # the source's dataset id as IncrementalDataSource sets it (:90), not parsed back out
+        # of the record ID (a dataset id may itself contain "__")
+        rec.add_value(DATASET_ID_PROPERTY_NAME, dataset_id)
         if packed.deleted[i]:
             rec.add_value(DELETED_PROPERTY_NAME, "true")
         return rec
@@ -342,7 +343,6 @@ class GpuBlockingDatabase:
         self.engine = GpuEngine(self.schema, device)
         self.pending = []
         self.rows = RowStore([p.name for p in self.props])   # row -> Record
-        self.by_id = {}         # ID -> row of the live version (Python-packed batches)
         self.ids = Interner()   # ID string -> dense identity number (both packing paths)
         self.row_ident = np.zeros(0, np.uint64)   # row -> its record ID's interned id
         self._native = {}       # DataSource id -> NativeSource
@@ -378,10 +378,11 @@ class GpuBlockingDatabase:
         return self.index_batch(recs)
 
     def find_record_by_id(self, rid):
-        row = self.by_id.get(rid)
-        if row is None:
-            ident = self.ids.find(rid)
-            row = None if ident is None else self.engine.row_of_ident(ident)
+        """IncrementalLuceneDatabase.findRecordById (:170-180): the row the index's ID map
+        holds for the ID (dk_row_of_ident -- one source of truth for both packing paths: the
+        live version, or the oldest under setOverwrite(true), Lucene's first hit)."""
+        ident = self.ids.find(rid)
+        row = None if ident is None else self.engine.row_of_ident(ident)
         return None if row is None else self.rows[row]
 
     def close(self):
@@ -438,9 +439,6 @@ class GpuBlockingDatabase:
             self._transient_row0 = len(self.rows)
         self.rows.append_records(records)
         self.row_ident = np.concatenate([self.row_ident, np.asarray(ident, np.uint64)])
-        if not transient:
-            for rid, row in zip(rids, rows):
-                self.by_id[rid] = int(row)
         return rows
 
     def native_source(self, source):
@@ -464,7 +462,7 @@ class GpuBlockingDatabase:
         rows = self.engine.upsert_packed(packed, transient=transient)
         if transient and self._transient_row0 is None:
             self._transient_row0 = len(self.rows)
-        self.rows.append_packed(packed, source.group_no)
+        self.rows.append_packed(packed, source.group_no, source.dataset_id)
         self.row_ident = np.concatenate([self.row_ident, np.asarray(packed.ident, np.uint64)])
         return rows, packed
 

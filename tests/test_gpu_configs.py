@@ -562,6 +562,35 @@ def test_deduplicate_json_equals_record_path(linkage):
         p.database.close()
 
 
+def test_find_record_by_id_across_packing_paths():
+    """An ID indexed through the Record path and re-posted through the native JSON path:
+    findRecordById returns the live (re-posted) version -- the index's ID map is the one
+    source of truth -- and a natively packed record's dukeDatasetId is its source's dataset
+    id, also when that id contains "__" (IncrementalDataSource.java:90)."""
+    with open(os.path.join(GOLDEN, "testdukeconfig_schema.json")) as f:
+        cfg_d = json.load(f)["pipelines"]["Deduplication/countries-dbpedia-mondial"]
+    cfg_d = json.loads(json.dumps(cfg_d))
+    cfg_d["data_sources"][0]["dataset_id"] = "db__pedia"
+    cfg = DukeConfig.from_dict(cfg_d)
+    db = dh.GpuBlockingDatabase(cfg, [dh.PartsKey(("NAME", None, 0, 3))])
+    proc = dh.GpuProcessor(cfg, db)
+    src = cfg.data_sources[0]
+    ents = stress_entities(200, 5)
+    proc.deduplicate(dh.records_from_entities(ents, src))
+    rid = db.find_record_by_id(f"db__pedia__{ents[7]['_id']}")
+    assert rid is not None and rid.get_value("dukeDatasetId") == "db__pedia"
+    changed = dict(ents[7])
+    name_col = next(c for c in src.columns if c.property == "NAME")
+    changed[name_col.name] = "Reposted Name"
+    proc.deduplicate_json(json.dumps([changed]), src)
+    r = db.find_record_by_id(f"db__pedia__{ents[7]['_id']}")
+    want = dh.records_from_entities([changed], src)[0]
+    assert r.get_value("NAME") == want.get_value("NAME") != rid.get_value("NAME")
+    assert r.get_value("dukeDatasetId") == "db__pedia"
+    assert r.get_value("dukeOriginalEntityId") == ents[7]["_id"]
+    db.close()
+
+
 class _LinkAdapter(dh.MatchListener):
     """Feeds the per-callback link-sink checker (oracle/linkdb_ref.py) from the replay."""
 

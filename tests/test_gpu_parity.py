@@ -505,3 +505,38 @@ def test_tables_rebuilt_after_each_upsert():
             assert_same(res, ot.match(q))
             res.close()
     eng.close()
+
+
+LATIN1 = "abcdefghijklmnopqrstuvwxyz éßÿ0123"
+
+
+@pytest.mark.parametrize("formula,tok", [(0, A.QGRAM_BASIC), (1, A.QGRAM_BASIC), (2, A.QGRAM_BASIC),
+                                         (1, A.QGRAM_ENDS)])
+def test_qgram_bigram_keys_allpairs(formula, tok):
+    """Latin-1 bigrams take the 16-bit-key replica and the per-row perfect hash (tables of
+    256 and 512 slots: sets of up to 64 grams), including the key-0 bigram U+00FF U+00FF
+    (its rows get no seed and read the candidate sets in place), one-gram and empty sets."""
+    rng = random.Random(formula * 3 + tok)
+    vals = [v for v in rand_strings(rng, 140, LATIN1, 1, 66) if v]
+    vals += ["ÿÿ", "aÿÿb", "ÿÿÿÿ", "ab", "a", "ÿ", "ba", "aba", "é" * 40, LATIN1 * 2]
+    res, ref = allpairs_single({"comparator": QG, "low": 0.2, "high": 0.8, "q": 2,
+                                "formula": formula, "tokenizer": tok}, vals)
+    assert_same(res, ref)
+
+
+def test_qgram_bigram_keys_widened_arena():
+    """A UTF-16 value arriving in a later batch widens the property's arena: the bigram-key
+    replica and its seeds are then no longer used (the next match rebuilds the replica with
+    u32 codes); both matches equal the oracle."""
+    rng = random.Random(77)
+    vals = [v for v in rand_strings(rng, 300, LATIN1, 2, 30) if v]
+    keys = [v[:1] for v in vals]
+    n = len(vals)
+    prop = {"comparator": QG, "low": 0.2, "high": 0.8, "q": 2, "formula": 2}
+    res, ref = run_both([prop], [vals], keys=[keys], threshold=0.5, maybe=0.3)
+    assert_same(res, ref)
+    vals2 = vals + ["Ā" + v for v in vals[:40]]
+    keys2 = keys + keys[:40]
+    res, ref = run_both([prop], [vals2], keys=[keys2], threshold=0.5, maybe=0.3,
+                        batches=[(0, n), (n, len(vals2))])
+    assert_same(res, ref)
