@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DK_ABI_VERSION 4
+#define DK_ABI_VERSION 5
 
 /* status codes */
 #define DK_OK 0
@@ -182,6 +182,23 @@ typedef struct dk_profile {
 typedef struct dk_ctx dk_ctx;
 
 int dk_create(const dk_schema* schema, int device, dk_ctx** out);
+/* One pipeline over several GPUs of this process (the reference's parallelism
+ * is in-process -- THREADS -> Processor.setThreads, App.java:232,344,465 -- so a JVM reaches
+ * every GPU of the node through ONE handle).  The index is replicated: every dk_upsert /
+ * dk_upsert_transient / dk_drop_transient / dk_set_overwrite goes to every device, on one
+ * host thread per device; a batch rejected on validation is rejected identically everywhere
+ * (failure-atomic as dk_upsert), a device failure on some devices only leaves the ctx
+ * unusable (DK_E_STATE afterwards).  dk_match splits the query rows into one contiguous tile
+ * per device, balanced by dk_candidate_counts (+32 per query, the padded wave), runs the
+ * tiles concurrently and returns ONE host list in query order -- each device copies its tile
+ * into its slice of the list over its own host link (DK_MATCH_DEVICE and
+ * dk_set_result_region are per-device features: DK_E_UNSUPPORTED here).  dk_compare_*,
+ * dk_property_similarity, dk_candidate_counts, dk_row_of_ident and dk_num_rows use the
+ * first device's replica; dk_get_profile sums counters and takes the largest time per
+ * phase.  A device may be listed more than once (one stream set per entry).  ndev == 1 is
+ * dk_create(devices[0]). */
+int dk_create_multi(const dk_schema* schema, const int* devices, int ndev, dk_ctx** out);
+int dk_num_devices(const dk_ctx* ctx);
 void dk_destroy(dk_ctx* ctx);
 /* Failure-atomic: a batch that is rejected (DK_E_INVALID / DK_E_UNSUPPORTED / DK_E_NOMEM)
  * leaves the index as it was -- no row added, no older version tombstoned -- so the caller
@@ -234,8 +251,9 @@ int dk_compare_values(dk_ctx* ctx, const dk_batch* pair, double* prob);
 /* Comparator.compare(v1, v2) of schema property `prop` for two indexed rows (the raw
  * similarity PropertyImpl.compare maps to a probability), computed by the production
  * scoring kernel.  NaN when either row has no (or an empty) value: Processor.compare never
- * calls a comparator then.  Levenshtein: when Duke's early-exit cutoff fires the GPU
- * returns a similarity below 0.5 (maxdist+1, not the column minimum); both map to <low>. */
+ * calls a comparator then.  Levenshtein: Duke's own value also where compactDistance's early
+ * exit fires (its column minimum; the fused match kernels use maxdist + 1 there, which maps
+ * to the same <low> probability). */
 int dk_property_similarity(dk_ctx* ctx, int prop, uint32_t r1, uint32_t r2, double* sim);
 int dk_set_overwrite(dk_ctx* ctx, int on);
 uint64_t dk_num_rows(const dk_ctx* ctx);
@@ -362,6 +380,11 @@ int dk_linkdb_apply(dk_linkdb* db, const dk_link_batch* batch, int64_t timestamp
  * (timestamp, assertion order) -- the reference iterates a HashMap (order unpinned) */
 int dk_linkdb_changes_since(const dk_linkdb* db, int64_t since, dk_link_list** out);
 void dk_free_link_list(dk_link_list* list);
+/* InMemoryLinkDatabase.getAllLinksFor: every link of one record ID (either side) */
+int dk_linkdb_links_for(const dk_linkdb* db, uint64_t id, dk_link_list** out);
+/* the POST route's deleted-record branch (App.java:994-999): each link of the record
+ * retracted (Link.retract() + assertLink) with the given timestamp */
+int dk_linkdb_retract_all(dk_linkdb* db, uint64_t id, int64_t timestamp, uint64_t* nretracted);
 
 /* the StandardAnalyzer tokens of one value (escape: escapeLucene first, the query side),
  * '\n'-joined into out (test hook of the DK_CAND_LUCENE analysis) */

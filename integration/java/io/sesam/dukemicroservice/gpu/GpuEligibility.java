@@ -29,14 +29,53 @@ public final class GpuEligibility {
         }
     }
 
-    public static boolean check(Configuration config) {
+    /**
+     * Whether the pipeline can run on the GPU.  keyFunctions empty = the reference's own
+     * database (IncrementalLuceneDatabase), whose candidate semantics the device then runs
+     * (dk_schema.lucene): eligible with the database knobs App.configureDatabase reads
+     * (App.java:550-563) unless FUZZY_SEARCH=true meets a tokenized lookup comparator
+     * (FuzzyQuery, IncrementalLuceneDatabase.java:311-315), a lookup property is
+     * Lookup.REQUIRED (MUST clauses, :487-488) or MAX_SEARCH_HITS exceeds 100.
+     */
+    public static boolean check(Configuration config, boolean keyFunctions) {
         try {
             for (Property p : config.getProperties())
                 if (!p.isIdProperty() && !p.isIgnoreProperty()) opcode(p.getComparator());
+            if (!keyFunctions) lucene(config);
             return true;
         } catch (IllegalArgumentException e) {
             return false;
         }
+    }
+
+    /** The Lucene candidate source's settings (App.configureDatabase, App.java:550-563). */
+    public static final class LuceneOptions {
+        public final int maxSearchHits;
+        public final float minRelevance;
+
+        LuceneOptions(int maxSearchHits, float minRelevance) {
+            this.maxSearchHits = maxSearchHits;
+            this.minRelevance = minRelevance;
+        }
+    }
+
+    public static LuceneOptions lucene(Configuration config) {
+        float minRelevance = 0.9f;
+        boolean fuzzy = false;
+        int maxHits = 10;
+        if (System.getenv("MIN_RELEVANCE") != null) minRelevance = Float.parseFloat(System.getenv("MIN_RELEVANCE"));
+        if (System.getenv("FUZZY_SEARCH") != null) fuzzy = Boolean.parseBoolean(System.getenv("FUZZY_SEARCH"));
+        if (System.getenv("MAX_SEARCH_HITS") != null) maxHits = Integer.parseInt(System.getenv("MAX_SEARCH_HITS"));
+        if (maxHits < 1 || maxHits > 100) throw new IllegalArgumentException("MAX_SEARCH_HITS " + maxHits);
+        if (config.getLookupProperties().isEmpty()) throw new IllegalArgumentException("no lookup properties");
+        for (Property p : config.getLookupProperties()) {
+            if (p.getLookupBehaviour() == Property.Lookup.REQUIRED)
+                throw new IllegalArgumentException("Lookup.REQUIRED: MUST clauses are not GPU-eligible");
+            Comparator c = p.getComparator();
+            if (fuzzy && c != null && c.isTokenized())
+                throw new IllegalArgumentException("FUZZY_SEARCH over a tokenized comparator");
+        }
+        return new LuceneOptions(maxHits, minRelevance);
     }
 
     public static Opcode opcode(Comparator c) {

@@ -58,6 +58,14 @@ class SinceAwareLinkDB:
         self.seq += 1
         return True
 
+    def retract_all(self, rid, timestamp):          # App.java:994-999 (deleted records)
+        # getAllLinksFor(id), link.retract() [recalled: status RETRACTED, timestamp now] on the
+        # stored Link itself, then assertLink (which then finds it unchanged)
+        for l in self.all_links_for(rid):
+            l.status, l.timestamp = RETRACTED, timestamp
+            self.order[l.key()] = self.seq
+            self.seq += 1
+
     def changes_since(self, since):                 # :32-40
         out = [l for l in self.links.values() if l.timestamp > since]
         return sorted(out, key=lambda l: (l.timestamp, self.order[l.key()]))

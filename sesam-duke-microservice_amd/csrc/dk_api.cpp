@@ -390,9 +390,14 @@ struct ResultHolder {
   std::unique_ptr<ResultBufs> bufs;
   int device = 0;
   hipStream_t stream = nullptr;
+  bool host_only = false;  // a multi-device ctx's list: host arrays only
 };
 
 struct dk_ctx {
+  // dk_create_multi: a ctx of per-device member ctxs (the index replicated on each); the
+  // fields below are then unused apart from schema, device (the first member's), pool, prof
+  std::vector<dk_ctx*> members;
+  bool broken = false;     // a replicated update failed on some members only
   dk_schema schema{};
   std::vector<PropState> P;
   int device = 0;
@@ -638,6 +643,11 @@ int dk_create(const dk_schema* schema, int device, dk_ctx** out) {
 
 void dk_destroy(dk_ctx* c) {
   if (!c) return;
+  if (!c->members.empty()) {
+    for (dk_ctx* m : c->members) dk_destroy(m);
+    delete c;
+    return;
+  }
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->copy_stream);
@@ -656,11 +666,16 @@ void dk_destroy(dk_ctx* c) {
   (void)hipStreamDestroy(s);
 }
 
-uint64_t dk_num_rows(const dk_ctx* c) { return c ? c->nrows : 0; }
+uint64_t dk_num_rows(const dk_ctx* c) {
+  return c ? (c->members.empty() ? c->nrows : c->members[0]->nrows) : 0;
+}
+
+int dk_num_devices(const dk_ctx* c) { return c ? (c->members.empty() ? 1 : (int)c->members.size()) : 0; }
 
 // IncrementalLuceneDatabase.findRecordById (:170-180): the row of the live version
 int dk_row_of_ident(const dk_ctx* c, uint64_t ident, uint32_t* row) {
   if (!c || !row) return fail(DK_E_INVALID, "NULL argument");
+  if (!c->members.empty()) return dk_row_of_ident(c->members[0], ident, row);
   const uint32_t r = c->ident_row.get(ident);
   if (r == IdentMap::kNoRow) return fail(DK_E_INVALID, "no indexed record with that ID");
   *row = r;
@@ -670,18 +685,41 @@ int dk_row_of_ident(const dk_ctx* c, uint64_t ident, uint32_t* row) {
 int dk_set_profiling(dk_ctx* c, int on) {
   if (!c) return fail(DK_E_INVALID, "ctx is NULL");
   c->profiling = on != 0;
+  for (dk_ctx* m : c->members) m->profiling = on != 0;
   return DK_OK;
 }
 
 int dk_get_profile(const dk_ctx* c, dk_profile* out) {
   if (!c || !out) return fail(DK_E_INVALID, "NULL argument");
   *out = c->prof;
+  if (!c->members.empty()) {  // counters summed, times the largest member's (they overlap)
+    dk_profile t{};
+    for (const dk_ctx* m : c->members) {
+      const dk_profile& p = m->prof;
+      t.ms_index = std::max(t.ms_index, p.ms_index);
+      t.ms_generate = std::max(t.ms_generate, p.ms_generate);
+      t.ms_score = std::max(t.ms_score, p.ms_score);
+      t.ms_gather = std::max(t.ms_gather, p.ms_gather);
+      t.ms_copy = std::max(t.ms_copy, p.ms_copy);
+      t.ms_emit = std::max(t.ms_emit, p.ms_emit);
+      t.score_launches += p.score_launches;
+      t.pairs_scored += p.pairs_scored;
+      t.pairs_generated += p.pairs_generated;
+      t.score_bytes += p.score_bytes;
+      t.sym_matches += p.sym_matches;
+      t.full_builds += p.full_builds;
+      t.delta_builds += p.delta_builds;
+    }
+    t.ms_total = c->prof.ms_total;  // the multi-device dk_match's own wall time
+    *out = t;
+  }
   return DK_OK;
 }
 
 int dk_reset_profile(dk_ctx* c) {
   if (!c) return fail(DK_E_INVALID, "ctx is NULL");
   c->prof = dk_profile{};
+  for (dk_ctx* m : c->members) m->prof = dk_profile{};
   return DK_OK;
 }
 
@@ -991,9 +1029,12 @@ static int stage_lucene(dk_ctx* c, const dk_batch* b, uint64_t n, uint64_t row0,
   return DK_OK;
 }
 
+static int group_upsert(dk_ctx* g, const dk_batch* b, uint32_t* rows_out, bool transient);
+
 static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool transient) {
   HostLap lap;
   if (!c || !b) return fail(DK_E_INVALID, "NULL argument");
+  if (!c->members.empty()) return group_upsert(c, b, rows_out, transient);
   if (!transient && c->transient)
     return fail(DK_E_STATE, "transient rows present: dk_drop_transient before indexing");
   if (b->n == 0) return DK_OK;
@@ -1195,8 +1236,13 @@ int dk_upsert_transient(dk_ctx* c, const dk_batch* b, uint32_t* rows_out) {
   return guarded([&] { return upsert_rows(c, b, rows_out, true); });
 }
 
+static int group_each(dk_ctx* c, int (*f)(dk_ctx*, void*), void* arg);
+static int drop_transient_impl(dk_ctx* c);
+static int drop_transient_member(dk_ctx* m, void*) { return drop_transient_impl(m); }
+
 static int drop_transient_impl(dk_ctx* c) {
   if (!c) return fail(DK_E_INVALID, "NULL argument");
+  if (!c->members.empty()) return group_each(c, drop_transient_member, nullptr);
   if (!c->transient) return DK_OK;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -2202,9 +2248,12 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   return DK_OK;
 }
 
+static int group_match(dk_ctx* g, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out);
+
 static int match_impl(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out) {
   if (!c || !out) return fail(DK_E_INVALID, "NULL argument");
   *out = nullptr;
+  if (!c->members.empty()) return group_match(c, query_rows, nq, flags, out);
   if (nq && !query_rows) return fail(DK_E_INVALID, "query_rows is NULL");
   if (flags & ~DK_MATCH_DEVICE) return fail(DK_E_INVALID, "unknown flags 0x%x", flags);
   bool contiguous = true;  // query rows r0, r0+1, ... (Processor.deduplicate's batch)
@@ -2244,6 +2293,10 @@ int dk_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags, dk_r
 // of the multi-GPU query tiles.  ALLPAIRS: every query gets the usable rows.
 static int candidate_counts_impl(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, uint64_t* counts) {
   if (!c || (nq && (!query_rows || !counts))) return fail(DK_E_INVALID, "NULL argument");
+  if (!c->members.empty()) {
+    if (c->broken) return fail(DK_E_STATE, "a replicated update failed on some devices only");
+    return candidate_counts_impl(c->members[0], query_rows, nq, counts);
+  }
   for (uint64_t i = 0; i < nq; ++i)
     if (query_rows[i] >= c->nrows)
       return fail(DK_E_INVALID, "query row %u not in the index (%llu rows)", query_rows[i],
@@ -2279,6 +2332,7 @@ int dk_result_copy_to_device(const dk_result* r, uint64_t* first, uint32_t* cand
                              double* prob, uint8_t* kind) {
   if (!r) return fail(DK_E_INVALID, "result is NULL");
   const ResultHolder* R = reinterpret_cast<const ResultHolder*>(r);
+  if (R->host_only) return fail(DK_E_UNSUPPORTED, "a multi-device ctx's list is in host memory only");
   HIPCHK(hipSetDevice(R->device));
   const ResultBufs& B = *R->bufs;
   hipStream_t s = R->stream;
@@ -2308,6 +2362,8 @@ int dk_result_region_layout(uint64_t bytes, uint64_t max_queries, dk_region_layo
 
 static int set_result_region_impl(dk_ctx* c, void* base, uint64_t bytes, uint64_t max_queries) {
   if (!c) return fail(DK_E_INVALID, "ctx is NULL");
+  if (!c->members.empty())
+    return fail(DK_E_UNSUPPORTED, "a multi-device ctx writes its list into its own host memory");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->copy_stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -2373,6 +2429,10 @@ int dk_property_similarity(dk_ctx* c, int prop, uint32_t r1, uint32_t r2, double
 
 static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double* prob) {
   if (!c || !prob) return fail(DK_E_INVALID, "NULL argument");
+  if (!c->members.empty()) {
+    if (c->broken) return fail(DK_E_STATE, "a replicated update failed on some devices only");
+    return compare_one(c->members[0], r1, r2, raw_prop, prob);
+  }
   if (r1 >= c->nrows || r2 >= c->nrows) return fail(DK_E_INVALID, "row out of range");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = c->stream;
@@ -2404,8 +2464,17 @@ static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double
   double p = NAN;
   HIPCHK(hipMemcpyAsync(&n, base + 96, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&p, base + 128, 8, hipMemcpyDeviceToHost, s));
+  // Levenshtein's raw similarity: Duke's own early-exit value (the fused kernel's cut-off
+  // distance differs from it; the probability it feeds does not)
+  double lev = NAN;
+  if (raw_prop >= 0 && c->P[raw_prop].cfg.comparator == DK_CMP_LEVENSHTEIN) {
+    const PropState& S = c->P[raw_prop];
+    HIPCHK(launch_lev_exact(S.off.as<uint32_t>(), S.len.as<uint16_t>(), S.units.p, S.width, r1, r2,
+                            reinterpret_cast<double*>(base + 120), s));
+    HIPCHK(hipMemcpyAsync(&lev, base + 120, 8, hipMemcpyDeviceToHost, s));
+  }
   HIPCHK(hipStreamSynchronize(s));
-  *prob = n ? p : NAN;
+  *prob = n ? (lev == lev ? lev : p) : NAN;
   return DK_OK;
 }
 
@@ -2435,6 +2504,7 @@ static void clear_index(dk_ctx* c) {
 
 static int compare_values_impl(dk_ctx* c, const dk_batch* pair, double* prob) {
   if (!c || !pair || !prob) return fail(DK_E_INVALID, "NULL argument");
+  if (!c->members.empty()) return compare_values_impl(c->members[0], pair, prob);
   if (pair->n != 2) return fail(DK_E_INVALID, "dk_compare_values takes a batch of 2 records (r1, r2)");
   if (!c->pair_ctx) {
     std::vector<dk_property> props(c->P.size());
@@ -2467,5 +2537,201 @@ int dk_compare_values(dk_ctx* c, const dk_batch* pair, double* prob) {
 int dk_set_overwrite(dk_ctx* c, int on) {
   if (!c) return fail(DK_E_INVALID, "ctx is NULL");
   c->overwrite = on != 0;
+  for (dk_ctx* m : c->members) m->overwrite = on != 0;
+  return DK_OK;
+}
+
+// ----------------------------------------------------------------------------------------
+// dk_create_multi: one handle over several devices (include/dukehip.h).  Members are plain
+// ctxs; the group fans updates out on one host thread per member and splits dk_match into
+// cost-balanced contiguous query tiles, then gathers the tiles' device lists into
+// one pinned host list, each member copying its slice over its own host link.
+// ----------------------------------------------------------------------------------------
+static int create_multi_impl(const dk_schema* schema, const int* devices, int ndev, dk_ctx** out) {
+  if (!out) return fail(DK_E_INVALID, "out is NULL");
+  *out = nullptr;
+  if (!devices || ndev < 1) return fail(DK_E_INVALID, "no devices");
+  if (ndev == 1) return create_impl(schema, devices[0], out);
+  std::unique_ptr<dk_ctx> g(new dk_ctx());
+  for (int i = 0; i < ndev; ++i) {
+    dk_ctx* m = nullptr;
+    const int rc = create_impl(schema, devices[i], &m);
+    if (rc) {
+      for (dk_ctx* x : g->members) dk_destroy(x);
+      g->members.clear();
+      return rc;
+    }
+    g->members.push_back(m);
+  }
+  g->schema = g->members[0]->schema;
+  g->device = devices[0];
+  *out = g.release();
+  return DK_OK;
+}
+
+int dk_create_multi(const dk_schema* schema, const int* devices, int ndev, dk_ctx** out) {
+  return guarded([&] { return create_multi_impl(schema, devices, ndev, out); });
+}
+
+// f on every member, one host thread each.  The replicas stay identical when every member
+// returns the same status (a batch is validated identically everywhere); otherwise the
+// group is marked broken.
+static int group_each(dk_ctx* g, int (*f)(dk_ctx*, void*), void* arg) {
+  if (g->broken) return fail(DK_E_STATE, "a replicated update failed on some devices only");
+  const int nd = (int)g->members.size();
+  std::vector<int> rc(nd, DK_OK);
+  std::vector<std::string> msg(nd);
+  dk_run_parts(nd, [&](int i) {
+    rc[i] = guarded([&] { return f(g->members[i], arg); });
+    if (rc[i]) msg[i] = g_err;
+  });
+  for (int i = 1; i < nd; ++i)
+    if (rc[i] != rc[0]) {
+      g->broken = true;
+      const int bad = rc[0] ? 0 : i;
+      return fail(DK_E_STATE, "device %d of %d diverged (%d): %s", bad, nd, rc[bad], msg[bad].c_str());
+    }
+  if (rc[0]) g_err = msg[0];
+  return rc[0];
+}
+
+struct GroupUpsert {
+  const dk_batch* b;
+  bool transient;
+  const std::vector<dk_ctx*>* members;
+  std::vector<std::vector<uint32_t>> rows;  // per member
+};
+
+static int upsert_member(dk_ctx* m, void* a) {
+  GroupUpsert* u = static_cast<GroupUpsert*>(a);
+  const size_t i = (size_t)(std::find(u->members->begin(), u->members->end(), m) - u->members->begin());
+  u->rows[i].resize(u->b->n);
+  return upsert_rows(m, u->b, u->rows[i].data(), u->transient);
+}
+
+static int group_upsert(dk_ctx* g, const dk_batch* b, uint32_t* rows_out, bool transient) {
+  GroupUpsert u{b, transient, &g->members, std::vector<std::vector<uint32_t>>(g->members.size())};
+  const int rc = group_each(g, upsert_member, &u);
+  if (rc) return rc;
+  for (size_t i = 1; i < u.rows.size(); ++i)
+    if (u.rows[i] != u.rows[0]) {
+      g->broken = true;
+      return fail(DK_E_STATE, "device %zu assigned other rows", i);
+    }
+  if (rows_out && b->n) memcpy(rows_out, u.rows[0].data(), b->n * 4);
+  return DK_OK;
+}
+
+static int group_match(dk_ctx* g, const uint32_t* q, uint64_t nq, int flags, dk_result** out) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (g->broken) return fail(DK_E_STATE, "a replicated update failed on some devices only");
+  if (nq && !q) return fail(DK_E_INVALID, "query_rows is NULL");
+  if (flags & DK_MATCH_DEVICE)
+    return fail(DK_E_UNSUPPORTED, "a multi-device ctx hands its list over in host memory");
+  if (flags) return fail(DK_E_INVALID, "unknown flags 0x%x", flags);
+  const int nd = (int)g->members.size();
+  // contiguous tiles of equal estimated cost: the query's candidates + one padded wave
+  // (dukehip.dist.cost_bounds); every member holds the same index, so member 0 counts
+  std::vector<uint64_t> bound(nd + 1, nq);
+  bound[0] = 0;
+  if (nq) {
+    std::vector<uint64_t> cnt(nq);
+    const int rc = candidate_counts_impl(g->members[0], q, nq, cnt.data());
+    if (rc) return rc;
+    double total = 0.0;
+    for (uint64_t i = 0; i < nq; ++i) total += (double)cnt[i] + 32.0;
+    double acc = 0.0;
+    int t = 1;
+    for (uint64_t i = 0; i < nq && t < nd; ++i) {
+      while (t < nd && acc >= total * t / nd) bound[t++] = i;
+      acc += (double)cnt[i] + 32.0;
+    }
+  }
+  std::vector<dk_result*> part(nd, nullptr);
+  std::vector<int> rc(nd, DK_OK);
+  std::vector<std::string> msg(nd);
+  dk_run_parts(nd, [&](int i) {
+    rc[i] = guarded([&] {
+      return match_impl(g->members[i], q + bound[i], bound[i + 1] - bound[i], DK_MATCH_DEVICE, &part[i]);
+    });
+    if (rc[i]) msg[i] = g_err;
+  });
+  auto release = [&] {
+    for (dk_result*& r : part) {
+      dk_free_result(r);
+      r = nullptr;
+    }
+  };
+  for (int i = 0; i < nd; ++i)
+    if (rc[i]) {
+      release();
+      g_err = msg[i];
+      return rc[i];
+    }
+  std::vector<uint64_t> base(nd + 1, 0);
+  uint64_t scored = 0, generated = 0;
+  for (int i = 0; i < nd; ++i) {
+    base[i + 1] = base[i] + part[i]->n;
+    scored += part[i]->pairs_scored;
+    generated += part[i]->pairs_generated;
+  }
+  const uint64_t n = base[nd];
+  std::unique_ptr<ResultHolder> R(new ResultHolder());
+  R->pool = g->pool;
+  R->bufs = g->pool->take();
+  R->device = g->device;
+  R->host_only = true;
+  ResultBufs& B = *R->bufs;
+  hipError_t e = B.h_first.reserve((nq + 1) * 8);
+  if (e == hipSuccess) e = B.h_cand.reserve(n * 4 + 4);
+  if (e == hipSuccess) e = B.h_prob.reserve(n * 8 + 8);
+  if (e == hipSuccess) e = B.h_kind.reserve(n + 1);
+  if (e != hipSuccess) {
+    release();
+    R->pool->give(std::move(R->bufs));
+    return fail(DK_E_NOMEM, "pinned host memory for the list: %s", hipGetErrorString(e));
+  }
+  // every member copies its tile's list into its slice, on its own stream and host link
+  dk_run_parts(nd, [&](int i) {
+    rc[i] = guarded([&] {
+      const ResultHolder* P = reinterpret_cast<const ResultHolder*>(part[i]);
+      const ResultBufs& D = *P->bufs;
+      const uint64_t nqi = bound[i + 1] - bound[i], ni = part[i]->n;
+      HIPCHK(hipSetDevice(P->device));
+      hipStream_t s = P->stream;
+      if (nqi)
+        HIPCHK(hipMemcpyAsync(B.h_first.as<uint64_t>() + bound[i], D.d_first.p, nqi * 8, hipMemcpyDeviceToHost, s));
+      if (ni) {
+        HIPCHK(hipMemcpyAsync(B.h_cand.as<uint32_t>() + base[i], D.d_cand.p, ni * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(B.h_prob.as<double>() + base[i], D.d_prob.p, ni * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(B.h_kind.as<uint8_t>() + base[i], D.d_kind.p, ni, hipMemcpyDeviceToHost, s));
+      }
+      HIPCHK(hipStreamSynchronize(s));
+      uint64_t* f = B.h_first.as<uint64_t>() + bound[i];
+      for (uint64_t k = 0; k < nqi; ++k) f[k] += base[i];  // tile-local -> list offsets
+      return DK_OK;
+    });
+    if (rc[i]) msg[i] = g_err;
+  });
+  release();
+  for (int i = 0; i < nd; ++i)
+    if (rc[i]) {
+      R->pool->give(std::move(R->bufs));
+      g_err = msg[i];
+      return rc[i];
+    }
+  B.h_first.as<uint64_t>()[nq] = n;
+  dk_result& r = R->r;
+  r.nqueries = nq;
+  r.n = n;
+  r.first = B.h_first.as<uint64_t>();
+  r.candidate = B.h_cand.as<uint32_t>();
+  r.prob = B.h_prob.as<double>();
+  r.kind = B.h_kind.as<uint8_t>();
+  r.pairs_scored = scored;
+  r.pairs_generated = generated;
+  if (g->profiling)
+    g->prof.ms_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = &R.release()->r;
   return DK_OK;
 }

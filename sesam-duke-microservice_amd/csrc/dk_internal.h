@@ -304,6 +304,10 @@ hipError_t launch_select_rows(const uint8_t* flags, const uint8_t* group, uint64
                               uint64_t nrows, int want_group, uint32_t* flag_out, hipStream_t s);
 hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64_t row0,
                                uint64_t nrows, uint32_t base, uint32_t* rows_out, hipStream_t s);
+// *out = Levenshtein.compare(row r1's value, row r2's value) with Duke's exact early exit
+// (NaN when either value is missing or empty)
+hipError_t launch_lev_exact(const uint32_t* off, const uint16_t* len, const void* units, int width,
+                            uint32_t r1, uint32_t r2, double* out, hipStream_t s);
 // rows [row0, row0 + n): seed[row] = the perfect-hash seed of the row's bigram keys
 hipError_t launch_gram_seed(const uint64_t* grams, const uint32_t* goff, const uint16_t* gcnt,
                             const uint16_t* len, uint64_t row0, uint64_t n, uint16_t* seed,

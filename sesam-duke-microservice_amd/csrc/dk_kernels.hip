@@ -1724,6 +1724,63 @@ __device__ __forceinline__ void replicate_units(const ReplicaJob& J, uint64_t g,
   for (int k = 0; k < rw; ++k) dst[(uint64_t)k * J.stride] = k < nw ? src[k] : 0u;
 }
 
+// [Duke 1.2] comparators.Levenshtein.compare for ONE pair, serially, with compactDistance's
+// early exit returning the column minimum exactly as Duke does.  Comparator.compare's raw
+// similarity (dk_property_similarity): the fused kernels return maxdist + 1 (short values) or
+// the full-matrix distance (long values) when the cutoff fires -- the same `low` probability,
+// a different raw similarity.  One thread; rows r1 (s1, the column) and r2 (s2).
+__global__ void k_lev_exact(const uint32_t* __restrict__ off, const uint16_t* __restrict__ len,
+                            const void* __restrict__ units, int width, uint32_t r1, uint32_t r2,
+                            double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int n1 = len[r1], n2 = len[r2];
+  if (n1 == (int)kMissing || n2 == (int)kMissing || n1 == 0 || n2 == 0) {
+    *out = __builtin_nan("");  // Processor.compare skips the property
+    return;
+  }
+  auto u = [&](uint32_t row, int i) -> uint32_t {
+    return width == 1 ? (uint32_t)reinterpret_cast<const uint8_t*>(units)[off[row] + i]
+                      : (uint32_t)reinterpret_cast<const uint16_t*>(units)[off[row] + i];
+  };
+  const int ln = min(n1, n2), maxlen = max(n1, n2);
+  if (2 * ln <= maxlen) {  // (double)len / maxlen <= 0.5
+    *out = 0.0;
+    return;
+  }
+  bool same = n1 == n2;
+  for (int i = 0; i < n1 && same; ++i) same = u(r1, i) == u(r2, i);
+  if (same) {
+    *out = 1.0;
+    return;
+  }
+  // compactDistance: one column over s1's rows, virtual first row ix2 + 1
+  int column[kMaxLongUnits + 1];
+  const int maxdist = ln / 2;
+  uint32_t ch2 = u(r2, 0);
+  column[0] = 1;
+  for (int i = 1; i <= n1; ++i) column[i] = min(column[i - 1], i - 1) + (u(r1, i - 1) == ch2 ? 0 : 1);
+  int above = 0, result = -1;
+  for (int j = 1; j < n2; ++j) {
+    ch2 = u(r2, j);
+    above = j + 1;
+    int smallest = 2 * n1;
+    for (int i = 1; i <= n1; ++i) {
+      const int v = min(min(above, column[i - 1]), column[i]) + (u(r1, i - 1) == ch2 ? 0 : 1);
+      column[i - 1] = above;
+      above = v;
+      smallest = min(smallest, v);
+    }
+    column[n1] = above;
+    if (smallest > maxdist) {
+      result = smallest;
+      break;
+    }
+  }
+  if (result < 0) result = above;
+  const int dist = min(result, ln);
+  *out = 1.0 - ((double)dist / (double)ln);
+}
+
 // Per-row perfect hash of a Latin-1 bigram set (DevProp::g16): the first multiplier of
 // gram_mult's sequence under which the set's keys land in distinct slots of a 2^lt table
 // (one thread per row, its occupancy bitmap in its own LDS words).  Rows of more than
@@ -2260,6 +2317,12 @@ hipError_t launch_scatter_rows(const uint32_t* flag, const uint32_t* pos, uint64
                                uint64_t nrows, uint32_t base, uint32_t* rows_out, hipStream_t s) {
   DK_LAUNCH_GUARD(nrows);
   k_scatter_rows<<<grid1d(nrows), 256, 0, s>>>(flag, pos, row0, nrows, base, rows_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_lev_exact(const uint32_t* off, const uint16_t* len, const void* units, int width,
+                            uint32_t r1, uint32_t r2, double* out, hipStream_t s) {
+  k_lev_exact<<<1, 64, 0, s>>>(off, len, units, width, r1, r2, out);
   return hipGetLastError();
 }
 

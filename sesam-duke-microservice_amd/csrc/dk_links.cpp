@@ -219,4 +219,70 @@ int dk_linkdb_changes_since(const dk_linkdb* db, int64_t since, dk_link_list** o
 
 void dk_free_link_list(dk_link_list* l) { delete reinterpret_cast<LinkList*>(l); }
 
+static int list_of(const std::vector<const LinkRec*>& sel, dk_link_list** out) {
+  LinkList* L = new (std::nothrow) LinkList();
+  if (!L) return dk_fail_ingest(DK_E_NOMEM, "out of host memory");
+  try {
+    for (const LinkRec* r : sel) {
+      L->id1.push_back(r->id1);
+      L->id2.push_back(r->id2);
+      L->status.push_back(r->status);
+      L->kind.push_back(r->kind);
+      L->confidence.push_back(r->confidence);
+      L->timestamp.push_back(r->timestamp);
+    }
+  } catch (const std::bad_alloc&) {
+    delete L;
+    return dk_fail_ingest(DK_E_NOMEM, "out of host memory");
+  }
+  L->pub.n = L->id1.size();
+  L->pub.id1 = L->id1.data();
+  L->pub.id2 = L->id2.data();
+  L->pub.status = L->status.data();
+  L->pub.kind = L->kind.data();
+  L->pub.confidence = L->confidence.data();
+  L->pub.timestamp = L->timestamp.data();
+  *out = &L->pub;
+  return DK_OK;
+}
+
+// InMemoryLinkDatabase.getAllLinksFor [recalled]: the links of one record ID, in the order
+// they were first asserted
+int dk_linkdb_links_for(const dk_linkdb* db, uint64_t id, dk_link_list** out) {
+  if (!db || !out) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
+  *out = nullptr;
+  std::vector<const LinkRec*> sel;
+  try {
+    auto bi = db->by_id.find(id);
+    if (bi != db->by_id.end())
+      for (const auto& k : bi->second) {
+        auto it = db->links.find(k);
+        if (it != db->links.end()) sel.push_back(&it->second);
+      }
+  } catch (const std::bad_alloc&) {
+    return dk_fail_ingest(DK_E_NOMEM, "out of host memory");
+  }
+  return list_of(sel, out);
+}
+
+// The deleted-record branch of the POST route (App.java:994-999): every link of the record
+// retracted -- Link.retract() [recalled: status RETRACTED, timestamp now] on the stored link
+// itself, so even an already retracted link takes the new timestamp
+int dk_linkdb_retract_all(dk_linkdb* db, uint64_t id, int64_t timestamp, uint64_t* nretracted) {
+  if (!db) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
+  uint64_t n = 0;
+  auto bi = db->by_id.find(id);
+  if (bi != db->by_id.end())
+    for (const auto& k : bi->second) {
+      auto it = db->links.find(k);
+      if (it == db->links.end()) continue;
+      it->second.status = DK_LINK_RETRACTED;
+      it->second.timestamp = timestamp;
+      it->second.seq = db->seq++;
+      ++n;
+    }
+  if (nretracted) *nretracted = n;
+  return DK_OK;
+}
+
 }  // extern "C"

@@ -24,9 +24,9 @@ MODE_DEDUP, MODE_LINKAGE, MODE_ALLPAIRS = 0, 1, 2
 KIND_MATCH, KIND_MAYBE = 1, 2
 
 MATCH_HOST, MATCH_DEVICE = 0, 1
-ABI_VERSION = 4   # include/dukehip.h DK_ABI_VERSION
+ABI_VERSION = 5   # include/dukehip.h DK_ABI_VERSION
 
-EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
+EXPORTS = ("dk_create", "dk_create_multi", "dk_num_devices", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
            "dk_match", "dk_candidate_counts", "dk_result_copy_to_device",
            "dk_free_result", "dk_result_region_layout", "dk_set_result_region",
            "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite", "dk_num_rows", "dk_row_of_ident", "dk_set_profiling", "dk_get_profile",
@@ -34,7 +34,8 @@ EXPORTS = ("dk_create", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_dr
            "dk_interner_create", "dk_interner_destroy", "dk_interner_size", "dk_interner_find",
            "dk_interner_intern", "dk_pack_json", "dk_free_packed", "dk_interner_string",
            "dk_linkdb_create", "dk_linkdb_destroy", "dk_linkdb_size", "dk_linkdb_apply",
-           "dk_linkdb_changes_since", "dk_free_link_list", "dk_lucene_analyze")
+           "dk_linkdb_changes_since", "dk_free_link_list", "dk_linkdb_links_for",
+           "dk_linkdb_retract_all", "dk_lucene_analyze")
 
 
 class DukeHipError(RuntimeError):
@@ -121,6 +122,10 @@ def load():
     L = C.CDLL(path)
     vp = C.c_void_p
     L.dk_create.argtypes = [C.POINTER(dk_schema), C.c_int, C.POINTER(vp)]
+    L.dk_create_multi.argtypes = [C.POINTER(dk_schema), C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]
+    L.dk_create_multi.restype = C.c_int
+    L.dk_num_devices.argtypes = [vp]
+    L.dk_num_devices.restype = C.c_int
     L.dk_destroy.argtypes = [vp]
     L.dk_destroy.restype = None
     L.dk_upsert.argtypes = [vp, C.POINTER(dk_batch), vp]

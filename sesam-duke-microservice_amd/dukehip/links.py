@@ -68,6 +68,10 @@ def _lib():
         L.dk_linkdb_apply.restype = C.c_int
         L.dk_linkdb_changes_since.argtypes = [vp, C.c_int64, C.POINTER(C.POINTER(dk_link_list))]
         L.dk_linkdb_changes_since.restype = C.c_int
+        L.dk_linkdb_links_for.argtypes = [vp, C.c_uint64, C.POINTER(C.POINTER(dk_link_list))]
+        L.dk_linkdb_links_for.restype = C.c_int
+        L.dk_linkdb_retract_all.argtypes = [vp, C.c_uint64, C.c_int64, C.POINTER(C.c_uint64)]
+        L.dk_linkdb_retract_all.restype = C.c_int
         L.dk_free_link_list.argtypes = [C.POINTER(dk_link_list)]
         L.dk_free_link_list.restype = None
         L.dk_interner_string.argtypes = [vp, C.c_uint64, C.POINTER(C.POINTER(C.c_uint16)),
@@ -131,6 +135,23 @@ class LinkDatabase:
         """getChangesSince(since): dict of arrays id1, id2, status, kind, confidence, timestamp."""
         out = C.POINTER(dk_link_list)()
         A.check(self.lib.dk_linkdb_changes_since(self.h, int(since), C.byref(out)))
+        return self._take(out)
+
+    def links_for(self, ident):
+        """InMemoryLinkDatabase.getAllLinksFor(id) of an interned record ID (same dict form)."""
+        out = C.POINTER(dk_link_list)()
+        A.check(self.lib.dk_linkdb_links_for(self.h, int(ident), C.byref(out)))
+        return self._take(out)
+
+    def retract_all(self, ident, timestamp=None):
+        """The POST route's deleted-record branch (App.java:994-999): every link of the record
+        retracted (Link.retract() + assertLink).  Returns the number of links."""
+        n = C.c_uint64()
+        ts = int(time.time() * 1000) if timestamp is None else int(timestamp)
+        A.check(self.lib.dk_linkdb_retract_all(self.h, int(ident), ts, C.byref(n)))
+        return int(n.value)
+
+    def _take(self, out):
         try:
             L = out.contents
             n = int(L.n)

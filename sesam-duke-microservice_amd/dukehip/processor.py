@@ -114,13 +114,23 @@ class MatchResult:
 
 
 class GpuEngine:
-    """Thin owner of one dk_ctx (one pipeline, one device)."""
+    """Thin owner of one dk_ctx (one pipeline): on one device, or -- `devices`, a list --
+    replicated over several devices of this process (dk_create_multi: one handle, the
+    query tiles matched concurrently, one list back)."""
 
-    def __init__(self, schema, device=0):
+    def __init__(self, schema, device=0, devices=None):
         self.lib = A.load()
         self.ctx = C.c_void_p()
-        A.check(self.lib.dk_create(C.byref(schema), int(device), C.byref(self.ctx)))
+        if devices is not None:
+            dv = (C.c_int * len(devices))(*[int(d) for d in devices])
+            A.check(self.lib.dk_create_multi(C.byref(schema), dv, len(devices), C.byref(self.ctx)))
+        else:
+            A.check(self.lib.dk_create(C.byref(schema), int(device), C.byref(self.ctx)))
         self._schema = schema
+
+    @property
+    def num_devices(self):
+        return int(self.lib.dk_num_devices(self.ctx))
 
     def close(self):
         if self.ctx:
@@ -318,11 +328,13 @@ class GpuBlockingDatabase:
     IncrementalLuceneDatabase.java:516-517, 578-590).  Records marked
     dukeDeleted=true stay indexed but are never candidates (:478)."""
 
-    def __init__(self, config: DukeConfig, key_functions=(), mode=None, device=0, lucene=None):
+    def __init__(self, config: DukeConfig, key_functions=(), mode=None, device=0, lucene=None,
+                 devices=None):
         """key_functions: Duke blocking key functions (the GPU blocking contract); none ->
         the reference's own Lucene candidate semantics (IncrementalLuceneDatabase.
         findCandidateMatches, dukehip.lucene; `lucene` = LuceneOptions, default from the
-        environment like App.configureDatabase)."""
+        environment like App.configureDatabase).  devices: a list of GPUs of this process to
+        replicate the index over (dk_create_multi), instead of the one `device`."""
         self.config = config
         self.key_functions = list(key_functions or ())
         if mode is None:
@@ -340,7 +352,7 @@ class GpuBlockingDatabase:
                 raise ValueError("no lookup properties: the Lucene query would match nothing")
             idx = {p.name: i for i, p in enumerate(self.props)}
             A.lucene_source(self.schema, [idx[n] for n in self.lookup], opts.max_hits, opts.min_relevance)
-        self.engine = GpuEngine(self.schema, device)
+        self.engine = GpuEngine(self.schema, device, devices=devices)
         self.pending = []
         self.rows = RowStore([p.name for p in self.props])   # row -> Record
         self.ids = Interner()   # ID string -> dense identity number (both packing paths)

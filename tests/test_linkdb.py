@@ -139,3 +139,48 @@ def test_since_feed_shape():
     assert ldb.since_feed(1234, recs.get) == "[]"
     ldb.close()
     ids.close()
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_deleted_record_retraction_and_links_for(seed):
+    """The POST route's deleted-record branch (App.java:994-999: getAllLinksFor, retract,
+    assertLink) natively (dk_linkdb_retract_all) between bulk batches, and getAllLinksFor
+    (dk_linkdb_links_for), against the per-callback restatement."""
+    batches = random_batches(seed)
+    rng = random.Random(seed)
+    ref = R.SinceAwareLinkDB()
+    ids = Interner()
+    ldb = LinkDatabase(ids)
+    for t, (qs, entries) in enumerate(batches):
+        ts = 1000 + 10 * t
+        L = R.LinkDBListener(ref, lambda ts=ts: ts)
+        L.batch_ready(len(qs))
+        for i, (q, lst) in enumerate(zip(qs, entries)):
+            if not lst:
+                L.no_match_for((i, q))
+            for c, p, kind in lst:
+                (L.matches if kind == 1 else L.matches_perhaps)((i, q), c, p)
+        L.batch_done()
+        qid = ids.intern(qs)
+        first = np.zeros(len(qs) + 1, np.uint64)
+        first[1:] = np.cumsum([len(x) for x in entries])
+        flat = [e for lst in entries for e in lst]
+        cid = ids.intern([c for c, _, _ in flat]) if flat else np.zeros(0, np.uint64)
+        ldb.apply(qid, first, cid, [p for _, p, _ in flat], [k for _, _, k in flat], timestamp=ts)
+        for q in rng.sample(qs, min(2, len(qs))):        # deleted records of the next POST
+            ref.retract_all(q, ts + 5)
+            assert ldb.retract_all(ids.intern([q])[0], ts + 5) == len(ref.all_links_for(q))
+    for since in (0, 1050, 1100):
+        ch = ldb.changes_since(since)
+        got = [(interned_string(ids, a), interned_string(ids, b), int(s), int(k), float(c), int(t))
+               for a, b, s, k, c, t in zip(ch["id1"], ch["id2"], ch["status"], ch["kind"],
+                                           ch["confidence"], ch["timestamp"])]
+        assert got == [(l.id1, l.id2, l.status, l.kind, l.confidence, l.timestamp)
+                       for l in ref.changes_since(since)]
+    some = batches[0][0][0]
+    lf = ldb.links_for(ids.intern([some])[0])
+    got = [(interned_string(ids, a), interned_string(ids, b), int(s)) for a, b, s in
+           zip(lf["id1"], lf["id2"], lf["status"])]
+    assert got == [(l.id1, l.id2, l.status) for l in ref.all_links_for(some)] and got
+    ldb.close()
+    ids.close()
