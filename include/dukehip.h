@@ -382,9 +382,10 @@ int dk_linkdb_changes_since(const dk_linkdb* db, int64_t since, dk_link_list** o
 void dk_free_link_list(dk_link_list* list);
 /* InMemoryLinkDatabase.getAllLinksFor: every link of one record ID (either side) */
 int dk_linkdb_links_for(const dk_linkdb* db, uint64_t id, dk_link_list** out);
-/* the POST route's deleted-record branch (App.java:994-999): each link of the record
- * retracted (Link.retract() + assertLink) with the given timestamp */
-int dk_linkdb_retract_all(dk_linkdb* db, uint64_t id, int64_t timestamp, uint64_t* nretracted);
+/* the POST route's deleted-record branch (App.java:994-999): Link.retract() + assertLink on
+ * the link between `id` and `other`, or (other == UINT64_MAX) on every link of `id`, with the
+ * given timestamp */
+int dk_linkdb_retract(dk_linkdb* db, uint64_t id, uint64_t other, int64_t timestamp, uint64_t* nretracted);
 
 /* the StandardAnalyzer tokens of one value (escape: escapeLucene first, the query side),
  * '\n'-joined into out (test hook of the DK_CAND_LUCENE analysis) */

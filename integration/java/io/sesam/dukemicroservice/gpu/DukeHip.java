@@ -154,6 +154,13 @@ public final class DukeHip {
     public static native long[] linkdbApply(long db, long[] queryIdent, long[] first, long[] candidateIdent,
                                             double[] prob, byte[] kind, long timestamp);
 
+    /** dk_linkdb_links_for: getAllLinksFor of an interned ID; released with freeLinkList. */
+    public static native long linkdbLinksFor(long db, long ident);
+
+    /** dk_linkdb_retract: Link.retract() + assertLink of the link ident-other (other = -1:
+     *  every link of ident), App.java:994-999.  Returns the links retracted. */
+    public static native long linkdbRetract(long db, long ident, long other, long timestamp);
+
     /** dk_linkdb_changes_since; the handle is released with freeLinkList. */
     public static native long linkdbChangesSince(long db, long since);
 

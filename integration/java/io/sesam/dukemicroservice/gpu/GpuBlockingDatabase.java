@@ -1,6 +1,7 @@
 package io.sesam.dukemicroservice.gpu;
 
 import java.util.ArrayList;
+import java.util.BitSet;
 import java.util.Collection;
 import java.util.HashMap;
 import java.util.List;
@@ -10,37 +11,56 @@ import no.priv.garshol.duke.Configuration;
 import no.priv.garshol.duke.Database;
 import no.priv.garshol.duke.Property;
 import no.priv.garshol.duke.Record;
+import no.priv.garshol.duke.RecordImpl;
 import no.priv.garshol.duke.databases.KeyFunction;
 
 /**
  * The index of one pipeline on the GPU: replaces IncrementalLuceneDatabase (App.java:329-342,
  * 450-463) for pipelines GpuEligibility accepts.  index() buffers, commit() upserts the
  * buffered records column-wise (delete-by-ID then add, IncrementalLuceneDatabase.java:
- * 516-517), findRecordById is served from the host-side ID -> row map.  Candidate generation
- * is key-function blocking on the device (dk_match), so findCandidateMatches is not called by
- * GpuProcessor.  Mirrors sesam-duke-microservice_amd/dukehip/processor.py GpuBlockingDatabase.
+ * 516-517).  Candidates come from dk_match: the device's key-function blocking, or -- no key
+ * functions, the reference's own configuration -- IncrementalLuceneDatabase's own query
+ * semantics (findCandidateMatches :459-492) run on the device, so findCandidateMatches is not
+ * called by GpuProcessor.  Record IDs are interned natively (dk_interner: the identity numbering
+ * of both packing paths, the link sink's IDs).  findRecordById is the device index's ID map.
+ * Mirrors sesam-duke-microservice_amd/dukehip/processor.py GpuBlockingDatabase.
+ *
+ * Host memory: a row's Record is held only while the row can still be handed to a listener or
+ * looked up -- superseded versions are released at the upsert that supersedes them (not under
+ * setOverwrite(true), where they stay candidates), and natively packed batches keep their
+ * columns, not Record objects (built per lookup), freed once every row of the batch is gone.
  */
 public class GpuBlockingDatabase implements Database {
     private final long ctx;
-    private final List<Property> props;           // scored properties, Processor.compare order
+    private final long ids;                        // dk_interner of record IDs
+    private final List<Property> props;            // scored properties, Processor.compare order
     private final List<KeyFunction> keyFunctions;
-    private final int mode;
     private final boolean linkage;
+    private final String idProp;
+    private final RowStore rows = new RowStore();
+    private long[] rowIdent = new long[1024];      // row -> interned record ID
     private final List<Record> pending = new ArrayList<>();
-    private final List<Record> rows = new ArrayList<>();            // row -> Record
-    private final Map<String, Integer> liveRow = new HashMap<>();   // ID -> live row
-    private final Map<String, Long> idents = new HashMap<>();       // ID -> dense identity
+    private final List<Integer> deferred = new ArrayList<>();   // releaseDeferred
     private boolean indexingIsDisabled;
+    private boolean overwrite;
     private int transientRow0 = -1;
     private Configuration config;
 
+    /**
+     * @param scoredProps  the scored properties in Processor.compare's iteration order
+     *                     (comparisonOrder gives it for a data source's records)
+     * @param keyFunctions key-function blocking; empty = the reference's Lucene candidate
+     *                     semantics on the device (lookup properties and App.configureDatabase's
+     *                     knobs, GpuEligibility.lucene)
+     * @param devices      the GPUs of this JVM to replicate the index over (dk_create_multi)
+     */
     public GpuBlockingDatabase(Configuration config, List<Property> scoredProps,
-                               List<KeyFunction> keyFunctions, boolean linkage, int device) {
+                               List<KeyFunction> keyFunctions, boolean linkage, int[] devices) {
         this.config = config;
         this.props = scoredProps;
         this.keyFunctions = keyFunctions;
         this.linkage = linkage;
-        this.mode = linkage ? DukeHip.MODE_LINKAGE : DukeHip.MODE_DEDUP;
+        this.idProp = config.getIdentityProperties().iterator().next().getName();
         int n = scoredProps.size();
         int[] cmp = new int[n], q = new int[n], formula = new int[n], tok = new int[n];
         double[] low = new double[n], high = new double[n], minRatio = new double[n];
@@ -54,20 +74,69 @@ public class GpuBlockingDatabase implements Database {
             low[i] = scoredProps.get(i).getLowProbability();
             high[i] = scoredProps.get(i).getHighProbability();
         }
+        int[] lookup = null;
+        int maxHits = 10;
+        float minRelevance = 0.9f;
+        if (keyFunctions.isEmpty()) {   // IncrementalLuceneDatabase.findCandidateMatches on the device
+            GpuEligibility.LuceneOptions opts = GpuEligibility.lucene(config);
+            maxHits = opts.maxSearchHits;
+            minRelevance = opts.minRelevance;
+            List<Property> lp = config.getLookupProperties();
+            lookup = new int[lp.size()];
+            for (int i = 0; i < lp.size(); i++) {
+                lookup[i] = -1;
+                for (int p = 0; p < n; p++)
+                    if (scoredProps.get(p).getName().equals(lp.get(i).getName())) lookup[i] = p;
+                if (lookup[i] < 0) throw new IllegalArgumentException("lookup property not scored: " + lp.get(i).getName());
+            }
+        }
+        this.ids = DukeHip.internerCreate();
         this.ctx = DukeHip.create(cmp, q, formula, tok, low, high, minRatio, config.getThreshold(),
-                                  config.getMaybeThreshold(), mode, keyFunctions.size(), device);
+                                  config.getMaybeThreshold(), linkage ? DukeHip.MODE_LINKAGE : DukeHip.MODE_DEDUP,
+                                  keyFunctions.size(), lookup, maxHits, minRelevance,
+                                  devices == null || devices.length == 0 ? new int[] {0} : devices);
+    }
+
+    /**
+     * Processor.compare iterates r1.getProperties(): RecordImpl's HashMap key order.  The keys a
+     * data source's RecordBuilder inserts -- its columns' properties in column order, then
+     * dukeGroupNo (linkage), ID, dukeOriginalEntityId, dukeDatasetId, dukeDeleted
+     * (IncrementalDataSource.java:67-98) -- put into a HashMap the same way give that order;
+     * at most 12 keys keep the table at 16 buckets, so a record missing some values iterates
+     * the rest in the same relative order.  Returns the scored properties in it.
+     */
+    public static List<Property> comparisonOrder(Configuration config, List<String> recordKeys) {
+        if (recordKeys.size() > 12)
+            throw new IllegalArgumentException("more than 12 record properties: HashMap order varies");
+        Map<String, Boolean> m = new HashMap<>();
+        for (String k : recordKeys) m.put(k, Boolean.TRUE);
+        List<Property> out = new ArrayList<>();
+        for (String k : m.keySet()) {
+            Property p = config.getPropertyByName(k);
+            if (p != null && !p.isIdProperty() && !p.isIgnoreProperty()) out.add(p);
+        }
+        return out;
     }
 
     long ctx() { return ctx; }
 
+    long ids() { return ids; }
+
     Record recordAtRow(int row) { return rows.get(row); }
+
+    long identAtRow(int row) { return rowIdent[row]; }
+
+    List<Property> properties() { return props; }
 
     boolean indexingIsDisabled() { return indexingIsDisabled; }
 
     // ---- Database (IncrementalLuceneDatabase.java) ----
     @Override public void setConfiguration(Configuration config) { this.config = config; }
 
-    @Override public void setOverwrite(boolean overwrite) { DukeHip.setOverwrite(ctx, overwrite); }
+    @Override public void setOverwrite(boolean overwrite) {                  // :99, :515
+        this.overwrite = overwrite;
+        DukeHip.setOverwrite(ctx, overwrite);
+    }
 
     @Override public boolean isInMemory() { return true; }
 
@@ -87,15 +156,21 @@ public class GpuBlockingDatabase implements Database {
     }
 
     @Override public Record findRecordById(String id) {              // :170-180
-        Integer row = liveRow.get(id);
-        return row == null ? null : rows.get(row);
+        long ident = DukeHip.internerFind(ids, id);
+        if (ident < 0) return null;
+        int row = DukeHip.rowOfIdent(ctx, ident);
+        return row < 0 ? null : rows.get(row);
     }
 
     @Override public Collection<Record> findCandidateMatches(Record record) {
         throw new UnsupportedOperationException("candidates come from dk_match (GpuProcessor)");
     }
 
-    @Override public void close() { DukeHip.destroy(ctx); }
+    @Override public void close() {
+        DukeHip.destroy(ctx);
+        rows.clear();
+        DukeHip.internerDestroy(ids);
+    }
 
     /** Records handed to index() before a deduplicate batch, committed with it. */
     List<Record> takePending() {
@@ -107,28 +182,72 @@ public class GpuBlockingDatabase implements Database {
     void dropTransient() {
         if (transientRow0 >= 0) {
             DukeHip.dropTransient(ctx);
-            while (rows.size() > transientRow0) rows.remove(rows.size() - 1);
+            rows.truncate(transientRow0);
             transientRow0 = -1;
         }
+    }
+
+    /** Every record the index holds, live versions (GpuProcessor's hand-over to stock Duke). */
+    List<Record> liveRecords() {
+        List<Record> out = new ArrayList<>();
+        for (int r = 0; r < rows.size(); r++) {
+            if (transientRow0 >= 0 && r >= transientRow0) break;
+            Record rec = rows.get(r);
+            if (rec != null && (overwrite || DukeHip.rowOfIdent(ctx, rowIdent[r]) == r)) out.add(rec);
+        }
+        return out;
+    }
+
+    private long[] intern(List<Record> batch) {
+        int n = batch.size();
+        String[] id = new String[n];
+        for (int i = 0; i < n; i++) {
+            id[i] = batch.get(i).getValue(idProp);
+            if (id[i] == null) throw new RuntimeException("record without ID property");
+        }
+        int[] off = new int[n + 1];
+        char[] units = arena(id, off, null);
+        return DukeHip.internerIntern(ids, off, units);
+    }
+
+    /** Rows the batch's IDs map to before the upsert: they are superseded by it. */
+    private int[] previousRows(long[] ident) {
+        int[] prev = new int[ident.length];
+        for (int i = 0; i < ident.length; i++) prev[i] = overwrite ? -1 : DukeHip.rowOfIdent(ctx, ident[i]);
+        return prev;
+    }
+
+    private void afterUpsert(long[] ident, int[] prev, int[] assigned, boolean asTransient) {
+        int row0 = assigned.length > 0 ? assigned[0] : rows.size();
+        if (rowIdent.length < row0 + ident.length)
+            rowIdent = java.util.Arrays.copyOf(rowIdent, Math.max(2 * rowIdent.length, row0 + ident.length));
+        System.arraycopy(ident, 0, rowIdent, row0, ident.length);
+        if (asTransient) return;
+        for (int i = 0; i < prev.length; i++) if (prev[i] >= 0) rows.release(prev[i]);
+        // an ID twice in this batch: the earlier copy is superseded by the later one, but it is
+        // still a query record of this batch -- released after the replay (releaseDeferred)
+        Map<Long, Integer> last = new HashMap<>();
+        for (int i = 0; i < ident.length; i++) {
+            Integer before = last.put(ident[i], assigned[i]);
+            if (before != null && !overwrite) deferred.add(before);
+        }
+    }
+
+    /** After a batch's replay: the rows its later copies superseded drop their Records. */
+    void releaseDeferred() {
+        for (int r : deferred) rows.release(r);
+        deferred.clear();
     }
 
     /** Packs `batch` column-wise and upserts it (dk_upsert, or dk_upsert_transient). */
     int[] indexBatch(List<Record> batch, boolean asTransient) {
         int n = batch.size();
         if (n == 0) return new int[0];
-        String idProp = config.getIdentityProperties().iterator().next().getName();
-        long[] ident = new long[n];
+        long[] ident = intern(batch);
         byte[] group = linkage ? new byte[n] : null;
         byte[] deleted = new byte[n];
         for (int i = 0; i < n; i++) {
             Record r = batch.get(i);
-            String id = r.getValue(idProp);
-            Long v = idents.get(id);
-            if (v == null) {
-                v = (long) idents.size();
-                idents.put(id, v);
-            }
-            ident[i] = v;
             deleted[i] = (byte) ("true".equals(r.getValue("dukeDeleted")) ? 1 : 0);
             if (linkage) {
                 String g = r.getValue("dukeGroupNo");
@@ -146,7 +265,7 @@ public class GpuBlockingDatabase implements Database {
             for (int i = 0; i < n; i++) {
                 Collection<String> vs = batch.get(i).getValues(props.get(p).getName());
                 if (vs != null && vs.size() > 1)
-                    throw new IllegalStateException("more than one value: not GPU-eligible");
+                    throw new DukeHipException(DukeHip.E_UNSUPPORTED, "more than one value for " + props.get(p).getName());
                 vals[i] = vs == null || vs.isEmpty() ? null : vs.iterator().next();
             }
             present[p] = new byte[n];
@@ -159,12 +278,44 @@ public class GpuBlockingDatabase implements Database {
             keyOffsets[k] = new int[n + 1];
             keyUnits[k] = arena(keys, keyOffsets[k], null);
         }
+        int[] prev = asTransient ? new int[0] : previousRows(ident);
         int[] assigned = DukeHip.upsert(ctx, asTransient, n, ident, group, deleted, offsets, units,
                                         present, keyOffsets, keyUnits);
         if (asTransient && transientRow0 < 0) transientRow0 = rows.size();
-        rows.addAll(batch);
-        if (!asTransient)
-            for (int i = 0; i < n; i++) liveRow.put(batch.get(i).getValue(idProp), assigned[i]);
+        rows.appendRecords(batch);
+        afterUpsert(ident, prev, assigned, asTransient);
+        return assigned;
+    }
+
+    /**
+     * The POSTed body of data source `src`, packed natively (dk_pack_json: no Gson tree, no
+     * Record objects) and upserted.  Returns the batch's rows; DukeHipException E_UNSUPPORTED
+     * when the native reader declines the body (the caller then takes the Record path).
+     */
+    int[] indexJson(byte[] body, JsonSource src, boolean asTransient) {
+        long packed = DukeHip.packJson(ids, body, src.datasetId, src.groupNo, src.columnNames,
+                                       src.columnProp, src.columnCleaner, props.size(), src.keyParts);
+        int n = DukeHip.packedSize(packed);
+        if (n == 0) {
+            DukeHip.freePacked(packed);
+            return new int[0];
+        }
+        if (linkage && src.groupNo == 0) {
+            DukeHip.freePacked(packed);
+            throw new RuntimeException("The 'dukeGroupNo' property was missing or empty!");
+        }
+        long[] ident = DukeHip.packedIdent(packed);
+        int[] prev = asTransient ? new int[0] : previousRows(ident);
+        int[] assigned;
+        try {
+            assigned = DukeHip.upsertPacked(ctx, packed, asTransient);
+        } catch (RuntimeException e) {
+            DukeHip.freePacked(packed);
+            throw e;
+        }
+        if (asTransient && transientRow0 < 0) transientRow0 = rows.size();
+        rows.appendPacked(new PackedBatch(packed, n, src, props));
+        afterUpsert(ident, prev, assigned, asTransient);
         return assigned;
     }
 
@@ -184,7 +335,7 @@ public class GpuBlockingDatabase implements Database {
         return vs == null || vs.isEmpty() ? null : vs.iterator().next();
     }
 
-    private static char[] arena(String[] vals, int[] off, byte[] present) {
+    static char[] arena(String[] vals, int[] off, byte[] present) {
         int total = 0;
         for (String v : vals) total += v == null ? 0 : v.length();
         char[] out = new char[total];
@@ -199,5 +350,153 @@ public class GpuBlockingDatabase implements Database {
         }
         off[vals.length] = at;
         return out;
+    }
+
+    /**
+     * A data source as dk_pack_json reads it (the microservice's IncrementalDataSource):
+     * dataset id, RecordLinkage group (0 = deduplication), its columns (JSON attribute, scored
+     * property index or -1, DukeHip.CLEAN_* cleaner) in data-source order, and the key
+     * functions as parts (PartsKeyFunction.parts(); null with the Lucene source).
+     */
+    public static final class JsonSource {
+        final String datasetId;
+        final int groupNo;
+        final String[] columnNames;
+        final int[] columnProp, columnCleaner;
+        final int[][] keyParts;
+
+        public JsonSource(String datasetId, int groupNo, String[] columnNames, int[] columnProp,
+                          int[] columnCleaner, int[][] keyParts) {
+            this.datasetId = datasetId;
+            this.groupNo = groupNo;
+            this.columnNames = columnNames;
+            this.columnProp = columnProp;
+            this.columnCleaner = columnCleaner;
+            this.keyParts = keyParts;
+        }
+    }
+
+    /** A natively packed batch: its columns stay in native memory, Records are built per row
+     *  on lookup (IncrementalDataSource.java:67-98's record shape). */
+    static final class PackedBatch {
+        final long handle;
+        final int n;
+        final JsonSource src;
+        final List<Property> props;
+        String[][] values;     // per scored property, fetched on the first lookup
+        String[] id, entityId;
+        byte[] deleted;
+
+        PackedBatch(long handle, int n, JsonSource src, List<Property> props) {
+            this.handle = handle;
+            this.n = n;
+            this.src = src;
+            this.props = props;
+        }
+
+        Record record(int i) {
+            if (values == null) {
+                values = new String[props.size()][];
+                for (int p = 0; p < props.size(); p++) values[p] = DukeHip.packedValues(handle, p);
+                id = DukeHip.packedIds(handle);
+                entityId = DukeHip.packedEntityIds(handle);
+                deleted = DukeHip.packedDeleted(handle);
+            }
+            RecordImpl r = new RecordImpl();   // [Duke 1.2, recalled] ModifiableRecord
+            for (int p = 0; p < props.size(); p++)
+                if (values[p][i] != null) r.addValue(props.get(p).getName(), values[p][i]);
+            if (src.groupNo != 0) r.addValue("dukeGroupNo", Integer.toString(src.groupNo));
+            r.addValue("ID", id[i]);
+            r.addValue("dukeOriginalEntityId", entityId[i]);
+            r.addValue("dukeDatasetId", src.datasetId);
+            if (deleted[i] != 0) r.addValue("dukeDeleted", "true");
+            return r;
+        }
+
+        void free() { DukeHip.freePacked(handle); }
+    }
+
+    /** row -> Record over segments of Record batches and packed batches; released rows drop
+     *  their Record, and a segment whose rows are all released drops its payload. */
+    static final class RowStore {
+        private static final class Segment {
+            final int row0, n;
+            List<Record> records;     // Record path
+            PackedBatch packed;       // native path
+            final BitSet released = new BitSet();
+            int live;
+
+            Segment(int row0, int n) {
+                this.row0 = row0;
+                this.n = n;
+                this.live = n;
+            }
+        }
+
+        private final List<Segment> segs = new ArrayList<>();
+        private int size;
+
+        int size() { return size; }
+
+        void appendRecords(List<Record> batch) {
+            Segment s = new Segment(size, batch.size());
+            s.records = new ArrayList<>(batch);
+            segs.add(s);
+            size += batch.size();
+        }
+
+        void appendPacked(PackedBatch b) {
+            Segment s = new Segment(size, b.n);
+            s.packed = b;
+            segs.add(s);
+            size += b.n;
+        }
+
+        private Segment seg(int row) {
+            int lo = 0, hi = segs.size();
+            while (hi - lo > 1) {
+                int mid = (lo + hi) >>> 1;
+                if (segs.get(mid).row0 <= row) lo = mid;
+                else hi = mid;
+            }
+            return segs.get(lo);
+        }
+
+        Record get(int row) {
+            if (row < 0 || row >= size) return null;
+            Segment s = seg(row);
+            int i = row - s.row0;
+            if (s.released.get(i)) return null;
+            return s.records != null ? s.records.get(i) : s.packed.record(i);
+        }
+
+        void release(int row) {
+            if (row < 0 || row >= size) return;
+            Segment s = seg(row);
+            int i = row - s.row0;
+            if (s.released.get(i)) return;
+            s.released.set(i);
+            if (s.records != null) s.records.set(i, null);
+            if (--s.live == 0) drop(s);
+        }
+
+        private static void drop(Segment s) {
+            s.records = null;
+            if (s.packed != null) {
+                s.packed.free();
+                s.packed = null;
+            }
+        }
+
+        void truncate(int n) {
+            while (!segs.isEmpty() && segs.get(segs.size() - 1).row0 >= n) drop(segs.remove(segs.size() - 1));
+            size = n;
+        }
+
+        void clear() {
+            for (Segment s : segs) drop(s);
+            segs.clear();
+            size = 0;
+        }
     }
 }

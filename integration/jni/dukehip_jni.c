@@ -581,6 +581,21 @@ JNIEXPORT jlong JFN(linkdbChangesSince)(JNIEnv* env, jclass cls, jlong db, jlong
   return (jlong)(intptr_t)l;
 }
 
+JNIEXPORT jlong JFN(linkdbLinksFor)(JNIEnv* env, jclass cls, jlong db, jlong ident) {
+  (void)cls;
+  dk_link_list* l = NULL;
+  if (throw_dk(env, dk_linkdb_links_for((const dk_linkdb*)(intptr_t)db, (uint64_t)ident, &l))) return 0;
+  return (jlong)(intptr_t)l;
+}
+
+JNIEXPORT jlong JFN(linkdbRetract)(JNIEnv* env, jclass cls, jlong db, jlong ident, jlong other, jlong timestamp) {
+  (void)cls;
+  uint64_t n = 0;
+  throw_dk(env, dk_linkdb_retract((dk_linkdb*)(intptr_t)db, (uint64_t)ident, other < 0 ? UINT64_MAX : (uint64_t)other,
+                                  (int64_t)timestamp, &n));
+  return (jlong)n;
+}
+
 #define LIST(h) ((const dk_link_list*)(intptr_t)(h))
 
 JNIEXPORT jlongArray JFN(linkListId1)(JNIEnv* env, jclass cls, jlong list) {

@@ -58,10 +58,12 @@ class SinceAwareLinkDB:
         self.seq += 1
         return True
 
-    def retract_all(self, rid, timestamp):          # App.java:994-999 (deleted records)
+    def retract(self, rid, timestamp, other=None):  # App.java:994-999 (deleted records)
         # getAllLinksFor(id), link.retract() [recalled: status RETRACTED, timestamp now] on the
         # stored Link itself, then assertLink (which then finds it unchanged)
         for l in self.all_links_for(rid):
+            if other is not None and other not in l.key():
+                continue
             l.status, l.timestamp = RETRACTED, timestamp
             self.order[l.key()] = self.seq
             self.seq += 1

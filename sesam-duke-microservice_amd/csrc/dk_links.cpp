@@ -265,15 +265,17 @@ int dk_linkdb_links_for(const dk_linkdb* db, uint64_t id, dk_link_list** out) {
   return list_of(sel, out);
 }
 
-// The deleted-record branch of the POST route (App.java:994-999): every link of the record
-// retracted -- Link.retract() [recalled: status RETRACTED, timestamp now] on the stored link
-// itself, so even an already retracted link takes the new timestamp
-int dk_linkdb_retract_all(dk_linkdb* db, uint64_t id, int64_t timestamp, uint64_t* nretracted) {
+// The deleted-record branch of the POST route (App.java:994-999): for every link of the
+// record, Link.retract() [recalled: status RETRACTED, timestamp now] on the stored link itself,
+// then assertLink -- so even an already retracted link takes the new timestamp.  `other` ==
+// UINT64_MAX: every link of `id`; else the one link between the two IDs.
+int dk_linkdb_retract(dk_linkdb* db, uint64_t id, uint64_t other, int64_t timestamp, uint64_t* nretracted) {
   if (!db) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
   uint64_t n = 0;
   auto bi = db->by_id.find(id);
   if (bi != db->by_id.end())
     for (const auto& k : bi->second) {
+      if (other != UINT64_MAX && k != db->key(id, other)) continue;
       auto it = db->links.find(k);
       if (it == db->links.end()) continue;
       it->second.status = DK_LINK_RETRACTED;

@@ -35,7 +35,7 @@ EXPORTS = ("dk_create", "dk_create_multi", "dk_num_devices", "dk_destroy", "dk_u
            "dk_interner_intern", "dk_pack_json", "dk_free_packed", "dk_interner_string",
            "dk_linkdb_create", "dk_linkdb_destroy", "dk_linkdb_size", "dk_linkdb_apply",
            "dk_linkdb_changes_since", "dk_free_link_list", "dk_linkdb_links_for",
-           "dk_linkdb_retract_all", "dk_lucene_analyze")
+           "dk_linkdb_retract", "dk_lucene_analyze")
 
 
 class DukeHipError(RuntimeError):

@@ -70,8 +70,8 @@ def _lib():
         L.dk_linkdb_changes_since.restype = C.c_int
         L.dk_linkdb_links_for.argtypes = [vp, C.c_uint64, C.POINTER(C.POINTER(dk_link_list))]
         L.dk_linkdb_links_for.restype = C.c_int
-        L.dk_linkdb_retract_all.argtypes = [vp, C.c_uint64, C.c_int64, C.POINTER(C.c_uint64)]
-        L.dk_linkdb_retract_all.restype = C.c_int
+        L.dk_linkdb_retract.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_int64, C.POINTER(C.c_uint64)]
+        L.dk_linkdb_retract.restype = C.c_int
         L.dk_free_link_list.argtypes = [C.POINTER(dk_link_list)]
         L.dk_free_link_list.restype = None
         L.dk_interner_string.argtypes = [vp, C.c_uint64, C.POINTER(C.POINTER(C.c_uint16)),
@@ -143,12 +143,14 @@ class LinkDatabase:
         A.check(self.lib.dk_linkdb_links_for(self.h, int(ident), C.byref(out)))
         return self._take(out)
 
-    def retract_all(self, ident, timestamp=None):
-        """The POST route's deleted-record branch (App.java:994-999): every link of the record
-        retracted (Link.retract() + assertLink).  Returns the number of links."""
+    def retract(self, ident, other=None, timestamp=None):
+        """The POST route's deleted-record branch (App.java:994-999): Link.retract() +
+        assertLink on the link between two interned IDs, or (other None) on every link of
+        `ident`.  Returns the number of links retracted."""
         n = C.c_uint64()
         ts = int(time.time() * 1000) if timestamp is None else int(timestamp)
-        A.check(self.lib.dk_linkdb_retract_all(self.h, int(ident), ts, C.byref(n)))
+        oth = 0xFFFFFFFFFFFFFFFF if other is None else int(other)
+        A.check(self.lib.dk_linkdb_retract(self.h, int(ident), oth, ts, C.byref(n)))
         return int(n.value)
 
     def _take(self, out):

@@ -168,8 +168,14 @@ def test_deleted_record_retraction_and_links_for(seed):
         cid = ids.intern([c for c, _, _ in flat]) if flat else np.zeros(0, np.uint64)
         ldb.apply(qid, first, cid, [p for _, p, _ in flat], [k for _, _, k in flat], timestamp=ts)
         for q in rng.sample(qs, min(2, len(qs))):        # deleted records of the next POST
-            ref.retract_all(q, ts + 5)
-            assert ldb.retract_all(ids.intern([q])[0], ts + 5) == len(ref.all_links_for(q))
+            links = ref.all_links_for(q)
+            if links and rng.random() < 0.5:              # one link of the record
+                o = links[0].id2 if links[0].id1 == q else links[0].id1
+                ref.retract(q, ts + 5, other=o)
+                assert ldb.retract(ids.intern([q])[0], ids.intern([o])[0], ts + 5) == 1
+            else:                                         # all of them
+                ref.retract(q, ts + 5)
+                assert ldb.retract(ids.intern([q])[0], timestamp=ts + 5) == len(links)
     for since in (0, 1050, 1100):
         ch = ldb.changes_since(since)
         got = [(interned_string(ids, a), interned_string(ids, b), int(s), int(k), float(c), int(t))
