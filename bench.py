@@ -226,6 +226,9 @@ def bpair_s8d(w, counts):
     from dukehip import _abi as A
     qs = np.asarray(w["queries"], dtype=np.int64)
     wt = np.asarray(counts, dtype=np.float64)
+    if len(qs) > 200_000:   # a uniform sample of the queries estimates the weighted means
+        pick = np.sort(np.random.default_rng(8).choice(len(qs), 200_000, replace=False))
+        qs, wt = qs[pick], wt[pick]
     tot = wt.sum()
     if tot <= 0:
         return None, {}
