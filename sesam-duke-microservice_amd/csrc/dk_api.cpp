@@ -1334,7 +1334,10 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
   P.lev_rows = 0;
   P.long_rows = 0;
   P.raw_prop = -1;
+  P.has_dp = 0;
   for (const auto& S : c->P) {
+    const int op = S.cfg.comparator;
+    if (op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER || op == DK_CMP_WEIGHTED_LEVENSHTEIN) P.has_dp = 1;
     if (S.cfg.comparator == DK_CMP_LEVENSHTEIN) {
       P.lev_rows = std::max(P.lev_rows, std::min(S.maxlen, kMaxUnits));
       if (S.maxlen > kMaxUnits) P.long_rows = std::max(P.long_rows, S.maxlen);

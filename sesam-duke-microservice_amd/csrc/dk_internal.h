@@ -107,7 +107,8 @@ struct ScoreParams {
   int32_t long_rows;      // longest value on the long-value DP (0 = none; selects the variant)
   int32_t raw_prop;       // >= 0: emit property raw_prop's comparator similarity instead of
                           // the probability (dk_property_similarity); -1 = normal scoring
-  int32_t pad_;
+  int32_t has_dp;         // some property is Levenshtein / JaroWinkler / WeightedLevenshtein
+                          // (0: the DP-free kernel variant, no DP code or registers)
   double threshold;
   double maybe;
   const uint64_t* ident;

@@ -24,6 +24,9 @@
 #ifndef DK_WAVES_SHORT
 #define DK_WAVES_SHORT 5  // k_score waves per SIMD up to 40 Levenshtein rows
 #endif
+#ifndef DK_WAVES_NODP
+#define DK_WAVES_NODP 8   // k_score_nodp waves per SIMD (no DP comparator: latency bound)
+#endif
 #ifndef DK_WAVES_LONG8
 #define DK_WAVES_LONG8 5  // k_score_long waves per SIMD, <= 8 DP rows per lane
 #endif
@@ -1199,7 +1202,7 @@ __device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool o
 // ------------------------------------------------------------------------------------
 // SYM: `rev` receives Comparator.compare(candidate, query) where it can differ from
 // compare(query, candidate) (JaroWinkler on equal lengths); it is left alone otherwise.
-template <int RMAX, int LR, typename CT, bool SYM>
+template <int RMAX, int LR, typename CT, bool SYM, bool DP>
 __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
                                              int lc, bool cmp, double& rev, uint32_t qch) {
@@ -1211,13 +1214,14 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
   double sim = 0.0;
   switch (D.op) {
     case DK_CMP_WEIGHTED_LEVENSHTEIN:
-      if (LR > 0) {  // the host only schedules WeightedLevenshtein on LR > 0 variants
+      if (DP && LR > 0) {  // the host only schedules WeightedLevenshtein on LR > 0 variants
         const bool same = cmp && str_equal(s1, lq, s2, lc);
         sim = same ? 1.0 : 0.0;
         sim = long_sims<LR, true, CT>(D, rstride, peq, q, lq, g, crow, lc, cmp && !same, sim);
       }
       break;
     case DK_CMP_LEVENSHTEIN:
+      if (!DP) break;  // the DP-free variant is only launched without DP comparators
       if (LR > 0 && lq > kMaxUnits) {  // query over 64 units: long-value DP
         bool need = false;
         if (cmp) {
@@ -1231,6 +1235,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
       }
       [[fallthrough]];
     case DK_CMP_JAROWINKLER: {
+      if (!DP) break;
       const bool table = lq <= 64 && (D.op == DK_CMP_LEVENSHTEIN || __ballot(cmp && lc > 64) == 0);
       if (table) {
         peq_set_unit<CT>(peq, qch, lq, true);
@@ -1388,7 +1393,7 @@ __device__ __forceinline__ double property_prob(const DevProp& D, double sim) {
 // SYM: the owner slots of the symmetric dedup schedule (PairSource::sym): every owned pair
 // is scored in both directions in one pass and the two probabilities go to S.ores; the
 // emission pass (k_emit) turns them into the match list.
-template <int RMAX, int LR, bool SYM>
+template <int RMAX, int LR, bool SYM, bool DP>
 __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
                                            uint64_t nslots, const StageOut& out) {
   uint64_t* peq = g_wave_tables[threadIdx.x >> 6];
@@ -1495,7 +1500,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     lq_ = (int)__builtin_amdgcn_readfirstlane((uint32_t)E.len[q]);
     const int lane = (int)lane_id();
     ch_ = 0u;
-    const bool table = E.op == DK_CMP_LEVENSHTEIN || E.op == DK_CMP_JAROWINKLER;  // Peq users
+    const bool table = DP && (E.op == DK_CMP_LEVENSHTEIN || E.op == DK_CMP_JAROWINKLER);  // Peq users
     if (table && lq_ != (int)kMissing && lane < lq_ && lane < 64) {
       const uint32_t o = __builtin_amdgcn_readfirstlane(E.off[q]);
       ch_ = E.width == 1 ? (uint32_t)reinterpret_cast<const uint8_t*>(E.units)[o + lane]
@@ -1525,8 +1530,8 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       rev = sim;
     } else if (D.op != DK_CMP_NONE) {
       rev = __builtin_nan("");  // marks "same as sim" unless the comparator sets it
-      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch)
-                         : string_sim<RMAX, LR, uint16_t, SYM>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch);
+      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM, DP>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch)
+                         : string_sim<RMAX, LR, uint16_t, SYM, DP>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch);
       if (!SYM || rev != rev) rev = sim;
       if (cmp) {
         if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2,
@@ -1570,14 +1575,23 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
 template <int RMAX, bool SYM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? DK_WAVES_SHORT : 4, 8)))
 void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
-  score_body<RMAX, 0, SYM>(P, S, slot0, nslots, out);
+  score_body<RMAX, 0, SYM, true>(P, S, slot0, nslots, out);
+}
+
+// Schemas without a DP comparator (QGram / Numeric / Exact / token comparators: configs[2]'s
+// linkage): none of the DP code, its registers or its spills; the kernel is memory-latency
+// bound, so it takes the occupancy instead.
+template <bool SYM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_NODP, 8)))
+void k_score_nodp(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
+  score_body<16, 0, SYM, false>(P, S, slot0, nslots, out);
 }
 
 template <int RMAX, int LR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LR <= 8 ? DK_WAVES_LONG8 : DK_WAVES_LONG16, 8)))
 void k_score_long(const ScoreParams P, const PairSource S,
                                                     uint64_t slot0, uint64_t nslots, StageOut out) {
-  score_body<RMAX, LR, false>(P, S, slot0, nslots, out);
+  score_body<RMAX, LR, false, true>(P, S, slot0, nslots, out);
 }
 
 // Emission pass of the symmetric dedup schedule: the query's slots in Duke's candidate
@@ -2421,7 +2435,10 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
   } while (0)
 #define DK_LONG(RM, L) k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
   if (src.sym && P.long_rows > 0) return hipErrorInvalidValue;  // the host never schedules it
-  if (P.long_rows > 0) {
+  if (!P.has_dp) {
+    if (src.sym) k_score_nodp<true><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+    else k_score_nodp<false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  } else if (P.long_rows > 0) {
     const bool lev64 = P.lev_rows > 16;
     if (P.long_rows <= 64) { if (lev64) DK_LONG(64, 4); else DK_LONG(16, 4); }
     else if (P.long_rows <= 128) { if (lev64) DK_LONG(64, 8); else DK_LONG(16, 8); }
