@@ -549,6 +549,18 @@ def main():
                 valu = {"insts_per_pair": ipp, "achieved": rate / 1e9, "peak": VALU_PEAK / 1e9,
                         "unit": "G wave-instructions/s", "frac": rate / VALU_PEAK,
                         "source": os.path.relpath(pmc, ROOT) + " (" + pj.get("commit", "?") + ")"}
+                # the achievable issue rate: the kernel's instruction mix priced by the measured
+                # cycles per wave-instruction (scripts/valu_mix.py: VOP3 / packed / f64 ~4
+                # cycles, plain VOP1/VOP2 ~2.3), not the 2-cycle best case
+                vm = os.path.join(ROOT, "profiles", "valu_mix.json")
+                if os.path.exists(vm):
+                    with open(vm) as f:
+                        mx = json.load(f).get(w["name"])
+                    if mx and mx.get("avg_cycles_per_valu"):
+                        ach = 1024 * 2.4e9 / mx["avg_cycles_per_valu"]
+                        valu.update(avg_cycles_per_valu=mx["avg_cycles_per_valu"],
+                                    peak_achievable=ach / 1e9, frac_achievable=rate / ach,
+                                    mix_source="profiles/valu_mix.json (" + mx["kernel"][:40] + ")")
         out = {
             "metric": METRIC,
             "value": value,
