@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DK_ABI_VERSION 5
+#define DK_ABI_VERSION 6
 
 /* status codes */
 #define DK_OK 0
@@ -211,6 +211,22 @@ int dk_upsert(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
  * until dk_drop_transient removes them again (App.java:1174-1175, indexing re-enabled). */
 int dk_upsert_transient(dk_ctx* ctx, const dk_batch* batch, uint32_t* rows_out);
 int dk_drop_transient(dk_ctx* ctx);
+/* Collection statistics (maxDoc, docFreq) of the Lucene candidate source.  Every upsert of a
+ * known ID deletes the older version and adds the new one (IncrementalLuceneDatabase.java:
+ * 516-517, 578-590); the older version is never a hit again, but Lucene 4 keeps counting a
+ * deleted document in maxDoc and docFreq until a merge of its segment reclaims it, and the
+ * reference never forces one (commit, :146-165).
+ *   DK_LUCENE_STATS_MERGED (default): the statistics of a fully merged index -- only the live
+ *     version of each ID (dukeDeleted records included) counts;
+ *   DK_LUCENE_STATS_UNMERGED: every version that entered the index counts until dk_lucene_merge
+ *     (IndexWriter.forceMerge) reclaims the superseded ones.  Lucene's background merge policy
+ *     reclaims them at times this ctx does not model: call dk_lucene_merge to follow it.
+ * Both are index changes (the next dk_match rebuilds the statistics).  DK_E_STATE without a
+ * Lucene source. */
+#define DK_LUCENE_STATS_MERGED 0
+#define DK_LUCENE_STATS_UNMERGED 1
+int dk_lucene_set_stats(dk_ctx* ctx, int mode);
+int dk_lucene_merge(dk_ctx* ctx);
 int dk_match(dk_ctx* ctx, const uint32_t* query_rows, uint64_t nq, int flags, dk_result** out);
 /* counts[i] = the candidates blocking produces for query_rows[i] (its buckets' sizes over
  * the key functions, before the isSameAs / already-a-candidate filters): the cost model for

@@ -63,6 +63,11 @@ public final class DukeHip {
 
     public static native void dropTransient(long ctx);                              // dk_drop_transient
 
+    public static final int LUCENE_STATS_MERGED = 0, LUCENE_STATS_UNMERGED = 1;
+    public static native void luceneSetStats(long ctx, int mode);                   // dk_lucene_set_stats
+
+    public static native void luceneMerge(long ctx);                                // dk_lucene_merge
+
     public static native void setOverwrite(long ctx, boolean on);                   // dk_set_overwrite
 
     public static native long numRows(long ctx);                                    // dk_num_rows

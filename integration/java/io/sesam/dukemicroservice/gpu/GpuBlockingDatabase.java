@@ -77,8 +77,9 @@ public class GpuBlockingDatabase implements Database {
         int[] lookup = null;
         int maxHits = 10;
         float minRelevance = 0.9f;
+        GpuEligibility.LuceneOptions opts = null;
         if (keyFunctions.isEmpty()) {   // IncrementalLuceneDatabase.findCandidateMatches on the device
-            GpuEligibility.LuceneOptions opts = GpuEligibility.lucene(config);
+            opts = GpuEligibility.lucene(config);
             maxHits = opts.maxSearchHits;
             minRelevance = opts.minRelevance;
             List<Property> lp = config.getLookupProperties();
@@ -95,6 +96,13 @@ public class GpuBlockingDatabase implements Database {
                                   config.getMaybeThreshold(), linkage ? DukeHip.MODE_LINKAGE : DukeHip.MODE_DEDUP,
                                   keyFunctions.size(), lookup, maxHits, minRelevance,
                                   devices == null || devices.length == 0 ? new int[] {0} : devices);
+        if (opts != null && opts.unmergedStats) DukeHip.luceneSetStats(ctx, DukeHip.LUCENE_STATS_UNMERGED);
+    }
+
+    /** IndexWriter.forceMerge of the Lucene source's statistics (dk_lucene_merge): superseded
+     *  versions stop counting in maxDoc / docFreq under DUKEHIP_LUCENE_STATS=unmerged. */
+    public void forceMerge() {
+        if (keyFunctions.isEmpty()) DukeHip.luceneMerge(ctx);
     }
 
     /**

@@ -52,10 +52,14 @@ public final class GpuEligibility {
     public static final class LuceneOptions {
         public final int maxSearchHits;
         public final float minRelevance;
+        /** DUKEHIP_LUCENE_STATS=unmerged: superseded versions keep counting in maxDoc / docFreq
+         *  (Lucene 4's deleted-but-unmerged documents) -- dk_lucene_set_stats */
+        public final boolean unmergedStats;
 
-        LuceneOptions(int maxSearchHits, float minRelevance) {
+        LuceneOptions(int maxSearchHits, float minRelevance, boolean unmergedStats) {
             this.maxSearchHits = maxSearchHits;
             this.minRelevance = minRelevance;
+            this.unmergedStats = unmergedStats;
         }
     }
 
@@ -75,7 +79,10 @@ public final class GpuEligibility {
             if (fuzzy && c != null && c.isTokenized())
                 throw new IllegalArgumentException("FUZZY_SEARCH over a tokenized comparator");
         }
-        return new LuceneOptions(maxHits, minRelevance);
+        String stats = System.getenv("DUKEHIP_LUCENE_STATS");
+        if (stats != null && !stats.equals("merged") && !stats.equals("unmerged"))
+            throw new IllegalArgumentException("DUKEHIP_LUCENE_STATS " + stats);
+        return new LuceneOptions(maxHits, minRelevance, "unmerged".equals(stats));
     }
 
     public static Opcode opcode(Comparator c) {

@@ -199,6 +199,16 @@ JNIEXPORT void JFN(dropTransient)(JNIEnv* env, jclass cls, jlong ctx) {
   throw_dk(env, dk_drop_transient(CTX(ctx)));
 }
 
+JNIEXPORT void JFN(luceneSetStats)(JNIEnv* env, jclass cls, jlong ctx, jint mode) {
+  (void)cls;
+  throw_dk(env, dk_lucene_set_stats(CTX(ctx), (int)mode));
+}
+
+JNIEXPORT void JFN(luceneMerge)(JNIEnv* env, jclass cls, jlong ctx) {
+  (void)cls;
+  throw_dk(env, dk_lucene_merge(CTX(ctx)));
+}
+
 JNIEXPORT void JFN(setOverwrite)(JNIEnv* env, jclass cls, jlong ctx, jboolean on) {
   (void)cls;
   throw_dk(env, dk_set_overwrite(CTX(ctx), on ? 1 : 0));

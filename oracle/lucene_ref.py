@@ -20,9 +20,12 @@ Follows the reference's IncrementalLuceneDatabase (src/main/java/io/sesam/dukemi
     decode(norm), norm byte = SmallFloat.floatToByte315(1/sqrt(#tokens)); float32 arithmetic
     except the per-document clause sum (double, in clause order: BooleanScorer's bucket) and
     its product with coord = overlap / #clauses;
-  * collection statistics of a fully merged index (maxDoc = documents in the index: every
-    live version, dukeDeleted ones included; superseded versions gone), ties by insertion
-    order (doc id).
+  * collection statistics: by default those of a fully merged index (maxDoc = documents in
+    the index: every live version, dukeDeleted ones included; superseded versions gone); with
+    `in_stats` those of an unmerged one -- the superseded versions (deleted by ID on re-post,
+    IncrementalLuceneDatabase.java:516-517, 578-590, never merged away: commit :146-165) still
+    count in maxDoc and docFreq, but are never hits (liveDocs); ties by insertion order
+    (doc id).
 [Duke 1.2, recalled] lookup properties (ConfigurationImpl.findLookupProperties): the scored
 properties sorted by <high> ascending; computeBayes over them from 0.5 until the result
 reaches maybe-threshold (threshold when that is 0.0): that property and every later one.
@@ -228,21 +231,24 @@ class LuceneIndexRef:
         self.linkage = linkage
         self.docs = []          # row -> dict or None (not in the index)
 
-    def set_docs(self, values, in_index, deleted=None, group=None):
+    def set_docs(self, values, in_index, deleted=None, group=None, in_stats=None):
         """values[f][row] (None = no value); in_index[row]: the row is a live version of an
-        indexed record (superseded and transient rows are not)."""
+        indexed record (superseded and transient rows are not); in_stats[row] (default
+        in_index): the row counts in maxDoc / docFreq (unmerged: every version indexed)."""
         n = len(in_index)
         self.values = values
         self.in_index = np.asarray(in_index, bool)
+        stats = self.in_index if in_stats is None else np.asarray(in_stats, bool)
+        assert not (self.in_index & ~stats).any()
         self.deleted = np.zeros(n, bool) if deleted is None else np.asarray(deleted, bool)
         self.group = np.zeros(n, np.int64) if group is None else np.asarray(group, np.int64)
-        self.max_doc = int(self.in_index.sum())
+        self.max_doc = int(stats.sum())
         self.postings = [dict() for _ in self.fields]     # term -> {row: tf}
         self.norms = [dict() for _ in self.fields]
         for fi in range(len(self.fields)):
             for r in range(n):
                 v = values[fi][r]
-                if not self.in_index[r] or v is None or v == "":
+                if not stats[r] or v is None or v == "":
                     continue
                 toks = analyze(v)
                 self.norms[fi][r] = norm_byte(len(toks))
@@ -279,7 +285,7 @@ class LuceneIndexRef:
         hits = []
         g = self.group[row]
         for r, (s, k) in acc.items():
-            if self.deleted[r] or (self.linkage and self.group[r] == g):
+            if not self.in_index[r] or self.deleted[r] or (self.linkage and self.group[r] == g):
                 continue
             hits.append((F(s * float(coord[k])), r))
         hits.sort(key=lambda h: (-float(h[0]), h[1]))

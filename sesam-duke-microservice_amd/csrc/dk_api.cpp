@@ -483,6 +483,7 @@ struct dk_ctx {
     std::vector<std::unordered_map<std::string, uint32_t>> dict;
     std::vector<uint64_t> qoff{0};
     uint64_t npost = 0, nsorted = 0, max_doc = 0;
+    bool unmerged = false;  // dk_lucene_set_stats(DK_LUCENE_STATS_UNMERGED)
     DevBuf pkey, ptf, qoff_d, qterm, norm, skey, stf, tkey, hits, exact;
   } luc;
 };
@@ -1104,7 +1105,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   std::vector<std::pair<uint64_t, uint32_t>> undo;
   c->ident_row.plan(row0 + n);
   for (uint64_t i = 0; i < n && !transient; ++i) {
-    flags[i] = kAlive | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
+    flags[i] = kAlive | kIndexed | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
     if (c->overwrite) continue;
     const uint32_t old = c->ident_row.get(b->ident[i]);
     if (old != IdentMap::kNoRow) {
@@ -1262,6 +1263,42 @@ static int drop_transient_impl(dk_ctx* c) {
 
 int dk_drop_transient(dk_ctx* c) {
   return guarded([&] { return drop_transient_impl(c); });
+}
+
+// Collection statistics of the Lucene source (include/dukehip.h dk_lucene_set_stats): every
+// upsert deletes the ID's older version and adds the new one (IncrementalLuceneDatabase.java:
+// 516-517, 578-590); Lucene 4 keeps a deleted document in maxDoc and docFreq until a merge of
+// its segment reclaims it, and the reference never forces one (commit, :146-165).
+static int lucene_stats_member(dk_ctx* m, void* a) {
+  if (!m->luc.on) return fail(DK_E_STATE, "the ctx has no Lucene candidate source");
+  m->luc.unmerged = *static_cast<int*>(a) == DK_LUCENE_STATS_UNMERGED;
+  m->index_gen++;  // the statistics are index state
+  return DK_OK;
+}
+
+static int lucene_merge_member(dk_ctx* m, void*) {
+  if (!m->luc.on) return fail(DK_E_STATE, "the ctx has no Lucene candidate source");
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(launch_lucene_merge(m->flags.as<uint8_t>(), m->nrows, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  m->index_gen++;
+  return DK_OK;
+}
+
+int dk_lucene_set_stats(dk_ctx* c, int mode) {
+  return guarded([&] {
+    if (!c) return fail(DK_E_INVALID, "ctx is NULL");
+    if (mode != DK_LUCENE_STATS_MERGED && mode != DK_LUCENE_STATS_UNMERGED)
+      return fail(DK_E_INVALID, "unknown statistics mode %d", mode);
+    return c->members.empty() ? lucene_stats_member(c, &mode) : group_each(c, lucene_stats_member, &mode);
+  });
+}
+
+int dk_lucene_merge(dk_ctx* c) {
+  return guarded([&] {
+    if (!c) return fail(DK_E_INVALID, "ctx is NULL");
+    return c->members.empty() ? lucene_merge_member(c, nullptr) : group_each(c, lucene_merge_member, nullptr);
+  });
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1697,7 +1734,8 @@ static int build_delta(dk_ctx* c, BlockTables& T) {
 
 // Lucene source: the postings of the rows in the index (kAlive: superseded versions were
 // deleted by ID, transient rows never entered; dukeDeleted rows stay, as in the reference's
-// index) sorted by (field, term, row), and maxDoc.  Index state, built like the blocking
+// index; with unmerged statistics also the superseded versions, kIndexed, which k_lucene_topk
+// never returns) sorted by (field, term, row), and maxDoc.  Index state, built like the blocking
 // tables by the first match after an index change.
 static int build_lucene(dk_ctx* c, BlockTables& T, uint64_t* Mout) {
   auto& L = c->luc;
@@ -1709,7 +1747,7 @@ static int build_lucene(dk_ctx* c, BlockTables& T, uint64_t* Mout) {
   uint64_t* cnt = c->counters.as<uint64_t>() + 2;
   HIPCHK(hipMemsetAsync(cnt, 0, 16, s));
   HIPCHK(launch_lucene_prep(L.pkey.as<uint64_t>(), np, c->flags.as<uint8_t>(), c->nrows,
-                            L.tkey.as<uint64_t>(), cnt, s));
+                            L.unmerged ? kIndexed : kAlive, L.tkey.as<uint64_t>(), cnt, s));
   if (np) {
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return sort_pairs_u64_u32(t, b, L.tkey.as<uint64_t>(), L.skey.as<uint64_t>(), L.ptf.as<uint32_t>(),

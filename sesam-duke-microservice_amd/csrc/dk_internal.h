@@ -44,6 +44,9 @@ __host__ __device__ constexpr bool uses_codes(int op) {
 
 constexpr uint8_t kAlive = 1;    // not superseded by a later upsert of the same ID
 constexpr uint8_t kDeleted = 2;  // dukeDeleted == "true" (IncrementalLuceneDatabase.java:478)
+// entered the index (not transient); kept when the row is superseded, so a superseded version
+// still counts in the Lucene source's unmerged statistics until dk_lucene_merge
+constexpr uint8_t kIndexed = 4;
 // replica identity of a base-table position whose row was superseded after the base was
 // sorted (delete-by-ID, IncrementalLuceneDatabase.java:516-517): never a candidate.  dk_upsert
 // rejects this identity value.
@@ -291,7 +294,8 @@ struct LuceneParams {
 // postings of rows that are in the index (kAlive): key kept, others set to ~0 (sorted last);
 // counts[0] += entries kept, counts[1] += rows in the index among [0, nrows)
 hipError_t launch_lucene_prep(const uint64_t* key, uint64_t npost, const uint8_t* flags, uint64_t nrows,
-                              uint64_t* out_key, uint64_t* counts, hipStream_t s);
+                              uint8_t mask, uint64_t* out_key, uint64_t* counts, hipStream_t s);
+hipError_t launch_lucene_merge(uint8_t* flags, uint64_t nrows, hipStream_t s);
 hipError_t launch_lucene_topk(const LuceneParams& L, hipStream_t s);
 hipError_t launch_widen_u8(const uint8_t* src, uint16_t* dst, uint64_t n, hipStream_t s);
 hipError_t launch_clear_flag(uint8_t* flags, const uint32_t* rows, uint64_t n, uint8_t bit,

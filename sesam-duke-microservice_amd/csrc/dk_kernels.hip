@@ -2063,18 +2063,21 @@ __global__ void k_mark_dead(const BlockTables T, const uint32_t* __restrict__ ro
 // Lucene-compatible candidate source (DK_CAND_LUCENE): IncrementalLuceneDatabase.
 // findCandidateMatches + EstimateResultTracker.doQuery over a postings table
 // ------------------------------------------------------------------------------------
+// The postings and maxDoc of the collection statistics: rows with a bit of `mask` set --
+// kAlive (merged: superseded versions gone) or kIndexed (unmerged: superseded versions still
+// counted, as Lucene counts deleted documents until their segment is merged).
 __global__ void k_lucene_prep(const uint64_t* __restrict__ key, uint64_t npost,
-                              const uint8_t* __restrict__ flags, uint64_t nrows,
+                              const uint8_t* __restrict__ flags, uint64_t nrows, uint8_t mask,
                               uint64_t* __restrict__ out_key, uint64_t* __restrict__ counts) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t kept = 0, docs = 0;
   if (i < npost) {
     const uint64_t k = key[i];
-    const bool in = (flags[(uint32_t)k] & kAlive) != 0;
+    const bool in = (flags[(uint32_t)k] & mask) != 0;
     out_key[i] = in ? k : ~0ull;
     kept = in;
   }
-  if (i < nrows) docs = (flags[i] & kAlive) != 0;
+  if (i < nrows) docs = (flags[i] & mask) != 0;
   for (int o = 32; o > 0; o >>= 1) {
     kept += __shfl_xor(kept, o);
     docs += __shfl_xor(docs, o);
@@ -2191,7 +2194,7 @@ __global__ __launch_bounds__(256) void k_lucene_topk(const LuceneParams L) {
       const int k = cnt[j];
       if (!k) continue;
       const uint32_t row = t0 + (uint32_t)j;
-      if (L.flags[row] & kDeleted) continue;
+      if ((L.flags[row] & (kAlive | kDeleted)) != kAlive) continue;  // liveDocs; dukeDeleted
       if (L.linkage && L.group[row] == qgroup) continue;
       const float score = (float)(acc[j] * (double)coordf[k]);
       if (!(score >= L.min_relevance)) continue;
@@ -2474,10 +2477,23 @@ hipError_t launch_first(const uint32_t* qidx, uint64_t n, uint64_t nq, uint64_t*
 }
 
 hipError_t launch_lucene_prep(const uint64_t* key, uint64_t npost, const uint8_t* flags, uint64_t nrows,
-                              uint64_t* out_key, uint64_t* counts, hipStream_t s) {
+                              uint8_t mask, uint64_t* out_key, uint64_t* counts, hipStream_t s) {
   const uint64_t n = std::max(npost, nrows);
   DK_LAUNCH_GUARD(n);
-  k_lucene_prep<<<grid1d(n), 256, 0, s>>>(key, npost, flags, nrows, out_key, counts);
+  k_lucene_prep<<<grid1d(n), 256, 0, s>>>(key, npost, flags, nrows, mask, out_key, counts);
+  return hipGetLastError();
+}
+
+// IndexWriter.forceMerge: superseded versions leave the statistics
+__global__ void k_lucene_merge(uint8_t* flags, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !(flags[i] & kAlive)) flags[i] &= (uint8_t)~kIndexed;
+}
+
+hipError_t launch_lucene_merge(uint8_t* flags, uint64_t nrows, hipStream_t s) {
+  if (!nrows) return hipSuccess;
+  DK_LAUNCH_GUARD(nrows);
+  k_lucene_merge<<<grid1d(nrows), 256, 0, s>>>(flags, nrows);
   return hipGetLastError();
 }
 

@@ -24,9 +24,11 @@ MODE_DEDUP, MODE_LINKAGE, MODE_ALLPAIRS = 0, 1, 2
 KIND_MATCH, KIND_MAYBE = 1, 2
 
 MATCH_HOST, MATCH_DEVICE = 0, 1
-ABI_VERSION = 5   # include/dukehip.h DK_ABI_VERSION
+LUCENE_STATS_MERGED, LUCENE_STATS_UNMERGED = 0, 1
+ABI_VERSION = 6   # include/dukehip.h DK_ABI_VERSION
 
 EXPORTS = ("dk_create", "dk_create_multi", "dk_num_devices", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
+           "dk_lucene_set_stats", "dk_lucene_merge",
            "dk_match", "dk_candidate_counts", "dk_result_copy_to_device",
            "dk_free_result", "dk_result_region_layout", "dk_set_result_region",
            "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite", "dk_num_rows", "dk_row_of_ident", "dk_set_profiling", "dk_get_profile",
@@ -131,6 +133,8 @@ def load():
     L.dk_upsert.argtypes = [vp, C.POINTER(dk_batch), vp]
     L.dk_upsert_transient.argtypes = [vp, C.POINTER(dk_batch), vp]
     L.dk_drop_transient.argtypes = [vp]
+    L.dk_lucene_set_stats.argtypes = [vp, C.c_int]
+    L.dk_lucene_merge.argtypes = [vp]
     L.dk_match.argtypes = [vp, vp, C.c_uint64, C.c_int, C.POINTER(C.POINTER(dk_result))]
     L.dk_candidate_counts.argtypes = [vp, vp, C.c_uint64, vp]
     L.dk_candidate_counts.restype = C.c_int
@@ -154,6 +158,7 @@ def load():
     L.dk_last_error.restype = C.c_char_p
     L.dk_abi_version.restype = C.c_int
     for f in ("dk_create", "dk_upsert", "dk_upsert_transient", "dk_drop_transient", "dk_match",
+              "dk_lucene_set_stats", "dk_lucene_merge",
               "dk_compare_rows", "dk_compare_values", "dk_property_similarity", "dk_set_overwrite",
               "dk_set_profiling",
               "dk_result_region_layout", "dk_set_result_region",

@@ -187,6 +187,16 @@ class GpuEngine:
     def drop_transient(self):
         A.check(self.lib.dk_drop_transient(self.ctx))
 
+    def lucene_stats(self, unmerged):
+        """dk_lucene_set_stats: Lucene collection statistics of a merged index (default), or
+        unmerged -- superseded versions keep counting in maxDoc / docFreq until lucene_merge."""
+        A.check(self.lib.dk_lucene_set_stats(self.ctx, A.LUCENE_STATS_UNMERGED if unmerged
+                                             else A.LUCENE_STATS_MERGED))
+
+    def lucene_merge(self):
+        """dk_lucene_merge (IndexWriter.forceMerge): superseded versions leave the statistics."""
+        A.check(self.lib.dk_lucene_merge(self.ctx))
+
     def match(self, query_rows, on_device=False):
         q = np.ascontiguousarray(query_rows, dtype=np.uint32)
         res = C.POINTER(A.dk_result)()

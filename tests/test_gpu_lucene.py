@@ -25,6 +25,11 @@ def expected(props, vals, lookup, ident, in_index, deleted, group, queries, thr,
              min_rel, mode):
     ref = R.LuceneIndexRef([f"f{i}" for i in lookup], max_hits, min_rel, linkage=mode == "linkage")
     ref.set_docs([vals[i] for i in lookup], in_index, deleted, group)
+    return expected_with(ref, props, vals, lookup, ident, queries, thr, maybe)
+
+
+def expected_with(ref, props, vals, lookup, ident, queries, thr=0.9, maybe=0.7):
+    """The pair list of Processor.compare over `ref`'s hits (isSameAs dropped)."""
     ot = O.OracleTable(props, vals, ident=ident, threshold=thr, maybe=maybe)
     out = {"query": [], "candidate": [], "prob": [], "kind": []}
     scored = 0
@@ -197,4 +202,73 @@ def test_malformed_large_batch_rejected(defect):
     res = eng.match(q)
     check(res, want, scored)
     res.close()
+    eng.close()
+
+
+def indexed_versions(ident, b):
+    """(alive, in_stats) after rows [0, b): the live version of each ID, and every version."""
+    alive = np.ones(b, bool)
+    last = {}
+    for r in range(b):
+        if int(ident[r]) in last:
+            alive[last[int(ident[r])]] = False
+        last[int(ident[r])] = r
+    return alive, np.ones(b, bool)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_lucene_unmerged_statistics_after_reposts(devices):
+    """Re-posted IDs under both statistics modes.  Every re-post deletes the older version and
+    adds the new one (IncrementalLuceneDatabase.java:516-517, 578-590); DK_LUCENE_STATS_MERGED
+    (the default, checked with re-posts by test_lucene_candidates_equal_restatement) counts only
+    live versions in maxDoc / docFreq, DK_LUCENE_STATS_UNMERGED keeps the superseded versions in
+    both (Lucene 4's deleted-but-unmerged documents) until dk_lucene_merge -- never as hits."""
+    p = synth.persons(1300, 600, seed=64)
+    vals = [p["name"], p["address"], p["dob"]]
+    n = len(vals[0])
+    ident = np.arange(n, dtype=np.uint64)
+    ident[1300:1600] = ident[0:300]                 # 300 re-posts of the first batch's IDs
+    ident[1700:1750] = ident[1300:1350]             # re-posts of re-posts
+    deleted = np.zeros(n, np.uint8)
+    lookup, max_hits, min_rel = [1, 2, 0], 5, 0.3
+    sch = schema_of(PROPS, 0.9, 0.7, "dedup", 0)
+    A.lucene_source(sch, lookup, max_hits, min_rel)
+    eng = dh.GpuEngine(sch, devices=devices)
+    eng.lucene_stats(unmerged=True)
+    differs = 0
+    for a, b in [(0, 1000), (1000, 1500), (1500, n)]:
+        upsert(eng, vals, ident, a, b)
+        alive, every = indexed_versions(ident, b)
+        q = np.arange(0, b, 3, dtype=np.uint32)
+        args = (PROPS, [v[:b] for v in vals], lookup, ident[:b])
+        res = eng.match(q)
+        ref = R.LuceneIndexRef([f"f{i}" for i in lookup], max_hits, min_rel)
+        ref.set_docs([vals[i][:b] for i in lookup], alive, deleted[:b], None, in_stats=every)
+        want = expected_with(ref, *args, q)
+        check(res, *want)
+        res.close()
+        merged = expected(*args, alive, deleted[:b], None, q, 0.9, 0.7, max_hits, min_rel, "dedup")
+        differs += merged != want
+    assert differs >= 1      # the superseded versions do move the scores
+    eng.lucene_merge()       # forceMerge: back to the merged statistics
+    alive, _ = indexed_versions(ident, n)
+    q = np.arange(0, n, 3, dtype=np.uint32)
+    res = eng.match(q)
+    check(res, *expected(PROPS, vals, lookup, ident, alive, deleted, None, q, 0.9, 0.7, max_hits,
+                         min_rel, "dedup"))
+    res.close()
+    eng.lucene_stats(unmerged=False)
+    res = eng.match(q)
+    check(res, *expected(PROPS, vals, lookup, ident, alive, deleted, None, q, 0.9, 0.7, max_hits,
+                         min_rel, "dedup"))
+    res.close()
+    eng.close()
+
+
+def test_lucene_stats_needs_lucene_source():
+    sch = schema_of(PROPS, 0.9, 0.7, "dedup", 1)
+    eng = dh.GpuEngine(sch)
+    assert eng.lib.dk_lucene_set_stats(eng.ctx, A.LUCENE_STATS_UNMERGED) == A.DK_E_STATE
+    assert eng.lib.dk_lucene_merge(eng.ctx) == A.DK_E_STATE
+    assert eng.lib.dk_lucene_set_stats(eng.ctx, 7) == A.DK_E_INVALID
     eng.close()
