@@ -398,13 +398,116 @@ __device__ __forceinline__ int compact_distance_pk(const uint64_t* peq, int n1, 
   return result;
 }
 
+// ------------------------------------------------------------------------------------
+// compact_distance_pk with the column loop unrolled over one candidate word (UPW columns)
+// and two register sets used in turn (ping-pong): column t reads set A and writes set B,
+// column t+1 reads B and writes A.  In the rolled loop a cell's `diag` is the previous
+// column's value of the row above, which the row above has already overwritten, so the
+// compiler kept two sets anyway and copied the new one back at every back-edge (one
+// v_mov per packed pair per column, and the copy of the prefetched word forced a vmcnt(0)
+// wait in the same column).  Unrolled, every value has a fixed register, the unit offset
+// inside the word is a constant, and the next word is issued a whole word (UPW columns)
+// ahead.  Lanes whose DP ended keep stepping (their result is latched; a masked lane
+// costs the SIMD nothing) until no lane of the wave is live, checked after every column.
+// The outcome is the same function of (peq, n1, s2, n2) as compact_distance_pk's.
+// ------------------------------------------------------------------------------------
+template <int R, typename CT>
+__device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, const Str<CT>& s2,
+                                                   int n2, bool act) {
+  constexpr int UPW = Str<CT>::UPW;
+  static_assert(UPW % 2 == 0, "the register sets alternate within one word");
+  constexpr int H = R / 2;
+  constexpr int TAIL = R <= 32 ? 4 : 8;  // rows past n1 lie in (R - TAIL, R]
+  constexpr int NC = (H + 15) / 16;      // cost words
+  constexpr uint32_t BIG = 0x7000u;
+  const int maxdist = min(n1, n2) >> 1;
+  const uint32_t B = 0x4000u - (uint32_t)(maxdist + 1);
+  uint32_t PA[H + 1], PB[H + 1];
+#pragma unroll
+  for (int i = 1; i <= H; ++i) PA[i] = ((uint32_t)i + B) | (BIG << 16);
+  uint32_t tm[H + 1];
+#pragma unroll
+  for (int i = 1; i <= H; ++i)
+    tm[i] = (i > n1 ? 0x4000u : 0u) | (H + i > n1 ? 0x40000000u : 0u);
+  const bool bottom_result = n1 > H;
+  int result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
+  bool live = act && n2 > 1;
+  const int fin = n2 - 1 + (bottom_result ? 1 : 0);
+
+  uint32_t w = act ? s2.word(0) : 0u;  // units of columns [t0, t0 + UPW)
+  uint32_t wn = s2.word_pf(1);         // the next word
+  uint64_t ne_cur = ~peq_eq<CT>(peq, Str<CT>::unit(w, 0));
+  uint64_t ne_prev = ~0ull;
+  uint32_t h2 = BIG;  // top row H of column t-2
+  uint32_t acc_prev = 0;
+  // column t = t0 + U from Pin into Pout; false once no lane of the wave is live
+  auto step = [&](auto U_, uint32_t(&Pin)[H + 1], uint32_t(&Pout)[H + 1], int t0) -> bool {
+    constexpr int U = decltype(U_)::value;
+    const int t = t0 + U;
+    const uint32_t xn = U + 1 < UPW ? Str<CT>::unit(w, U + 1) : Str<CT>::unit(wn, 0);
+    const uint64_t ne_nx = ~peq_eq<CT>(peq, xn);
+    uint32_t C[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      C[c] = ((uint32_t)(ne_cur >> (16 * c)) & 0xFFFFu) | ((uint32_t)(ne_prev >> (H + 16 * c)) << 16);
+    const uint32_t h1 = Pin[H] & 0xFFFFu;  // top row H of column t-1
+    uint32_t above = ((uint32_t)t + 1u + B) | (h1 << 16);
+    uint32_t diag = ((uint32_t)t + B) | (h2 << 16);
+    uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 1; i <= H; ++i) {
+      const uint32_t cost = (C[(i - 1) >> 4] >> ((i - 1) & 15)) & 0x10001u;
+      const uint32_t v = pk_min3_u16(above, diag, Pin[i]) + cost;
+      diag = Pin[i];
+      Pout[i] = v;
+      above = v;
+      if (H + i > R - TAIL) acc &= v | tm[i];
+      else acc &= v;
+    }
+    h2 = h1;
+    if (live) {
+      if (t >= 2 && (acc_prev & acc & 0x40004000u) == 0x40004000u) {  // column t-1 cut off
+        result = maxdist + 1;
+        live = false;
+      } else if (t == fin) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int row = R - TAIL + 1; row <= R; ++row)
+          if (row == n1) r = row <= H ? (Pout[row] & 0xFFFFu) : (Pout[row - H] >> 16);
+        result = (int)(r - B);
+        live = false;
+      }
+    }
+    acc_prev = acc;
+    ne_prev = ne_cur;
+    ne_cur = ne_nx;
+    return __ballot(live) != 0ull;
+  };
+  if (__ballot(live) != 0ull) {
+    for (int t0 = 0;; t0 += UPW) {
+      const uint32_t wn2 = s2.word_pf(t0 / UPW + 2);  // a whole word of columns ahead
+      if (!step(std::integral_constant<int, 0>{}, PA, PB, t0)) break;
+      if (!step(std::integral_constant<int, 1>{}, PB, PA, t0)) break;
+      if constexpr (UPW == 4) {
+        if (!step(std::integral_constant<int, 2>{}, PA, PB, t0)) break;
+        if (!step(std::integral_constant<int, 3>{}, PB, PA, t0)) break;
+      }
+      w = wn;
+      wn = wn2;
+    }
+  }
+  return result;
+}
+
 // [Duke 1.2] comparators.Levenshtein.compare.  RMAX: the largest row bucket this kernel
 // variant instantiates (the host picks the variant from the longest Levenshtein value),
 // which bounds the VGPRs of the whole fused kernel and so its occupancy.
-#ifdef DK_LEV_SCALAR
+#if defined(DK_LEV_SCALAR)
 #define DK_LEV_DP compact_distance_peq
-#else
+#elif defined(DK_LEV_ROLLED)
 #define DK_LEV_DP compact_distance_pk
+#else
+#define DK_LEV_DP compact_distance_pp
 #endif
 
 template <int RMAX, typename CT>
