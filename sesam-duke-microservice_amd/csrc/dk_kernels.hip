@@ -523,8 +523,22 @@ __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str
     if (2 * len <= maxlen) run = false;
     else if (len == maxlen && str_equal(s1, n1, s2, n2)) { r = 1.0; run = false; }
   }
-  // row buckets of 4 up to 32 rows, of 8 above (n1 is wave-uniform: a scalar switch)
+  // row buckets of 2 up to 16 rows (a date "YYYY-MM-DD" takes 10 rows, not 12), of 4 up to
+  // 32, of 8 above (n1 is wave-uniform: a scalar switch)
   int d;
+#ifndef DK_LEV_BUCKET4
+  if (n1 <= 16) {
+    switch ((n1 + 1) >> 1) {
+      case 1: case 2: d = DK_LEV_DP<4>(peq, n1, s2, n2, run); break;
+      case 3: d = DK_LEV_DP<6>(peq, n1, s2, n2, run); break;
+      case 4: d = DK_LEV_DP<8>(peq, n1, s2, n2, run); break;
+      case 5: d = DK_LEV_DP<10>(peq, n1, s2, n2, run); break;
+      case 6: d = DK_LEV_DP<12>(peq, n1, s2, n2, run); break;
+      case 7: d = DK_LEV_DP<14>(peq, n1, s2, n2, run); break;
+      default: d = DK_LEV_DP<16>(peq, n1, s2, n2, run); break;
+    }
+  } else
+#endif
   switch ((n1 + 3) >> 2) {
     case 1: d = DK_LEV_DP<4>(peq, n1, s2, n2, run); break;
     case 2: d = DK_LEV_DP<8>(peq, n1, s2, n2, run); break;
