@@ -403,6 +403,9 @@ struct dk_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // device->host copies of finished chunks
+  // symmetric schedule: chunk i's emission pass runs here beside chunk i+1's owner scoring
+  hipStream_t emit_stream = nullptr;
+  hipEvent_t score_done = nullptr;  // a chunk's owner results are complete
   hipEvent_t chunk_done = nullptr;
   uint64_t nrows = 0, cap = 0;
   DevBuf ident, flags, group;
@@ -449,6 +452,8 @@ struct dk_ctx {
   DevBuf counters;
   struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx; };
   StageBufs stage[2];                          // double-buffered per-chunk staging
+  StageBufs owner_stage;  // block counters of the owner phase (it emits no entries)
+  DevBuf etmp;            // scan scratch of the emission stream
   hipEvent_t count_ready[2] = {nullptr, nullptr};  // a chunk's entry count reached hs[]
   hipEvent_t compact_done[2] = {nullptr, nullptr}; // a chunk's staging set was drained
   // deferred profiling spans (Timer), resolved after dk_match's final synchronisation
@@ -620,6 +625,8 @@ static int create_impl(const dk_schema* schema, int device, dk_ctx** out) {
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->emit_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->score_done, hipEventDisableTiming);
   for (int b = 0; b < 2 && e == hipSuccess; ++b)
     e = hipEventCreateWithFlags(&c->count_ready[b], hipEventDisableTiming);
   for (int b = 0; b < 2 && e == hipSuccess; ++b)
@@ -652,10 +659,11 @@ void dk_destroy(dk_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->copy_stream);
+  if (c->emit_stream) (void)hipStreamSynchronize(c->emit_stream);
   if (c->region.base) (void)hipHostUnregister(c->region.base);
   if (c->pair_ctx) dk_destroy(c->pair_ctx);
-  hipStream_t s = c->stream, cs = c->copy_stream;
-  hipEvent_t ev = c->chunk_done;
+  hipStream_t s = c->stream, cs = c->copy_stream, es = c->emit_stream;
+  hipEvent_t ev = c->chunk_done, sd = c->score_done;
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->count_ready)
     if (e) (void)hipEventDestroy(e);
@@ -663,6 +671,8 @@ void dk_destroy(dk_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   delete c;
   if (ev) (void)hipEventDestroy(ev);
+  if (sd) (void)hipEventDestroy(sd);
+  if (es) (void)hipStreamDestroy(es);
   if (cs) (void)hipStreamDestroy(cs);
   (void)hipStreamDestroy(s);
 }
@@ -1819,6 +1829,15 @@ static int ensure_tables(dk_ctx* c, BlockTables* Tout, uint64_t* Mout) {
   return DK_OK;
 }
 
+// DK_EMIT_OVERLAP=1: the symmetric schedule's emission pass on its own stream, beside the
+// next chunk's owner scoring.  Off by default: measured on configs[1] the step gained 0.1 ms
+// (34.36 vs 34.45, 2 x 20 steps) because the two kernels share the CUs, while k_score's
+// launches stretched by the emission's work (profiles/r03/ab_emit_ne_tail/).
+static bool emit_overlap() {
+  const char* e = getenv("DK_EMIT_OVERLAP");
+  return e && e[0] == '1';
+}
+
 static bool sym_enabled() {
   const char* e = getenv("DK_SYM");
   return !(e && e[0] == '0');
@@ -1913,6 +1932,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
                      ResultHolder* R, bool contiguous) {
   hipStream_t s = c->stream;
   c->spans.clear();   // left over by a failed call
+  HIPCHK(hipStreamSynchronize(c->emit_stream));  // (idle unless a failed call left work)
+  HIPCHK(hipStreamSynchronize(c->copy_stream));
   c->ev_next = 0;
   const auto t0 = std::chrono::steady_clock::now();
   const int nk = c->schema.nkeys;
@@ -2019,7 +2040,14 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     total = nq * mpad;
     generated = nq * M;
   }
-  const uint64_t CH = (chunk_slots() + kScoreBlock - 1) / kScoreBlock * kScoreBlock;
+  // at least kMinChunks chunks (down to CH0/16 slots each): the emission pass and the list's
+  // copies of chunk i overlap the scoring of chunk i+1, so a small call (one GPU's tile of a
+  // multi-GPU match) still pipelines
+  constexpr uint64_t kMinChunks = 8;
+  const uint64_t CH0 = chunk_slots();
+  const uint64_t CH = std::max<uint64_t>(
+      kScoreBlock, (std::max(CH0 / 16, std::min(CH0, (total + kMinChunks - 1) / kMinChunks)) +
+                    kScoreBlock - 1) / kScoreBlock * kScoreBlock);
   // chunk boundaries in slots: full chunks, then (host modes) the last two chunks' worth
   // halved down to CH/16, so the copy of the final chunk's entries (not overlapped with
   // scoring) is short.  The symmetric schedule cuts by queries instead (an emission chunk
@@ -2083,6 +2111,18 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     st[b] = StageOut{c->counters.as<uint64_t>(), G.bcnt.as<uint32_t>(), G.bscored.as<uint32_t>(),
                      G.bbytes.as<uint32_t>(), G.prob.as<double>(), G.cand.as<uint32_t>(),
                      G.qidx.as<uint32_t>()};
+  }
+  StageOut so{};  // SYM: the owner phase's block counters (it stages no entries)
+  if (sym) {
+    uint64_t ochunk = 1;
+    for (size_t i = 0; i + 1 < obounds.size(); ++i) ochunk = std::max(ochunk, obounds[i + 1] - obounds[i]);
+    const uint64_t onblk = (ochunk + kScoreBlock - 1) / kScoreBlock;
+    dk_ctx::StageBufs& G = c->owner_stage;
+    HIPCHK(G.bcnt.reserve(onblk * 4 + 4, 0, s));
+    HIPCHK(G.bscored.reserve(onblk * 4 + 4, 0, s));
+    HIPCHK(G.bbytes.reserve(onblk * 4 + 4, 0, s));
+    so = StageOut{c->counters.as<uint64_t>(), G.bcnt.as<uint32_t>(), G.bscored.as<uint32_t>(),
+                  G.bbytes.as<uint32_t>(), nullptr, nullptr, nullptr};
   }
   HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * sizeof(uint64_t), s));
   ResultBufs& B = *R->bufs;
@@ -2195,25 +2235,34 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     return DK_OK;
   };
   const size_t nchunks = bounds.size() - 1;
+  // SYM: chunk ci's owner scoring runs on the ctx stream and its emission pass, scan and
+  // count read-back on the emission stream, so emission (latency bound) overlaps the next
+  // chunk's scoring (VALU bound).  Emission of chunk ci reads owner / mirror results of
+  // chunks <= ci only: an owner pushes mirror results to candidates after it in bucket
+  // order, i.e. to later queries.
+  hipStream_t es = sym && emit_overlap() ? c->emit_stream : s;
   for (size_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
     const uint64_t s0 = bounds[ci], s1 = bounds[ci + 1];
     const uint64_t nblk = (s1 - s0 + kScoreBlock - 1) / kScoreBlock;
-    if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging b drained
     if (sym) {
       // phase 1: the chunk's owner slots, both directions of every owned pair -> ores
       const uint64_t o0 = obounds[ci], o1 = obounds[ci + 1];
       {
         Timer t_score(c, &c->prof.ms_score, s);
-        HIPCHK(launch_score(P, src, o0, o1 - o0, st[b], s));
+        HIPCHK(launch_score(P, src, o0, o1 - o0, so, s));
         t_score.stop();
       }
-      HIPCHK(launch_reduce_blocks(st[b], (o1 - o0 + kScoreBlock - 1) / kScoreBlock, s));
+      HIPCHK(launch_reduce_blocks(so, (o1 - o0 + kScoreBlock - 1) / kScoreBlock, s));
+      HIPCHK(hipEventRecord(c->score_done, s));
       // phase 2: the chunk's full slots in Duke's candidate order -> staged entries
-      Timer t_emit(c, &c->prof.ms_emit, s);
-      HIPCHK(launch_emit(esrc, s0, s1 - s0, st[b], s));
+      HIPCHK(hipStreamWaitEvent(es, c->score_done, 0));
+      if (ci >= 2) HIPCHK(hipStreamWaitEvent(es, c->compact_done[b], 0));  // staging b drained
+      Timer t_emit(c, &c->prof.ms_emit, es);
+      HIPCHK(launch_emit(esrc, s0, s1 - s0, st[b], es));
       t_emit.stop();
     } else {
+      if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging b drained
       {
         Timer t_score(c, &c->prof.ms_score, s);
         HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
@@ -2223,14 +2272,22 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     }
     c->prof.score_launches += 1;
     {
-      Timer t_gather(c, &c->prof.ms_gather, s);
-      HIPCHK(with_tmp(c, [&](void* t, size_t& bytes) {
-        return exclusive_scan_u32_u64(t, bytes, st[b].bcnt, c->stage[b].boff.as<uint64_t>(), nblk, s);
-      }));
+      Timer t_gather(c, &c->prof.ms_gather, es);
+      auto scan = [&](void* t, size_t& bytes) {
+        return exclusive_scan_u32_u64(t, bytes, st[b].bcnt, c->stage[b].boff.as<uint64_t>(), nblk, es);
+      };
+      if (sym) {
+        size_t bytes = 0;
+        HIPCHK(scan(nullptr, bytes));
+        HIPCHK(c->etmp.reserve(bytes + 16, 0, es));
+        HIPCHK(scan(c->etmp.p, bytes));
+      } else {
+        HIPCHK(with_tmp(c, scan));
+      }
       hs[5 + 2 * b] = 0;
-      HIPCHK(hipMemcpyAsync(&hs[4 + 2 * b], c->stage[b].boff.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(&hs[5 + 2 * b], st[b].bcnt + nblk - 1, 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipEventRecord(c->count_ready[b], s));
+      HIPCHK(hipMemcpyAsync(&hs[4 + 2 * b], c->stage[b].boff.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost, es));
+      HIPCHK(hipMemcpyAsync(&hs[5 + 2 * b], st[b].bcnt + nblk - 1, 4, hipMemcpyDeviceToHost, es));
+      HIPCHK(hipEventRecord(c->count_ready[b], es));
       t_gather.stop();
     }
     // the previous chunk's count is ready once its scan ran (before this chunk's score
@@ -2407,6 +2464,7 @@ static int set_result_region_impl(dk_ctx* c, void* base, uint64_t bytes, uint64_
     return fail(DK_E_UNSUPPORTED, "a multi-device ctx writes its list into its own host memory");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->copy_stream));
+  HIPCHK(hipStreamSynchronize(c->emit_stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (c->region.base) {
     (void)hipHostUnregister(c->region.base);

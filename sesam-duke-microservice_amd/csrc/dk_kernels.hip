@@ -187,6 +187,17 @@ __device__ __forceinline__ uint64_t peq_eq(const uint64_t* peq, uint32_t x) {
   return peq[x & 0xFF] & peq[256 + (x >> 8)];
 }
 
+// Peq lookups and window masks at the width of the query's position masks: 32 bits when
+// the query value has <= 32 units (wave-uniform), which halves the mask arithmetic and
+// reads only the low half of each 64-bit Peq entry.
+template <typename MT, typename CT>
+__device__ __forceinline__ MT peq_eq_t(const uint64_t* peq, uint32_t x) {
+  if (sizeof(MT) == 8) return (MT)peq_eq<CT>(peq, x);
+  const uint32_t* p32 = reinterpret_cast<const uint32_t*>(peq);  // little-endian low halves
+  if (sizeof(CT) == 1) return (MT)p32[2 * x];
+  return (MT)(p32[2 * (x & 0xFF)] & p32[2 * (256 + (x >> 8))]);
+}
+
 __device__ __forceinline__ uint64_t range_mask(int lo, int hi) {  // bits [lo, hi), 0<=lo<=hi<=64
   const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
   const uint64_t dn = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
@@ -409,7 +420,9 @@ __device__ __forceinline__ int compact_distance_pk(const uint64_t* peq, int n1, 
 // inside the word is a constant, and the next word is issued a whole word (UPW columns)
 // ahead.  Lanes whose DP ended keep stepping (their result is latched; a masked lane
 // costs the SIMD nothing) until no lane of the wave is live, checked after every column.
-// The outcome is the same function of (peq, n1, s2, n2) as compact_distance_pk's.
+// Outcome: Duke's distance when it is <= maxdist, else some value > maxdist (maxdist + 1 at
+// a cutoff, D(n1, n2) when the lane reaches its last column) -- compact_distance_pk's
+// contract; the raw similarity of a cut-off pair comes from k_lev_exact.
 // ------------------------------------------------------------------------------------
 template <int R, typename CT>
 __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, const Str<CT>& s2,
@@ -425,10 +438,17 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
   uint32_t PA[H + 1], PB[H + 1];
 #pragma unroll
   for (int i = 1; i <= H; ++i) PA[i] = ((uint32_t)i + B) | (BIG << 16);
+  // The cutoff AND covers the rows past n1 too (at most TAIL - 1 of them): they can only
+  // keep the AND false longer, i.e. delay a lane's exit to a later cutoff or to its last
+  // column, whose D(n1, n2) then exceeds maxdist as well (a column minimum above maxdist
+  // stays above it in every later column), so the probability (low) is the same; masking
+  // them cost one v_or per tail pair per column (-1.6 % dedup step without it).
+#ifdef DK_LEV_TAILMASK
   uint32_t tm[H + 1];
 #pragma unroll
   for (int i = 1; i <= H; ++i)
     tm[i] = (i > n1 ? 0x4000u : 0u) | (H + i > n1 ? 0x40000000u : 0u);
+#endif
   const bool bottom_result = n1 > H;
   int result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
   bool live = act && n2 > 1;
@@ -436,8 +456,21 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
 
   uint32_t w = act ? s2.word(0) : 0u;  // units of columns [t0, t0 + UPW)
   uint32_t wn = s2.word_pf(1);         // the next word
-  uint64_t ne_cur = ~peq_eq<CT>(peq, Str<CT>::unit(w, 0));
-  uint64_t ne_prev = ~0ull;
+  // cost masks at the width the column needs: rows [0, H + 16) of a Peq entry, so 32 bits
+  // up to 32 rows (a 32-bit LDS read leaves no dead half whose register reuse would force
+  // the read's wait in the column that issues it)
+#ifdef DK_LEV_NE64
+  constexpr bool kNarrow = false;  // A/B: 64-bit Peq reads at every row count
+#else
+  constexpr bool kNarrow = H <= 16;
+#endif
+  using NT = typename std::conditional<kNarrow, uint32_t, uint64_t>::type;
+  auto ne_of = [&](uint32_t x) -> NT {
+    if constexpr (sizeof(NT) == 4) return (NT)~peq_eq_t<uint32_t, CT>(peq, x);
+    else return (NT)~peq_eq<CT>(peq, x);
+  };
+  NT ne_cur = ne_of(Str<CT>::unit(w, 0));
+  NT ne_prev = (NT)~(NT)0;
   uint32_t h2 = BIG;  // top row H of column t-2
   uint32_t acc_prev = 0;
   // column t = t0 + U from Pin into Pout; false once no lane of the wave is live
@@ -445,7 +478,7 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
     constexpr int U = decltype(U_)::value;
     const int t = t0 + U;
     const uint32_t xn = U + 1 < UPW ? Str<CT>::unit(w, U + 1) : Str<CT>::unit(wn, 0);
-    const uint64_t ne_nx = ~peq_eq<CT>(peq, xn);
+    const NT ne_nx = ne_of(xn);
     uint32_t C[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
@@ -461,8 +494,12 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
       diag = Pin[i];
       Pout[i] = v;
       above = v;
+#ifdef DK_LEV_TAILMASK
       if (H + i > R - TAIL) acc &= v | tm[i];
       else acc &= v;
+#else
+      acc &= v;  // rows past n1 in the cutoff AND: see above
+#endif
     }
     h2 = h1;
     if (live) {
@@ -965,17 +1002,6 @@ template <typename MT>
 __device__ __forceinline__ MT carry_to_next(MT plane, MT found) {
   // bit i of the result = bit of `plane` at the matched row before matched row i
   return (((plane & found) << 1) + ~found) & found;
-}
-
-// Peq lookups and window masks at the width of the query's position masks: 32 bits when
-// the query value has <= 32 units (wave-uniform), which halves the mask arithmetic and
-// reads only the low half of each 64-bit Peq entry.
-template <typename MT, typename CT>
-__device__ __forceinline__ MT peq_eq_t(const uint64_t* peq, uint32_t x) {
-  if (sizeof(MT) == 8) return (MT)peq_eq<CT>(peq, x);
-  const uint32_t* p32 = reinterpret_cast<const uint32_t*>(peq);  // little-endian low halves
-  if (sizeof(CT) == 1) return (MT)p32[2 * x];
-  return (MT)(p32[2 * (x & 0xFF)] & p32[2 * (256 + (x >> 8))]);
 }
 
 template <typename MT>

@@ -538,11 +538,12 @@ def test_symmetric_schedule_equals_direct(seed, monkeypatch):
                        alive=alive_after(list(ident), n), threshold=0.75, maybe=0.55)
     for q in (np.arange(n, dtype=np.uint32), np.arange(700, 1900, dtype=np.uint32),
               np.arange(1500, n, dtype=np.uint32)):
-        for chunk in (None, "3000"):
+        for chunk, overlap in ((None, "0"), ("3000", "0"), ("3000", "1")):
             if chunk:
                 monkeypatch.setenv("DK_CHUNK_SLOTS", chunk)
             else:
                 monkeypatch.delenv("DK_CHUNK_SLOTS", raising=False)
+            monkeypatch.setenv("DK_EMIT_OVERLAP", overlap)   # emission on its own stream
             eng.reset_profile()
             eng.set_profiling(True)
             res = eng.match(q)
