@@ -1634,6 +1634,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
 
   double prob = P.raw_prop < 0 ? 0.5 : __builtin_nan("");
   double prob2 = 0.5;  // SYM: Processor.compare(candidate, query)
+  bool asym = false;   // SYM: a JaroWinkler property came before (prob2 may differ from prob)
   uint32_t bytes = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
   // property p+1's query length, this lane's query unit (its Peq bit) and the candidate's
   // length are loaded while property p computes: a property then starts without the
@@ -1686,6 +1687,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
           bytes += (uint32_t)lc * (uint32_t)D.width;
       }
     }
+    if (SYM && D.op == DK_CMP_JAROWINKLER) asym = true;  // wave-uniform
     if (p == P.raw_prop) {  // Comparator.compare(v1, v2) itself (wave-uniform branch)
       if (cmp) prob = sim;
       break;
@@ -1694,7 +1696,10 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       // [Duke 1.2] Processor.compare: high = max(0.0, PropertyImpl.compare) over the value
       // pairs (one each here), then computeBayes
       prob = compute_bayes(prob, cmp ? property_prob(D, sim) : 0.0);
-      if (SYM) prob2 = compute_bayes(prob2, cmp ? property_prob(D, rev) : 0.0);
+      // the reverse direction differs only from the first JaroWinkler property on (every
+      // other comparator of the symmetric schedule has rev == sim): until then prob2 == prob
+      // bit for bit, and its computeBayes would repeat prob's
+      if (SYM) prob2 = asym ? compute_bayes(prob2, cmp ? property_prob(D, rev) : 0.0) : prob;
     }
   }
 
