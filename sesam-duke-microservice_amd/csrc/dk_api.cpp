@@ -48,8 +48,15 @@ static int fail(int code, const char* fmt, ...) {
 // The exception barrier of every C-ABI entry and host task: nothing C++ crosses the boundary
 // (an escaping exception would std::terminate the JVM / Python host).  Out of host memory is
 // DK_E_NOMEM; RAII undo logs (dk_upsert's Rollback) have run by the time it is returned.
+// vzeroupper on entry (dk_ingest.cpp, host-compiled): a caller that left 256/512-bit upper
+// halves dirty (numpy under Python) makes every legacy-SSE instruction of the host staging
+// pay a merge dependency on Intel cores (measured 4x on the packer); AMD cores do not care.
+extern "C" void dk_clear_upper_state(void);
+static void clear_upper() { dk_clear_upper_state(); }
+
 template <typename F>
 static int guarded(F&& f) {
+  clear_upper();
   try {
     return f();
   } catch (const std::bad_alloc&) {

@@ -31,6 +31,8 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "dk_clean_table.h"
 #include "dk_interner.h"
 #include "dukehip.h"
@@ -56,6 +58,14 @@ struct Val {
   uint32_t nelem = 0;       // J_ARR: element count
   int32_t first = -1;       // J_ARR with one element: that element's index in the side store
 };
+
+// a zero byte in x (the classic SWAR test)
+inline uint64_t zero_byte(uint64_t x) { return (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull; }
+// does the 8-byte word hold a '"', a '\\' or a byte below 0x20?
+inline bool word_special(uint64_t w) {
+  return (zero_byte(w ^ 0x2222222222222222ull) | zero_byte(w ^ 0x5C5C5C5C5C5C5C5Cull) |
+          ((w - 0x2020202020202020ull) & ~w & 0x8080808080808080ull)) != 0;
+}
 
 struct Reader {
   const char* p;
@@ -83,6 +93,13 @@ struct Reader {
   void str(const char** a, const char** b) {
     ++p;  // '"'
     *a = p;
+    // 8 bytes at a time while none is '"', '\\' or a control character
+    while (e - p >= 8) {
+      uint64_t w;
+      memcpy(&w, p, 8);
+      if (word_special(w)) break;
+      p += 8;
+    }
     while (p < e && *p != '"') {
       if ((unsigned char)*p < 0x20) fail(DK_E_UNSUPPORTED, "JSON: control character in a string");
       if (*p == '\\') {
@@ -190,6 +207,17 @@ struct Reader {
 void decode_string(const char* a, const char* b, std::u16string& out) {
   const unsigned char* p = reinterpret_cast<const unsigned char*>(a);
   const unsigned char* e = reinterpret_cast<const unsigned char*>(b);
+  {  // the common case: an ASCII run without escapes, widened in one resize
+    const unsigned char* q = p;
+    while (q < e && *q != '\\' && *q < 0x80) ++q;
+    if (q > p) {
+      const size_t o = out.size(), n = (size_t)(q - p);
+      out.resize(o + n);
+      char16_t* d = &out[o];
+      for (size_t i = 0; i < n; ++i) d[i] = (char16_t)p[i];
+      p = q;
+    }
+  }
   auto hex4 = [&](const unsigned char* q) -> uint32_t {
     uint32_t v = 0;
     for (int i = 0; i < 4; ++i) {
@@ -384,8 +412,42 @@ void py_slice(int64_t n, int32_t start, int32_t end, int64_t* a, int64_t* b) {
   if (*b < *a) *b = *a;
 }
 
+// key_part over a value without surrogates: code points are its units
+void key_part_bmp(const std::u16string& v, const dk_key_part& kp, std::u16string& out) {
+  size_t lo = 0, hi = v.size();
+  if (kp.token != INT32_MIN) {  // str.split() then toks[token], without materialising toks
+    // count the tokens, then find token t (negative: from the end)
+    int64_t nt = 0;
+    for (size_t i = 0; i < v.size();) {
+      while (i < v.size() && py_isspace(v[i])) ++i;
+      if (i >= v.size()) break;
+      ++nt;
+      while (i < v.size() && !py_isspace(v[i])) ++i;
+    }
+    int64_t t = kp.token;
+    if (t < -nt || t >= nt) return;
+    if (t < 0) t += nt;
+    for (size_t i = 0, k = 0; i < v.size(); ++k) {
+      while (i < v.size() && py_isspace(v[i])) ++i;
+      const size_t a = i;
+      while (i < v.size() && !py_isspace(v[i])) ++i;
+      if ((int64_t)k == t) {
+        lo = a;
+        hi = i;
+        break;
+      }
+    }
+  }
+  int64_t a, b;
+  py_slice((int64_t)(hi - lo), kp.start, kp.end, &a, &b);
+  out.append(v, lo + (size_t)a, (size_t)(b - a));
+}
+
 void key_part(const std::u16string* value, const dk_key_part& kp, std::u16string& out, KeyScratch& ks) {
   if (!value) return;  // a missing value contributes ""
+  bool surrogate = false;
+  for (char16_t c : *value) surrogate |= (c >= 0xD800 && c <= 0xDFFF);
+  if (!surrogate) return key_part_bmp(*value, kp, out);
   std::vector<uint32_t>& cp = ks.cp;
   code_points(*value, cp);
   size_t lo = 0, hi = cp.size();
@@ -506,6 +568,107 @@ void for_brackets(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr,
   }
 }
 
+// ---- 64-byte blocks (AVX2 + carry-less multiply), the split's fast path ----------------
+// Per block: the masks of '"', '\\' and the four brackets (movemask of byte compares); the
+// escaped characters from the backslash mask (a character is escaped when an odd-length
+// run of backslashes precedes it: runs starting on odd bits carry through the run when
+// added to their start bit), carried from block to block; the in-string mask as the
+// prefix XOR of the unescaped quotes (one PCLMULQDQ by all-ones), carried as a sign mask.
+// The same state machine as quote_parity / for_brackets, 64 bytes per step.
+struct BlockMasks {
+  uint64_t quote, bs, open, close;
+};
+
+__attribute__((target("avx2"))) inline BlockMasks block_masks(const char* p) {
+  const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p));
+  const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p + 32));
+#define DK_EQ64(c)                                                                               \
+  ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(a, _mm256_set1_epi8(c))) |          \
+   ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(b, _mm256_set1_epi8(c))) << 32))
+  const BlockMasks m{DK_EQ64('"'), DK_EQ64('\\'), DK_EQ64('{') | DK_EQ64('['), DK_EQ64('}') | DK_EQ64(']')};
+#undef DK_EQ64
+  return m;
+}
+
+// characters escaped by a preceding backslash run; *carry: the next block's first
+// character is escaped
+inline uint64_t escaped_bits(uint64_t bs, uint64_t* carry) {
+  constexpr uint64_t kEven = 0x5555555555555555ull;
+  bs &= ~*carry;  // an escaped backslash starts no escape
+  const uint64_t follows = (bs << 1) | *carry;
+  const uint64_t odd_starts = bs & ~kEven & ~follows;
+  uint64_t seq_even;
+  *carry = __builtin_add_overflow(odd_starts, bs, &seq_even) ? 1u : 0u;
+  return (kEven ^ (seq_even << 1)) & follows;
+}
+
+__attribute__((target("avx2,pclmul"))) inline uint64_t prefix_xor(uint64_t x) {  // VEX-encoded: no SSE/AVX transition in the AVX2 loop
+  return (uint64_t)_mm_cvtsi128_si64(
+      _mm_clmulepi64_si128(_mm_set_epi64x(0, (long long)x), _mm_set1_epi8((char)0xFF), 0));
+}
+
+// vzeroupper when the CPU has AVX: a caller that used 256/512-bit registers (numpy under
+// Python, or this file's AVX2 split) leaves the upper halves dirty, and on Intel cores every
+// legacy-SSE instruction of the (compiler-vectorised) parse then pays a merge dependency --
+// measured 4x slower per entity in this container until cleared.  AMD cores do not care.
+__attribute__((target("avx"))) void zero_upper_avx() { _mm256_zeroupper(); }
+void clear_upper() {
+  static const bool avx = [] {
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx") != 0;
+  }();
+  if (avx) zero_upper_avx();
+}
+
+bool simd_split_ok() {
+  static const bool cpu = [] {
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("pclmul");
+  }();
+  const char* e = getenv("DK_INGEST_SCALAR");  // A/B and the differential tests
+  return cpu && !(e && e[0] == '1');
+}
+
+// f(block base, masks) over [c0, c1) in 64-byte blocks, the last one zero padded
+template <typename F>
+__attribute__((target("avx2"))) void for_blocks(const char* J, uint64_t c0, uint64_t c1, F&& f) {
+  uint64_t i = c0;
+  for (; i + 64 <= c1; i += 64) f(i, block_masks(J + i));
+  if (i < c1) {
+    alignas(32) char tail[64] = {};
+    memcpy(tail, J + i, c1 - i);
+    f(i, block_masks(tail));
+  }
+}
+
+// quote_parity of [c0, c1), 64 bytes per step
+__attribute__((target("avx2,pclmul"))) uint32_t quote_parity_simd(const char* J, uint64_t c0, uint64_t c1, bool esc) {
+  uint64_t carry = esc ? 1u : 0u;
+  uint32_t q = 0;
+  for_blocks(J, c0, c1, [&](uint64_t, const BlockMasks& m) {
+    const uint64_t e = escaped_bits(m.bs, &carry);
+    q ^= (uint32_t)__builtin_popcountll(m.quote & ~e) & 1u;
+  });
+  return q;
+}
+
+// the positions of the brackets outside strings in [c0, c1), in order
+__attribute__((target("avx2,pclmul"))) void brackets_simd(const char* J, uint64_t c0, uint64_t c1, bool esc,
+                                                         bool instr, std::vector<uint64_t>& out) {
+  uint64_t carry = esc ? 1u : 0u;
+  uint64_t inmask = instr ? ~0ull : 0ull;  // in a string at the block's start: all ones
+  for_blocks(J, c0, c1, [&](uint64_t base, const BlockMasks& m) {
+    const uint64_t e = escaped_bits(m.bs, &carry);
+    const uint64_t s = prefix_xor(m.quote & ~e) ^ inmask;
+    inmask = (uint64_t)((int64_t)s >> 63);
+    uint64_t br = (m.open | m.close) & ~s;
+    while (br) {
+      out.push_back(base + (uint64_t)__builtin_ctzll(br));
+      br &= br - 1;
+    }
+  });
+}
+
 // One chunk of the top-level array, its depth at the start known: entity starts ('{' at
 // depth 1) and ends (one past the '}' back to depth 1), the array's closing ']', or the
 // first bracket that cannot be there.
@@ -515,8 +678,10 @@ struct ChunkScan {
   uint64_t bad = UINT64_MAX;    // a non-object element's '[' or a stray closer
 };
 
-void scan_chunk(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr, int64_t depth, ChunkScan& C) {
-  for_brackets(J, c0, c1, esc, instr, [&](uint64_t pos, char ch) {
+// the chunk's depth walk over its brackets (each visited once, in order, by `each`)
+template <typename Each>
+void walk_chunk(Each&& each, int64_t depth, ChunkScan& C) {
+  each([&](uint64_t pos, char ch) {
     if (ch == '{' || ch == '[') {
       if (depth == 1) {
         if (ch != '{') { C.bad = pos; return false; }
@@ -538,6 +703,20 @@ void scan_chunk(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr, i
     }
     return true;
   });
+}
+
+void scan_chunk(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr, int64_t depth, ChunkScan& C) {
+  walk_chunk([&](auto&& f) { for_brackets(J, c0, c1, esc, instr, f); }, depth, C);
+}
+
+// the same over a chunk's bracket positions found by brackets_simd
+void scan_chunk_list(const char* J, const std::vector<uint64_t>& br, int64_t depth, ChunkScan& C) {
+  walk_chunk(
+      [&](auto&& f) {
+        for (uint64_t pos : br)
+          if (!f(pos, J[pos])) return;
+      },
+      depth, C);
 }
 
 // The text between two elements of the top-level array: whitespace only, one ',' in
@@ -594,6 +773,14 @@ bool element_check(Gap g, uint64_t r, Next nx, Split& S) {
 // each chunk knows whether it starts inside a string), bracket depth change, then the
 // entity starts / ends at the chunk's now known depth; the gaps between entities last.
 void split_entities(const char* J, uint64_t len, Split& S) {
+  static const bool timing = getenv("DK_INGEST_TIMING") != nullptr;  // sub-phase times
+  auto T0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* w) {
+    if (!timing) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "  split %s %.2f ms\n", w, std::chrono::duration<double, std::milli>(t1 - T0).count());
+    T0 = t1;
+  };
   uint64_t p = 0;
   while (p < len && is_ws(J[p])) ++p;
   if (p >= len) {
@@ -619,26 +806,40 @@ void split_entities(const char* J, uint64_t len, Split& S) {
   std::vector<char> esc0(T), instr(T);
   std::vector<int64_t> delta(T), d0(T);
   std::vector<ChunkScan> CS(T);
+  const bool simd = simd_split_ok();
+  std::vector<std::vector<uint64_t>> BR(simd ? T : 0);  // SIMD: each chunk's brackets
   parallel_for(T, [&](int t) {
     esc0[t] = chunk_escaped_at(J, lo, cut[t]);
-    par[t] = quote_parity(J, cut[t], cut[t + 1], esc0[t]);
+    par[t] = simd ? quote_parity_simd(J, cut[t], cut[t + 1], esc0[t])
+                  : quote_parity(J, cut[t], cut[t + 1], esc0[t]);
   });
+  lap("parity");
   for (int t = 0, q = 0; t < T; ++t) {
     instr[t] = (char)q;
     q ^= (int)par[t];
   }
   parallel_for(T, [&](int t) {
     int64_t d = 0;
-    for_brackets(J, cut[t], cut[t + 1], esc0[t], instr[t], [&](uint64_t, char ch) {
-      d += (ch == '{' || ch == '[') ? 1 : -1;
-      return true;
-    });
+    if (simd) {  // one pass: the positions (the depth walk reads their characters later)
+      BR[t].reserve((cut[t + 1] - cut[t]) / 32 + 16);
+      brackets_simd(J, cut[t], cut[t + 1], esc0[t], instr[t], BR[t]);
+      for (uint64_t pos : BR[t]) d += (J[pos] == '{' || J[pos] == '[') ? 1 : -1;
+    } else {
+      for_brackets(J, cut[t], cut[t + 1], esc0[t], instr[t], [&](uint64_t, char ch) {
+        d += (ch == '{' || ch == '[') ? 1 : -1;
+        return true;
+      });
+    }
     delta[t] = d;
   });
+  lap("brackets");
   for (int t = 0; t < T; ++t) d0[t] = t ? d0[t - 1] + delta[t - 1] : 1;
   parallel_for(T, [&](int t) {
-    if (d0[t] > 0) scan_chunk(J, cut[t], cut[t + 1], esc0[t], instr[t], d0[t], CS[t]);
+    if (d0[t] <= 0) return;
+    if (simd) scan_chunk_list(J, BR[t], d0[t], CS[t]);
+    else scan_chunk(J, cut[t], cut[t + 1], esc0[t], instr[t], d0[t], CS[t]);
   });
+  lap("walk");
   // the chunks up to the first that closes the array or holds a misplaced bracket
   uint64_t stop = len, close = UINT64_MAX, bad = UINT64_MAX;
   int tl = T - 1;
@@ -656,6 +857,7 @@ void split_entities(const char* J, uint64_t len, Split& S) {
     std::copy(CS[t].starts.begin(), CS[t].starts.end(), starts.begin() + so[t]);
     std::copy(CS[t].ends.begin(), CS[t].ends.end(), ends.begin() + eo[t]);
   });
+  lap("concat");
   const uint64_t ns = starts.size(), ne = ends.size();  // ne == ns or ns - 1
   // the first entity whose gap is malformed (gaps in parallel; the first one found wins)
   std::vector<uint64_t> first_bad(T, UINT64_MAX);
@@ -666,6 +868,7 @@ void split_entities(const char* J, uint64_t len, Split& S) {
       if (g != (k ? kComma : kEmpty)) { first_bad[t] = k; break; }
     }
   });
+  lap("gaps");
   uint64_t kbad = UINT64_MAX;
   for (int t = 0; t < T && kbad == UINT64_MAX; ++t) kbad = first_bad[t];
   const uint64_t nspans = kbad != UINT64_MAX ? kbad : ne;
@@ -735,6 +938,7 @@ struct SourceView {
 
 // IncrementalDataSource.DatasetDataSourceRecordIterator.next for entities [e0, e1)
 void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out) {
+  clear_upper();  // the calling thread's (a worker's is clean)
   const dk_source* src = V.src;
   const int np = src->nprops, nk = src->nkeys;
   out.cols.assign(np + nk + 2, ColPart());
@@ -988,6 +1192,8 @@ int dk_interner_intern(dk_interner* it, const dk_column* col, uint64_t n, uint64
   return DK_OK;
 }
 
+extern "C" void dk_clear_upper_state(void) { clear_upper(); }
+
 int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_interner* ids,
                  dk_packed** out) {
   if (!src || !json || !ids || !out) return dk_fail_ingest(DK_E_INVALID, "NULL argument");
@@ -1012,6 +1218,7 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
     V.names.emplace_back("_deleted");
     decode_string(src->dataset_id, src->dataset_id + strlen(src->dataset_id), V.ds);
 
+    clear_upper();
     auto T0 = std::chrono::steady_clock::now();
     static const bool timing = getenv("DK_INGEST_TIMING") != nullptr;  // phase times to stderr
     auto lap = [&](const char* w) {
@@ -1023,6 +1230,7 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
     // 1. entity spans
     Split S;
     split_entities(json, len, S);
+    clear_upper();
     const uint64_t n = S.spans.size();
     lap("split");
     // 2. entity slices, parsed in parallel

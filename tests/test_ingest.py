@@ -266,3 +266,41 @@ def test_parallel_interning_equals_sequential(monkeypatch):
         seen.setdefault(r, len(seen))
     assert [x for batch in got["8"] for x in batch] == [seen[f"ds__{e['_id']}"] for body in bodies
                                                         for e in json.loads(body)]
+
+
+def _pack_or_error(ns, body):
+    try:
+        pk = ns.pack(body, I.Interner())
+    except I.NativeUnsupported:
+        return ("unsupported",)
+    except A.DukeHipError as e:
+        return ("error", e.code)
+    return ("ok", pk.n, [pk.values(p) for p in range(len(PROPS))],
+            [pk.keys(k) for k in range(len(KEYS))], pk.ids())
+
+
+@pytest.mark.parametrize("threads", [1, 5])
+def test_split_simd_equals_scalar(threads, monkeypatch):
+    """The 64-byte-block split (escape runs carried across blocks, prefix-XOR string mask)
+    against the byte-at-a-time split: values with backslash / quote / bracket runs of every
+    length at every offset, valid and corrupted bodies."""
+    monkeypatch.setenv("DK_INGEST_THREADS", str(threads))
+    rng = random.Random(7 + threads)
+    ns = I.NativeSource(source(), PROPS, KEYS)
+    pieces = ["\\", "\\\\", '"', '\\"', "{", "}", "[", "]", "a", " ", ",", ":", "é"]
+    for trial in range(40):
+        ents = []
+        for i in range(rng.randint(0, 120)):
+            v = "".join(rng.choice(pieces) * rng.randint(1, 70 if rng.random() < 0.1 else 3)
+                        for _ in range(rng.randint(0, 12)))
+            ents.append({"_id": f"{i}{v[:5]}", "raw": v, "area": rng.choice(["1", [2], 3]),
+                         "nested": {"k": [v, {"x": v}]}})
+        body = json.dumps(ents, ensure_ascii=rng.random() < 0.5)
+        if trial % 4 == 3 and body:   # corrupt one byte: both splits must fail the same way
+            k = rng.randrange(len(body))
+            body = body[:k] + rng.choice(['"', "\\", "}", "]", "{", ","]) + body[k + 1:]
+        monkeypatch.setenv("DK_INGEST_SCALAR", "1")
+        want = _pack_or_error(ns, body)
+        monkeypatch.setenv("DK_INGEST_SCALAR", "0")
+        got = _pack_or_error(ns, body)
+        assert got == want, (trial, body[:200])
