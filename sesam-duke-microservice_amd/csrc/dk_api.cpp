@@ -1392,6 +1392,7 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
   for (const auto& S : c->P) {
     const int op = S.cfg.comparator;
     if (op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER || op == DK_CMP_WEIGHTED_LEVENSHTEIN) P.has_dp = 1;
+    if (op == DK_CMP_QGRAM || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS) P.has_grams = 1;
     if (S.cfg.comparator == DK_CMP_LEVENSHTEIN) {
       P.lev_rows = std::max(P.lev_rows, std::min(S.maxlen, kMaxUnits));
       if (S.maxlen > kMaxUnits) P.long_rows = std::max(P.long_rows, S.maxlen);

@@ -112,6 +112,8 @@ struct ScoreParams {
                           // the probability (dk_property_similarity); -1 = normal scoring
   int32_t has_dp;         // some property is Levenshtein / JaroWinkler / WeightedLevenshtein
                           // (0: the DP-free kernel variant, no DP code or registers)
+  int32_t has_grams;      // some property is QGram / Dice / Jaccard tokens (0: the short
+                          // kernels' variant without the gram-set code or its registers)
   double threshold;
   double maybe;
   const uint64_t* ident;

@@ -1345,7 +1345,7 @@ __device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool o
 // ------------------------------------------------------------------------------------
 // SYM: `rev` receives Comparator.compare(candidate, query) where it can differ from
 // compare(query, candidate) (JaroWinkler on equal lengths); it is left alone otherwise.
-template <int RMAX, int LR, typename CT, bool SYM, bool DP>
+template <int RMAX, int LR, typename CT, bool SYM, bool DP, bool GR>
 __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
                                              int lc, bool cmp, double& rev, uint32_t qch) {
@@ -1401,6 +1401,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
       if (cmp) sim = str_equal(s1, lq, s2, lc) ? 1.0 : 0.0;
       break;
     case DK_CMP_QGRAM: {
+      if (!GR) break;  // the host launches GR = false only for schemas without gram sets
       const int m1 = (int)__builtin_amdgcn_readfirstlane((uint32_t)D.gcnt[q]);
       const uint64_t* g1 = D.grams + D.goff[q];
       if (D.g16) {
@@ -1442,7 +1443,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
     }
     case DK_CMP_DICE_TOKENS:
     case DK_CMP_JACCARD_TOKENS:
-      if (cmp) {
+      if (GR && cmp) {
         if (str_equal(s1, lq, s2, lc)) {
           sim = 1.0;
         } else {
@@ -1536,7 +1537,7 @@ __device__ __forceinline__ double property_prob(const DevProp& D, double sim) {
 // SYM: the owner slots of the symmetric dedup schedule (PairSource::sym): every owned pair
 // is scored in both directions in one pass and the two probabilities go to S.ores; the
 // emission pass (k_emit) turns them into the match list.
-template <int RMAX, int LR, bool SYM, bool DP>
+template <int RMAX, int LR, bool SYM, bool DP, bool GR = true>
 __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
                                            uint64_t nslots, const StageOut& out) {
   uint64_t* peq = g_wave_tables[threadIdx.x >> 6];
@@ -1674,8 +1675,8 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       rev = sim;
     } else if (D.op != DK_CMP_NONE) {
       rev = __builtin_nan("");  // marks "same as sim" unless the comparator sets it
-      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM, DP>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch)
-                         : string_sim<RMAX, LR, uint16_t, SYM, DP>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch);
+      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM, DP, GR>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch)
+                         : string_sim<RMAX, LR, uint16_t, SYM, DP, GR>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch);
       if (!SYM || rev != rev) rev = sim;
       if (cmp) {
         if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2,
@@ -1720,10 +1721,12 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
 // The fused scoring kernel.  Short-value variants pin the occupancy (the DP is
 // latency-bound: 5 waves/SIMD up to 40 rows, 4 above); the long-value variants (LR > 0)
 // carry the systolic DP's f64 rows and take what the register allocator needs.
-template <int RMAX, bool SYM>
+// GR = false: no QGram / token property (the dedup headline's Levenshtein + JaroWinkler):
+// the gram-set code and its registers are compiled out.
+template <int RMAX, bool SYM, bool GR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? DK_WAVES_SHORT : 4, 8)))
 void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
-  score_body<RMAX, 0, SYM, true>(P, S, slot0, nslots, out);
+  score_body<RMAX, 0, SYM, true, GR>(P, S, slot0, nslots, out);
 }
 
 // Schemas without a DP comparator (QGram / Numeric / Exact / token comparators: configs[2]'s
@@ -2572,6 +2575,15 @@ hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t 
   return hipGetLastError();
 }
 
+// DK_GRAM_VARIANT=0: always the kernels with the gram-set code (A/B)
+static bool gram_variant_off() {
+  static const bool off = [] {
+    const char* e = getenv("DK_GRAM_VARIANT");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                         uint64_t nslots, const StageOut& out, hipStream_t s) {
   DK_LAUNCH_GUARD(nslots);
@@ -2581,8 +2593,13 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
   // Levenshtein value over 64 units): both bound the VGPRs of the fused kernel
 #define DK_SHORT(RM)                                                               \
   do {                                                                             \
-    if (src.sym) k_score<RM, true><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out); \
-    else k_score<RM, false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);        \
+    if (P.has_grams || gram_variant_off()) {                                                \
+      if (src.sym) k_score<RM, true, true><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out); \
+      else k_score<RM, false, true><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);        \
+    } else {                                                                                  \
+      if (src.sym) k_score<RM, true, false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out); \
+      else k_score<RM, false, false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);        \
+    }                                                                                         \
   } while (0)
 #define DK_LONG(RM, L) k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
   if (src.sym && P.long_rows > 0) return hipErrorInvalidValue;  // the host never schedules it
