@@ -53,6 +53,38 @@ __device__ __forceinline__ uint32_t mask_rank(uint64_t m) {  // set bits below t
 
 __device__ __forceinline__ int imin3(int a, int b, int c) { return min(min(a, b), c); }
 
+// Whole-wave max / sum, wave-uniform result (every lane active).  DPP steps instead of
+// __shfl_xor's LDS crossbar (ds_bpermute + lgkm waits per step, and loop-invariant lane
+// addresses that the fused kernels spilled): quad permutes, row half-mirror and mirror
+// (16-lane rows), then row_bcast:15 / row_bcast:31 carry rows into lane 63.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_max_step(int v) {
+  return max(v, __builtin_amdgcn_update_dpp(v, v, CTRL, ROWS, 0xF, false));
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+  v = dpp_max_step<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = dpp_max_step<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = dpp_max_step<0x141, 0xF>(v);  // row_half_mirror
+  v = dpp_max_step<0x140, 0xF>(v);  // row_mirror
+  v = dpp_max_step<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+  v = dpp_max_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+  return __builtin_amdgcn_readlane(v, 63);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_add_step(uint32_t v) {
+  // lanes outside ROWS add 0 (old = 0)
+  return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v = dpp_add_step<0xB1, 0xF>(v);
+  v = dpp_add_step<0x4E, 0xF>(v);
+  v = dpp_add_step<0x141, 0xF>(v);
+  v = dpp_add_step<0x140, 0xF>(v);
+  v = dpp_add_step<0x142, 0xA>(v);
+  v = dpp_add_step<0x143, 0xC>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // java.lang.Math.max(double, double)
 __device__ __forceinline__ double java_max(double a, double b) {
   if (a != a) return a;
@@ -737,7 +769,7 @@ __device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1
   const int cnt = nneed / NG + (spos(nneed / NG) < nneed ? 1 : 0);
   int tlen = 0;
   for (int m = 0; m < cnt; ++m) tlen += (int)(meta[spos(m)] & 0xFFFFu);
-  for (int o = 32; o > 0; o >>= 1) tlen = max(tlen, __shfl_xor(tlen, o));
+  tlen = wave_max_i32(tlen);
   const int tend = tlen + kstar + 1;  // lane kstar closes its last matrix at step tlen + kstar
 
   // this lane's query rows, packed like the ring units (equal packed values <=> equal
@@ -1037,7 +1069,7 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
   MT found = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
   const int maxn = act ? nc : 0;
   int wmax = maxn;
-  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
+  wmax = wave_max_i32(wmax);
   constexpr int UPW = Str<CT>::UPW;
   // Units past a candidate's end read as 0 (zero padded): Peq[0] is empty unless the
   // query itself holds U+0000 (wave-uniform), and only then do lanes mask past-end units.
@@ -1278,8 +1310,7 @@ __device__ __forceinline__ int qgram_common_perfect(uint32_t* tab, const uint64_
   }
   wave_lds_sync();
   int njw = (m2 + 3) >> 2;  // word rows: this lane's, then the wave's most (the trip count)
-  for (int o = 32; o > 0; o >>= 1) njw = max(njw, __shfl_xor(njw, o));
-  njw = (int)__builtin_amdgcn_readfirstlane((uint32_t)njw);
+  njw = wave_max_i32(njw);
   // the word row's base is wave-uniform, the lane adds a 32-bit byte offset
   const char* base = reinterpret_cast<const char*>(rg);
   const uint32_t boff = g * 8u;
@@ -1476,11 +1507,7 @@ __device__ __forceinline__ void block_emit_at(const StageOut& out, uint64_t blk,
   __shared__ uint32_t wcount[kScoreBlock / 64], wscored[kScoreBlock / 64], wbytes[kScoreBlock / 64];
   const uint32_t wave = threadIdx.x >> 6;
   const uint64_t em = __ballot(kind != 0);
-  uint32_t sb = bytes, ss = scored;
-  for (int o = 32; o > 0; o >>= 1) {
-    sb += __shfl_xor(sb, o);
-    ss += __shfl_xor(ss, o);
-  }
+  const uint32_t sb = wave_sum_u32(bytes), ss = wave_sum_u32(scored);
   if (lane_id() == 0) {
     wcount[wave] = (uint32_t)__popcll(em);
     wscored[wave] = ss;
