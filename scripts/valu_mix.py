@@ -22,9 +22,9 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
 KERNELS = {  # bench.py workload -> the k_score variant its launches use
-    "dedup": "_ZN2dk7k_scoreILi40ELb1E",
+    "dedup": "_ZN2dk7k_scoreILi40ELb1ELb0E",  # GR = false: no gram-set code
     "linkage": "_ZN2dk12k_score_nodpILb0E",
-    "allpairs": "_ZN2dk7k_scoreILi16ELb0E",
+    "allpairs": "_ZN2dk7k_scoreILi16ELb0ELb0E",
     "longtext": "_ZN2dk12k_score_longILi16ELi16E",
 }
 # cycles per wave64 instruction per SIMD (profiles/r01/valu_rate_gfx950.txt), by class
