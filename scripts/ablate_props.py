@@ -37,5 +37,5 @@ for names in SETS:
     el = (time.perf_counter() - t) / 3
     pr = eng.profile()
     print(f"{'+'.join(names) or 'none':20s} step {el*1e3:8.1f} ms  score {pr['ms_score']/3:8.1f} ms  "
-          f"gen {pr['ms_generate']/3:6.1f}  gather {pr['ms_gather']/3:6.1f}  pairs {r.pairs_scored}", flush=True)
+          f"gen {pr['ms_generate']/3:6.1f}  emit {pr['ms_emit']/3:6.2f}  gather {pr['ms_gather']/3:6.1f}  pairs {r.pairs_scored}", flush=True)
     eng.close()

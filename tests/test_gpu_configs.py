@@ -536,8 +536,10 @@ def test_symmetric_schedule_equals_direct(seed, monkeypatch):
     upsert_slice(eng, vals, keys, ident, 1500, n, deleted)
     ot = O.OracleTable(props, vals, keys=keys, ident=ident, deleted=deleted,
                        alive=alive_after(list(ident), n), threshold=0.75, maybe=0.55)
+    # the mirror results' NaN fill is restored by each call's emission passes and carried to
+    # the next call: shrinking then growing query sets on one engine
     for q in (np.arange(n, dtype=np.uint32), np.arange(700, 1900, dtype=np.uint32),
-              np.arange(1500, n, dtype=np.uint32)):
+              np.arange(1500, n, dtype=np.uint32), np.arange(n, dtype=np.uint32)):
         for chunk, overlap in ((None, "0"), ("3000", "0"), ("3000", "1")):
             if chunk:
                 monkeypatch.setenv("DK_CHUNK_SLOTS", chunk)
