@@ -147,8 +147,26 @@ template <typename CT>
 __device__ __forceinline__ bool str_equal(const Str<CT>& a, int na, const Str<CT>& b, int nb) {
   if (na != nb) return false;
   const int nw = (na + Str<CT>::UPW - 1) / Str<CT>::UPW;
+#ifdef DK_STREQ_SERIAL
   for (int k = 0; k < nw; ++k)
     if (a.word(k) != b.word(k)) return false;
+#else
+  // the first word alone (most unequal values differ in it: all-pairs Levenshtein pays
+  // for extra loads there), then four words per round with their loads issued together: a
+  // 10-unit date is two round trips instead of three dependent ones (word_any stays inside
+  // both layouts' padding; words past the value are masked)
+  if (nw == 0) return true;
+  if (a.word(0) != b.word(0)) return false;
+  for (int k = 1; k < nw; k += 4) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t x = a.word_any(k + i) ^ b.word_any(k + i);
+      d |= k + i < nw ? x : 0u;
+    }
+    if (d) return false;
+  }
+#endif
   return true;
 }
 
