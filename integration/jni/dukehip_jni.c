@@ -19,19 +19,31 @@
 #define JFN(name) JNICALL Java_io_sesam_dukemicroservice_gpu_DukeHip_##name
 #define CTX(h) ((dk_ctx*)(intptr_t)(h))
 
-static int throw_dk(JNIEnv* env, int rc) {
-  if (rc >= 0) return 0;
-  jclass ex = (*env)->FindClass(env, "io/sesam/dukemicroservice/gpu/DukeHipException");
-  jmethodID init = ex ? (*env)->GetMethodID(env, ex, "<init>", "(ILjava/lang/String;)V") : NULL;
-  jstring msg = (*env)->NewStringUTF(env, dk_last_error());
-  jobject e = init && msg ? (*env)->NewObject(env, ex, init, (jint)rc, msg) : NULL;
-  if (e) (*env)->Throw(env, (jthrowable)e);
-  else (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/RuntimeException"), dk_last_error());
-  return 1;
-}
-
 static void throw_msg(JNIEnv* env, const char* msg) {
   (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/RuntimeException"), msg);
+}
+
+/* DukeHipException(code, dk_last_error()); if that class, its constructor or the object
+ * cannot be made, the pending NoClassDefFoundError / OutOfMemoryError is cleared (no JNI call
+ * but a few may run with an exception pending) and a RuntimeException carries the message. */
+static int throw_dk(JNIEnv* env, int rc) {
+  if (rc >= 0) return 0;
+  const char* text = dk_last_error();
+  jclass ex = (*env)->FindClass(env, "io/sesam/dukemicroservice/gpu/DukeHipException");
+  jmethodID init = NULL;
+  jstring msg = NULL;
+  jobject e = NULL;
+  if (ex && !(*env)->ExceptionCheck(env))
+    init = (*env)->GetMethodID(env, ex, "<init>", "(ILjava/lang/String;)V");
+  if (init && !(*env)->ExceptionCheck(env)) msg = (*env)->NewStringUTF(env, text);
+  if (msg && !(*env)->ExceptionCheck(env)) e = (*env)->NewObject(env, ex, init, (jint)rc, msg);
+  if (e && !(*env)->ExceptionCheck(env)) {
+    (*env)->Throw(env, (jthrowable)e);
+  } else {
+    (*env)->ExceptionClear(env);
+    throw_msg(env, text);
+  }
+  return 1;
 }
 
 /* ---- pipeline ctx --------------------------------------------------------------------- */
@@ -557,13 +569,33 @@ JNIEXPORT jlongArray JFN(linkdbApply)(JNIEnv* env, jclass cls, jlong db, jlongAr
                                       jlongArray first, jlongArray candidateIdent, jdoubleArray prob,
                                       jbyteArray kind, jlong timestamp) {
   (void)cls;
+  /* the C-ABI trusts these sizes: first[] holds nqueries + 1 non-decreasing offsets into the
+   * candidate arrays, which all have one length */
+  const jsize nq = (*env)->GetArrayLength(env, queryIdent);
+  const jsize nc = (*env)->GetArrayLength(env, candidateIdent);
+  if ((*env)->GetArrayLength(env, first) != nq + 1 || (*env)->GetArrayLength(env, prob) != nc ||
+      (*env)->GetArrayLength(env, kind) != nc) {
+    throw_msg(env, "linkdbApply: first must hold queryIdent.length + 1 entries and prob / kind "
+                   "candidateIdent.length");
+    return NULL;
+  }
+  {
+    jlong f0 = 0, fl = 0;
+    (*env)->GetLongArrayRegion(env, first, 0, 1, &f0);
+    (*env)->GetLongArrayRegion(env, first, nq, 1, &fl);
+    if (f0 != 0 || fl < 0 || fl > (jlong)nc) {
+      throw_msg(env, "linkdbApply: first[0] must be 0 and first[queryIdent.length] at most "
+                     "candidateIdent.length");
+      return NULL;
+    }
+  }
   jlong* qi = (*env)->GetLongArrayElements(env, queryIdent, NULL);
   jlong* fi = (*env)->GetLongArrayElements(env, first, NULL);
   jlong* ci = (*env)->GetLongArrayElements(env, candidateIdent, NULL);
   jdouble* pr = (*env)->GetDoubleArrayElements(env, prob, NULL);
   jbyte* kd = (*env)->GetByteArrayElements(env, kind, NULL);
   dk_link_batch b;
-  b.nqueries = (uint64_t)(*env)->GetArrayLength(env, queryIdent);
+  b.nqueries = (uint64_t)nq;
   b.query_ident = (const uint64_t*)qi;
   b.first = (const uint64_t*)fi;
   b.candidate_ident = (const uint64_t*)ci;

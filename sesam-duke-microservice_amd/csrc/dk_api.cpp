@@ -238,6 +238,37 @@ static bool java_parse_double(const uint16_t* u, size_t n, double* out) {
   while (a < b && u[a] <= 0x20) ++a;
   while (b > a && u[b - 1] <= 0x20) --b;
   if (a == b) return false;
+  {
+    // fast path: [sign] digits [. digits], at most 15 digits in all -- the significand is
+    // exact in a double and so is 10^k (k <= 15), so one IEEE division (or none) is the
+    // correctly rounded value strtod returns (Clinger's fast path); -0 stays -0.0
+    size_t i = a;
+    const bool neg = u[i] == '-';
+    if (u[i] == '+' || u[i] == '-') ++i;
+    int64_t m = 0;
+    int nd = 0, frac = 0;
+    bool dot = false, ok = i < b;
+    for (; i < b && ok; ++i) {
+      const uint16_t ch = u[i];
+      if (ch >= '0' && ch <= '9') {
+        m = m * 10 + (ch - '0');
+        ++nd;
+        if (dot) ++frac;
+      } else if (ch == '.' && !dot) {
+        dot = true;
+      } else {
+        ok = false;
+      }
+    }
+    if (ok && nd > 0 && nd <= 15) {
+      static const double kPow10[16] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7,
+                                        1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15};
+      double v = (double)m;
+      if (frac) v = v / kPow10[frac];
+      *out = neg ? -v : v;
+      return true;
+    }
+  }
   std::string s;
   s.reserve(b - a);
   for (size_t i = a; i < b; ++i) {
@@ -452,6 +483,8 @@ struct dk_ctx {
   const uint32_t* rowof_p = nullptr;  // replica position -> row (rowof, or usable in ALLPAIRS)
   uint64_t rstride = 0;               // replica positions
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
+  // k_score_grouped's execution order: task sort keys / values (double-buffered), chunk starts
+  DevBuf task_key, task_val, task_cb;
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
   DevBuf ocounts, oqoff, owq, obase, ores, mcounts, mqoff, mbase, mres, bidx, bval;
@@ -831,32 +864,68 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
     }
   });
   if (!is_num && !is_qg) return DK_OK;
-  // numeric values / q-gram and token codes (per value, in row order)
-  std::vector<uint16_t> v16;
-  std::vector<uint64_t> g;
+  // numeric values / q-gram and token codes (per value, in row order).  Numeric parses and
+  // q-gram sets run over row ranges on their own threads (serial staging was
+  // most of a 1M-row linkage upsert); each range fills a gram buffer of its own, merged in
+  // range order, so the code lists are in row order as before.  Token ids come from one
+  // interner per property and stay serial.
   if (is_num) { S.num.assign(n, 0.0); S.numok.assign(n, 0); }
   if (is_qg) { S.goff.assign(n, 0); S.gcnt.assign(n, 0); }
-  for (uint64_t i = 0; i < n; ++i) {
-    if (S.len[i] == kMissing) continue;
-    const uint64_t a = col->offsets[i], L = S.len[i];
-    v16.resize(L);
-    for (uint64_t k = 0; k < L; ++k) v16[k] = col->width == 1 ? u8[a + k] : u16[a + k];
-    if (is_num) {
-      double v = 0.0;
-      S.numok[i] = java_parse_double(v16.data(), L, &v) ? 1 : 0;
-      S.num[i] = v;
+  const int parts = is_tok || n < (1u << 15) ? 1 : 8;
+  std::vector<std::vector<uint64_t>> pg(parts);
+  std::vector<int> pmax(parts, 0);
+  std::vector<uint64_t> pbad(parts, ~0ull);  // first row of a range with too many codes
+  dk_run_parts(parts, [&](int t) {
+    const uint64_t lo = n * t / parts, hi = n * (t + 1) / parts;
+    std::vector<uint16_t> v16;
+    std::vector<uint64_t> g;
+    std::vector<uint64_t>& out = pg[t];
+    for (uint64_t i = lo; i < hi; ++i) {
+      if (S.len[i] == kMissing) continue;
+      const uint64_t a = col->offsets[i], L = S.len[i];
+      v16.resize(L);
+      if (col->width == 1) for (uint64_t k = 0; k < L; ++k) v16[k] = u8[a + k];
+      else memcpy(v16.data(), u16 + a, L * 2);
+      if (is_num) {
+        double v = 0.0;
+        S.numok[i] = java_parse_double(v16.data(), L, &v) ? 1 : 0;
+        S.num[i] = v;
+      }
+      if (is_qg) {
+        // token ids are interned per property; an id handed out by a batch that is then
+        // rejected is merely unused (ids only need to be equal <=> tokens equal)
+        if (is_tok) token_codes(v16.data(), (int)L, P.tokens, g);
+        else qgram_codes(v16.data(), (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, g);
+        if (g.size() >= kMissing) {
+          pbad[t] = i;
+          return;
+        }
+        S.goff[i] = (uint32_t)out.size();  // relative to the range's buffer until the merge
+        S.gcnt[i] = (uint16_t)g.size();
+        pmax[t] = std::max<int>(pmax[t], (int)g.size());
+        out.insert(out.end(), g.begin(), g.end());
+      }
     }
-    if (is_qg) {
-      // token ids are interned per property; an id handed out by a batch that is then
-      // rejected is merely unused (ids only need to be equal <=> tokens equal)
-      if (is_tok) token_codes(v16.data(), (int)L, P.tokens, g);
-      else qgram_codes(v16.data(), (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, g);
-      if (g.size() >= kMissing)
-        return fail(DK_E_UNSUPPORTED, "property %d: %zu q-grams / tokens", pidx, g.size());
-      S.goff[i] = (uint32_t)S.grams.size();
-      S.gcnt[i] = (uint16_t)g.size();
-      S.maxgrams = std::max<int>(S.maxgrams, (int)g.size());
-      S.grams.insert(S.grams.end(), g.begin(), g.end());
+  });
+  for (int t = 0; t < parts; ++t)
+    if (pbad[t] != ~0ull)
+      return fail(DK_E_UNSUPPORTED, "property %d: row %llu has too many q-grams / tokens", pidx,
+                  (unsigned long long)pbad[t]);
+  if (is_qg) {
+    std::vector<uint64_t> base(parts + 1, 0);
+    for (int t = 0; t < parts; ++t) {
+      base[t + 1] = base[t] + pg[t].size();
+      S.maxgrams = std::max(S.maxgrams, pmax[t]);
+    }
+    if (parts == 1) {
+      S.grams.swap(pg[0]);
+    } else {
+      S.grams.resize(base[parts]);
+      dk_run_parts(parts, [&](int t) {
+        const uint64_t lo = n * t / parts, hi = n * (t + 1) / parts;
+        if (!pg[t].empty()) memcpy(S.grams.data() + base[t], pg[t].data(), pg[t].size() * 8);
+        for (uint64_t i = lo; i < hi; ++i) S.goff[i] += (uint32_t)base[t];
+      });
     }
   }
   if (P.grams_used + S.grams.size() >= (1ull << 32))
@@ -1193,9 +1262,10 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     int rc = commit_column(c, p, cols[p], n, row0);
     if (rc) return rc;
     // a Latin-1 bigram property: the new rows' perfect-hash seeds (once the arena is wide,
-    // bigram keys are never used again, and neither are seeds)
+    // or a set outgrows the replica, bigram keys are never used again, and neither are
+    // seeds: both only grow until a rollback, which drops these rows too)
     PropState& P = c->P[p];
-    if (bigram_prop(P.cfg) && P.width == 1)
+    if (bigram_prop(P.cfg) && P.width == 1 && P.maxgrams <= kMaxReplicaGrams)
       HIPCHK(launch_gram_seed(P.grams.as<uint64_t>(), P.goff.as<uint32_t>(), P.gcnt.as<uint16_t>(),
                               P.len.as<uint16_t>(), row0, n, P.gseed.as<uint16_t>(), s));
   }
@@ -1866,6 +1936,25 @@ static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
   return true;
 }
 
+// k_score_grouped (dk_score_grouped.hip) serves the direct schedule of schemas made of
+// Numeric properties and at most kGroupedTabs Latin-1 bigram QGram properties with a key
+// replica (configs[2]); DK_GROUPED=0 keeps them on k_score_nodp (A/B).
+static bool grouped_schema_ok(const ScoreParams& P) {
+  const char* e = getenv("DK_GROUPED");
+  if ((e && e[0] == '0') || P.has_dp || P.raw_prop >= 0 || P.nprops < 1) return false;
+  int tabs = 0;
+  for (int p = 0; p < P.nprops; ++p) {
+    const DevProp& D = P.props[p];
+    if (D.op == DK_CMP_QGRAM) {
+      if (!D.g16 || D.rgrows < 1 || D.width != 1) return false;
+      ++tabs;
+    } else if (D.op != DK_CMP_NUMERIC && D.op != DK_CMP_NONE) {
+      return false;
+    }
+  }
+  return tabs <= kGroupedTabs;
+}
+
 // Lucene source, per dk_match: every query's hits (k_lucene_topk) become its candidate
 // range -- positions qi * max_hits + j of a per-call candidate replica, in hit order -- and
 // the slot layout (counts, offsets, wave map) of the direct schedule.  d_queries holds the
@@ -1968,6 +2057,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   }
   const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
   bool sym = !lucene && contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
+  bool grouped = false;  // k_score_grouped: query slots padded to kScoreBlock
   const uint32_t r0 = nq ? query_rows[0] : 0;
   uint64_t* hs = c->h_small.as<uint64_t>();
   if (sym) {
@@ -2025,12 +2115,13 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), c->mqoff.as<uint64_t>(),
                         nq, T.nseg, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
   } else if (!allpairs && !lucene) {
+    grouped = grouped_schema_ok(P);
     HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
     HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
     HIPCHK(c->qoff.reserve((nq + 1) * 8, 0, s));
     HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
     HIPCHK(launch_count(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(), c->counts.as<uint64_t>(),
-                        c->counters.as<uint64_t>() + 2, s));
+                        c->counters.as<uint64_t>() + 2, grouped ? kScoreBlock : 64, s));
     HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
@@ -2183,6 +2274,30 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     esrc.threshold = P.threshold;
     esrc.maybe = P.maybe;
   }
+  // k_score_grouped: the tasks of each chunk in the order of their first candidate's replica
+  // position (bucket by bucket), DK_TASK_SORT=0: slot order (A/B)
+  const uint32_t* perm = nullptr;
+  if (grouped && !(getenv("DK_TASK_SORT") && getenv("DK_TASK_SORT")[0] == '0')) {
+    const uint64_t ntask = total / kScoreBlock;
+    const int nch = (int)bounds.size() - 1;
+    HIPCHK(c->task_key.reserve(ntask * 16 + 16, 0, s));
+    HIPCHK(c->task_val.reserve(ntask * 8 + 8, 0, s));
+    HIPCHK(c->task_cb.reserve((uint64_t)(nch + 1) * 8, 0, s));
+    HIPCHK(c->h_bounds.reserve((uint64_t)(nch + 1) * 8));
+    uint64_t* hb = c->h_bounds.as<uint64_t>();
+    for (int i = 0; i <= nch; ++i) hb[i] = bounds[i] / kScoreBlock;
+    HIPCHK(hipMemcpyAsync(c->task_cb.p, hb, (uint64_t)(nch + 1) * 8, hipMemcpyHostToDevice, s));
+    uint64_t* k0 = c->task_key.as<uint64_t>();
+    uint32_t* v0 = c->task_val.as<uint32_t>();
+    HIPCHK(launch_task_keys(src, ntask, c->task_cb.as<uint64_t>(), nch, k0, v0, s));
+    int bits = 32;
+    while ((1ll << (bits - 32)) <= nch) ++bits;
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return sort_pairs_u64_u32_bits(t, b, k0, k0 + ntask, v0, v0 + ntask, ntask, bits, s);
+    }));
+    perm = v0 + ntask;
+    HIPCHK(hipStreamSynchronize(s));  // h_bounds is reused below
+  }
   hipStream_t cs = c->copy_stream;
   // Chunk ci scores on the main stream; its block-ordered compaction onto the match list and
   // (host modes) the copy of its entries run on the copy stream, beside the next chunk's
@@ -2273,7 +2388,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging b drained
       {
         Timer t_score(c, &c->prof.ms_score, s);
-        HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
+        if (grouped) HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, st[b], s));
+        else HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
         t_score.stop();
       }
       HIPCHK(launch_reduce_blocks(st[b], nblk, s));

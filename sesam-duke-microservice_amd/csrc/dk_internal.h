@@ -23,11 +23,13 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // filtered candidate slot
 // (u0 << 16) | u1 (16 bits per UTF-16 unit); with both units < 256 the 16-bit bigram
 // (u0 << 8) | u1 is injective, and key = bigram + 1 (mod 2^16) is never 0 except for the
 // bigram U+00FF U+00FF, whose rows get no seed -- so a zero key is padding.  A row's seed
-// s = (lt - 8) << 8 | i names the table size 2^lt (lt 8..10) and multiplier gram_mult(i)
+// s = (lt - 8) << 8 | i names the table size 2^lt (lt 8..9) and multiplier gram_mult(i)
 // under which slot(key) = low32(key * mult) >> (32 - lt) is injective on the row's keys.
 constexpr uint16_t kGramSeedNone = 0xFFFF;
 constexpr int kGramSeedTries = 256;
-constexpr int kGramPerfectMax = 128;  // grams of a set that get a seed (table <= 1024 u32)
+// grams of a set that get a seed (table <= 512 u32): a property whose longest set has more
+// grams has no candidate replica (kMaxReplicaGrams), so no seed of it would ever be read
+constexpr int kGramPerfectMax = kMaxReplicaGrams;
 __host__ __device__ inline uint32_t gram_key(uint64_t code) {
   return ((((uint32_t)(code >> 8) & 0xFF00u) | ((uint32_t)code & 0xFFu)) + 1u) & 0xFFFFu;
 }
@@ -168,6 +170,11 @@ struct PairSource {
 };
 
 constexpr uint32_t kNoPos = 0xFFFFFFFFu;
+
+// k_score_grouped (dk_score_grouped.hip): schemas of Numeric properties and at most
+// kGroupedTabs Latin-1 bigram QGram properties (DevProp::g16), direct schedule; each
+// query's slots are padded to kScoreBlock (one task = one wave = one staging block)
+constexpr int kGroupedTabs = 2;
 
 // The emission pass of the symmetric schedule: slots of the full candidate order (qoff /
 // wq / ranges as in PairSource) read their probability from the owner results.
@@ -325,10 +332,10 @@ hipError_t launch_replicate(const ReplicaJob& J, const uint32_t* rowof, uint64_t
 // superseded base rows: their positions in every base segment get rident = kDeadIdent
 hipError_t launch_mark_dead(const BlockTables& T, const uint32_t* rows, uint64_t n, uint64_t* rident,
                             hipStream_t s);
-// counts[i] = candidate slots of query i rounded up to 64 (one query per score wave);
-// real[0] += the unpadded total
+// counts[i] = candidate slots of query i rounded up to `pad` (64: one query per score wave;
+// kScoreBlock: one query per k_score_grouped task); real[0] += the unpadded total
 hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint2* ranges,
-                        uint64_t* counts, uint64_t* real, hipStream_t s);
+                        uint64_t* counts, uint64_t* real, int pad, hipStream_t s);
 // counts[i] = candidate slots of query i, unpadded (dk_candidate_counts)
 hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockTables& T,
                               uint2* ranges, uint64_t* counts, hipStream_t s);
@@ -340,6 +347,15 @@ hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t pos0, uint64_t 
                                  uint64_t* const* rkeys, hipStream_t s);
 hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                         uint64_t nslots, const StageOut& out, hipStream_t s);
+// k_score_grouped: slot0 and nslots multiples of kScoreBlock, slots padded per query to it;
+// perm (or NULL: task order) = the tasks in execution order (k_task_keys, sorted)
+hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
+                                uint64_t nslots, const uint32_t* perm, const StageOut& out,
+                                hipStream_t s);
+// key[t] = chunk << 32 | first candidate's replica position of task t, val[t] = t;
+// cb[0..nchunks] = first task of each chunk
+hipError_t launch_task_keys(const PairSource& src, uint64_t ntask, const uint64_t* cb, int nchunks,
+                            uint64_t* key, uint32_t* val, hipStream_t s);
 // symmetric dedup schedule: per query its bucket positions (sranges), full and owner slot
 // counts (each padded to 64), real[0] += the unpadded full total
 hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
@@ -362,6 +378,10 @@ hipError_t launch_iota_u32(uint32_t* p, uint64_t n, hipStream_t s);
 // rocPRIM wrappers (dk_kernels.hip)
 hipError_t sort_pairs_u64_u32(void* tmp, size_t& tmp_bytes, const uint64_t* kin, uint64_t* kout,
                               const uint32_t* vin, uint32_t* vout, uint64_t n, hipStream_t s);
+// the same over key bits [0, end_bit)
+hipError_t sort_pairs_u64_u32_bits(void* tmp, size_t& tmp_bytes, const uint64_t* kin, uint64_t* kout,
+                                   const uint32_t* vin, uint32_t* vout, uint64_t n, int end_bit,
+                                   hipStream_t s);
 hipError_t exclusive_scan_u64(void* tmp, size_t& tmp_bytes, const uint64_t* in, uint64_t* out,
                               uint64_t n, hipStream_t s);
 hipError_t exclusive_scan_u32(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint32_t* out,

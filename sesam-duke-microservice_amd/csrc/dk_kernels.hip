@@ -17,6 +17,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "dk_internal.h"
+#include "dk_device.h"
 
 #ifndef DK_JW_NARROW
 #define DK_JW_NARROW 32  // JaroWinkler on 32-bit position masks up to this query length
@@ -39,153 +40,6 @@ namespace dk {
 struct RowKeys {
   uint64_t* p[kMaxKeys];
 };
-
-// ------------------------------------------------------------------------------------
-// small helpers
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_id() {
-  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
-
-__device__ __forceinline__ uint32_t mask_rank(uint64_t m) {  // set bits below this lane
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-__device__ __forceinline__ int imin3(int a, int b, int c) { return min(min(a, b), c); }
-
-// Whole-wave max / sum, wave-uniform result (every lane active).  DPP steps instead of
-// __shfl_xor's LDS crossbar (ds_bpermute + lgkm waits per step, and loop-invariant lane
-// addresses that the fused kernels spilled): quad permutes, row half-mirror and mirror
-// (16-lane rows), then row_bcast:15 / row_bcast:31 carry rows into lane 63.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ int dpp_max_step(int v) {
-  return max(v, __builtin_amdgcn_update_dpp(v, v, CTRL, ROWS, 0xF, false));
-}
-__device__ __forceinline__ int wave_max_i32(int v) {
-  v = dpp_max_step<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
-  v = dpp_max_step<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
-  v = dpp_max_step<0x141, 0xF>(v);  // row_half_mirror
-  v = dpp_max_step<0x140, 0xF>(v);  // row_mirror
-  v = dpp_max_step<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
-  v = dpp_max_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
-  return __builtin_amdgcn_readlane(v, 63);
-}
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t dpp_add_step(uint32_t v) {
-  // lanes outside ROWS add 0 (old = 0)
-  return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, false);
-}
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-  v = dpp_add_step<0xB1, 0xF>(v);
-  v = dpp_add_step<0x4E, 0xF>(v);
-  v = dpp_add_step<0x141, 0xF>(v);
-  v = dpp_add_step<0x140, 0xF>(v);
-  v = dpp_add_step<0x142, 0xA>(v);
-  v = dpp_add_step<0x143, 0xC>(v);
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-// java.lang.Math.max(double, double)
-__device__ __forceinline__ double java_max(double a, double b) {
-  if (a != a) return a;
-  if (b != b) return b;
-  if (a == 0.0 && b == 0.0) return __signbit(a) ? b : a;
-  return a >= b ? a : b;
-}
-
-// [Duke 1.2] utils.Utils.computeBayes
-__device__ __forceinline__ double compute_bayes(double p1, double p2) {
-  return (p1 * p2) / ((p1 * p2) + ((1.0 - p1) * (1.0 - p2)));
-}
-
-// A Java String's code units, read a 32-bit word (4 Latin-1 or 2 UTF-16 units) at a time.
-// Words of one value are `wstride` words apart: 1 in the canonical arena (strings start
-// 4-byte aligned, zero padded), the replica's position count in the candidate replica
-// ([word k][position g]: the 64 lanes of a wave read 64 consecutive words).  Units past
-// a value's length read as 0 in both layouts.
-template <typename CT>
-struct Str {
-  static constexpr int UPW = 4 / (int)sizeof(CT);  // units per word
-  const uint32_t* w;
-  uint64_t wstride;
-  int kmax;  // last word that may be read speculatively (replica: its row count - 1)
-  __device__ __forceinline__ uint32_t word(int k) const { return w[(uint64_t)k * wstride]; }
-  // a word read without a per-lane branch (the caller masks words past the value): the
-  // canonical arena keeps >= 512 zero bytes after the last value, the replica is clamped
-  __device__ __forceinline__ uint32_t word_any(int k) const { return w[(uint64_t)min(k, kmax) * wstride]; }
-  // the same read issued where it stands: an invariant load may be sunk to its use by the
-  // compiler (undoing a software prefetch); a relaxed atomic load is a plain global_load
-  // that stays put
-  __device__ __forceinline__ uint32_t word_pf(int k) const {
-    return __hip_atomic_load(w + (uint64_t)min(k, kmax) * wstride, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-  }
-  static __device__ __forceinline__ uint32_t unit(uint32_t x, int u) {
-    return sizeof(CT) == 1 ? (x >> (8 * u)) & 0xFFu : (x >> (16 * u)) & 0xFFFFu;
-  }
-  __device__ __forceinline__ uint32_t operator[](int j) const { return unit(word(j / UPW), j % UPW); }
-};
-
-// Length of the common prefix of a and b, at most `last` (<= 4 and <= both lengths), from
-// their first words by XOR and trailing-zero count (units past a value read as 0 in both
-// layouts, and `last` cuts at the shorter value) — no per-unit loop of dependent loads.
-template <typename CT>
-__device__ __forceinline__ int common_prefix4(const Str<CT>& a, const Str<CT>& b, int last) {
-  constexpr int UB = 8 * (int)sizeof(CT);
-  int p;
-  const uint32_t x0 = a.word(0) ^ b.word(0);
-  if (sizeof(CT) == 1) {
-    p = x0 ? (int)(__builtin_ctz(x0) / UB) : 4;
-  } else {
-    const uint32_t x1 = a.word_any(1) ^ b.word_any(1);
-    p = x0 ? (int)(__builtin_ctz(x0) / UB) : (x1 ? 2 + (int)(__builtin_ctz(x1) / UB) : 4);
-  }
-  return min(p, last);
-}
-
-template <typename CT>
-__device__ __forceinline__ bool str_equal(const Str<CT>& a, int na, const Str<CT>& b, int nb) {
-  if (na != nb) return false;
-  const int nw = (na + Str<CT>::UPW - 1) / Str<CT>::UPW;
-#ifdef DK_STREQ_SERIAL
-  for (int k = 0; k < nw; ++k)
-    if (a.word(k) != b.word(k)) return false;
-#else
-  // the first word alone (most unequal values differ in it: all-pairs Levenshtein pays
-  // for extra loads there), then four words per round with their loads issued together: a
-  // 10-unit date is two round trips instead of three dependent ones (word_any stays inside
-  // both layouts' padding; words past the value are masked)
-  if (nw == 0) return true;
-  if (a.word(0) != b.word(0)) return false;
-  for (int k = 1; k < nw; k += 4) {
-    uint32_t d = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t x = a.word_any(k + i) ^ b.word_any(k + i);
-      d |= k + i < nw ? x : 0u;
-    }
-    if (d) return false;
-  }
-#endif
-  return true;
-}
-
-// ------------------------------------------------------------------------------------
-// Per-wave query tables.  Every wave of k_score holds ONE query record (the candidate
-// slots of a query are padded to a multiple of 64), so the query's value of a property
-// is wave-uniform.  For it the wave builds, in its LDS slice, the position-mask table
-// Peq[c] = {i : q[i] == c} (Myers' "Peq"): 256 entries for Latin-1 units; UTF-16 units
-// use a low-byte and a high-byte table whose AND is exact.  A candidate code unit x then
-// yields all query positions holding x with one or two LDS reads.
-// ------------------------------------------------------------------------------------
-constexpr int kPeqEntries = 512;  // per wave: [0,256) low byte, [256,512) high byte
-
-__device__ __forceinline__ void wave_lds_sync() {
-  // orders this wave's LDS accesses (no other wave touches its slice)
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-  __builtin_amdgcn_wave_barrier();
-}
 
 template <typename CT>
 __device__ __forceinline__ void peq_set(uint64_t* peq, const CT* s, int n, bool on) {
@@ -259,90 +113,11 @@ __device__ __forceinline__ int ffs64(uint64_t m) { return (int)__builtin_ctzll(m
 // ------------------------------------------------------------------------------------
 // [Duke 1.2] comparators.Levenshtein.compactDistance with a wave-uniform s1 (the query
 // value, Processor.compare's r1).  One lane per candidate s2; the DP column over s1's
-// rows lives in VGPRs, unrolled to MAXM and cut at the uniform n1 by scalar branches.
-// The cell is Duke's min(above, aboveleft, left) + cost; the cost bit of row i in column
-// j is bit i of ~Peq[s2[j]].  Per cell: one v_bfe, one v_min3, one add, a min for the
-// cutoff.  Preconditions: 1 <= n1 <= MAXM; act lanes have n2 >= 1.
-// ------------------------------------------------------------------------------------
-// R rows are computed unconditionally (R = n1 rounded up to the bucket); rows past n1
-// compute values that never feed rows <= n1 (the recurrence only looks up and left) and
-// are masked out of the cutoff minimum.  Only the last TAIL rows can lie past n1.
-template <int R>
-struct LevCol {  // one lane's DP column over the query rows, kept in VGPRs
-  static constexpr int TAIL = R <= 32 ? 4 : 8;
-  int col[R + 1];
-  int n1, n2, maxdist, result;
-  bool live;
-
-  // column j >= 1 of Duke's loop with cost mask ne (bit i = s1[i] != s2[j])
-  __device__ __forceinline__ void step(uint64_t ne, int j) {
-    int above = j + 1, diag = j, smallest = 0x3FFFFFFF;
-#pragma unroll
-    for (int i = 1; i <= R; ++i) {
-      const int left = col[i];
-      const int v = imin3(above, diag, left) + (int)((ne >> (i - 1)) & 1ull);
-      diag = left;
-      col[i] = v;
-      above = v;
-      // n1 is wave-uniform: the tail-row mask is a scalar select
-      smallest = min(smallest, (i <= R - TAIL || i <= n1) ? v : 0x3FFFFFFF);
-    }
-    if (smallest > maxdist) {        // Duke's cutoff: return the column minimum
-      result = smallest;
-      live = false;
-    } else if (j + 1 >= n2) {        // last column: return D[n1][n2]
-      int r = col[R - TAIL + 1];
-#pragma unroll
-      for (int i = R - TAIL + 2; i <= R; ++i) r = i == n1 ? col[i] : r;
-      result = r;
-      live = false;
-    }
-  }
-};
-
-template <int R, typename CT>
-__device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1, const Str<CT>& s2,
-                                                    int n2, bool act) {
-  constexpr int UPW = Str<CT>::UPW;
-  LevCol<R> L;
-  L.n1 = n1;
-  L.n2 = n2;
-  L.maxdist = min(n1, n2) >> 1;
-  L.result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
-  uint32_t w = act ? s2.word(0) : 0u;
-  // first column: min(column[ix1-1], ix1-1) + cost
-  const uint64_t ne0 = ~peq_eq<CT>(peq, Str<CT>::unit(w, 0));
-  int prev = 1;
-#pragma unroll
-  for (int i = 1; i <= R; ++i) {
-    const int v = min(prev, i - 1) + (int)((ne0 >> (i - 1)) & 1ull);
-    L.col[i] = v;
-    prev = v;
-  }
-  L.live = act && n2 > 1;
-  // one word of s2 prefetched ahead (UPW columns of latency cover), and the Peq read of
-  // column j+1 issued before column j's DP so it lands while the column computes;
-  // (j + 1) % UPW is wave-uniform, so the word rotation is a scalar branch
-  // Words past the value are read speculatively (word_any) and only ever feed columns no
-  // live lane computes: a load under a per-lane condition would be waited for at once
-  // (hipcc branches around it and waits vmcnt(0) at the join).
-  uint32_t wn = s2.word_any(1);
-  uint64_t ne_next = ~peq_eq<CT>(peq, UPW > 1 ? Str<CT>::unit(w, 1) : wn);
-  for (int j = 1; L.live; ++j) {
-    const uint64_t ne = ne_next;
-    const int jn = j + 1;
-    if (jn % UPW == 0) {
-      w = wn;
-      wn = s2.word_any(jn / UPW + 1);
-    }
-    ne_next = ~peq_eq<CT>(peq, Str<CT>::unit(w, jn % UPW));
-    L.step(ne, j);
-  }
-  return L.result;
-}
-
-// ------------------------------------------------------------------------------------
-// The same DP with two rows per VGPR.  The column is split into a top half (rows 1..H)
+// rows lives in VGPRs, unrolled to the row bucket R and cut at the uniform n1 by scalar
+// branches.  The cell is Duke's min(above, aboveleft, left) + cost; the cost bit of row i
+// in column j is bit i of ~Peq[s2[j]].
+//
+// Two rows per VGPR: the column is split into a top half (rows 1..H)
 // and a bottom half (rows H+1..2H), the bottom half running one column behind: at step t
 // the register of pair i holds (lo) top row i of column t and (hi) bottom row H+i of
 // column t-1.  The two halves of a register are then independent, so one packed 3-way
@@ -365,103 +140,18 @@ __device__ __forceinline__ int compact_distance_peq(const uint64_t* peq, int n1,
 // all-BIG bottom "column -2"; bottom's step-0 costs are all 1, which turns that into
 // D(H+i, -1) = H + i.
 // ------------------------------------------------------------------------------------
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(us2, a),
-                                                                __builtin_bit_cast(us2, b)));
-}
-
-// min of three packed pairs.  Default: one v_pk_minimum3_f16 — every DP value is kept in
+// min of three packed pairs: one v_pk_minimum3_f16 — every DP value is kept in
 // [0x3F00, 0x7000], positive normal half floats, whose order is their bit patterns' order
 // (no NaN, infinity, denormal or sign bit can occur), so the f16 minimum is the u16 minimum.
 __device__ __forceinline__ uint32_t pk_min3_u16(uint32_t a, uint32_t b, uint32_t c) {
-#ifdef DK_LEV_PKMIN
-  return pk_min_u16(a, pk_min_u16(b, c));
-#else
   uint32_t r;
   asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
-#endif
-}
-
-template <int R, typename CT>
-__device__ __forceinline__ int compact_distance_pk(const uint64_t* peq, int n1, const Str<CT>& s2,
-                                                   int n2, bool act) {
-  constexpr int UPW = Str<CT>::UPW;
-  constexpr int H = R / 2;
-  constexpr int TAIL = R <= 32 ? 4 : 8;  // rows past n1 lie in (R - TAIL, R]
-  constexpr int NC = (H + 15) / 16;      // cost words
-  constexpr uint32_t BIG = 0x7000u;
-  const int maxdist = min(n1, n2) >> 1;
-  const uint32_t B = 0x4000u - (uint32_t)(maxdist + 1);
-  uint32_t P[H + 1];
-#pragma unroll
-  for (int i = 1; i <= H; ++i) P[i] = ((uint32_t)i + B) | (BIG << 16);
-  // the cutoff AND skips rows past n1 (wave-uniform: scalar masks)
-  uint32_t tm[H + 1];
-#pragma unroll
-  for (int i = 1; i <= H; ++i)
-    tm[i] = (i > n1 ? 0x4000u : 0u) | (H + i > n1 ? 0x40000000u : 0u);
-  const bool bottom_result = n1 > H;
-  int result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
-  bool live = act && n2 > 1;
-  const int fin = n2 - 1 + (bottom_result ? 1 : 0);  // step at which D(n1, n2-1) is known
-
-  uint32_t w = act ? s2.word(0) : 0u;
-  uint32_t wn = s2.word_any(1);
-  uint64_t ne_cur = ~peq_eq<CT>(peq, Str<CT>::unit(w, 0));
-  uint64_t ne_prev = ~0ull;
-  uint32_t h1 = 0, h2 = BIG;  // top row H of columns t-1, t-2 (h1 is read from P[H])
-  uint32_t acc_prev = 0;
-  for (int t = 0; live; ++t) {
-    const int tn = t + 1;
-    if (tn % UPW == 0) {
-      w = wn;
-      wn = s2.word_any(tn / UPW + 1);
-    }
-    const uint64_t ne_nx = ~peq_eq<CT>(peq, Str<CT>::unit(w, tn % UPW));
-    uint32_t C[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-      C[c] = ((uint32_t)(ne_cur >> (16 * c)) & 0xFFFFu) | ((uint32_t)(ne_prev >> (H + 16 * c)) << 16);
-    h1 = P[H] & 0xFFFFu;
-    uint32_t above = ((uint32_t)t + 1u + B) | (h1 << 16);
-    uint32_t diag = ((uint32_t)t + B) | (h2 << 16);
-    uint32_t acc = 0xFFFFFFFFu;
-#pragma unroll
-    for (int i = 1; i <= H; ++i) {
-      const uint32_t cost = (C[(i - 1) >> 4] >> ((i - 1) & 15)) & 0x10001u;
-      const uint32_t left = P[i];
-      const uint32_t v = pk_min3_u16(above, diag, left) + cost;
-      diag = left;
-      P[i] = v;
-      above = v;
-      if (H + i > R - TAIL) acc &= v | tm[i];
-      else acc &= v;
-    }
-    h2 = h1;
-    if (t >= 2 && (acc_prev & acc & 0x40004000u) == 0x40004000u) {  // column t-1 cut off
-      result = maxdist + 1;
-      live = false;
-    } else if (t == fin) {
-      uint32_t r = 0;
-#pragma unroll
-      for (int row = R - TAIL + 1; row <= R; ++row)
-        if (row == n1) r = row <= H ? (P[row] & 0xFFFFu) : (P[row - H] >> 16);
-      result = (int)(r - B);
-      live = false;
-    }
-    acc_prev = acc;
-    ne_prev = ne_cur;
-    ne_cur = ne_nx;
-  }
-  return result;
 }
 
 // ------------------------------------------------------------------------------------
-// compact_distance_pk with the column loop unrolled over one candidate word (UPW columns)
-// and two register sets used in turn (ping-pong): column t reads set A and writes set B,
+// The column loop is unrolled over one candidate word (UPW columns) with two register
+// sets used in turn (ping-pong): column t reads set A and writes set B,
 // column t+1 reads B and writes A.  In the rolled loop a cell's `diag` is the previous
 // column's value of the row above, which the row above has already overwritten, so the
 // compiler kept two sets anyway and copied the new one back at every back-edge (one
@@ -471,8 +161,8 @@ __device__ __forceinline__ int compact_distance_pk(const uint64_t* peq, int n1, 
 // ahead.  Lanes whose DP ended keep stepping (their result is latched; a masked lane
 // costs the SIMD nothing) until no lane of the wave is live, checked after every column.
 // Outcome: Duke's distance when it is <= maxdist, else some value > maxdist (maxdist + 1 at
-// a cutoff, D(n1, n2) when the lane reaches its last column) -- compact_distance_pk's
-// contract; the raw similarity of a cut-off pair comes from k_lev_exact.
+// a cutoff, D(n1, n2) when the lane reaches its last column), as stated above; the raw
+// similarity of a cut-off pair comes from k_lev_exact.
 // ------------------------------------------------------------------------------------
 template <int R, typename CT>
 __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, const Str<CT>& s2,
@@ -493,12 +183,6 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
   // column, whose D(n1, n2) then exceeds maxdist as well (a column minimum above maxdist
   // stays above it in every later column), so the probability (low) is the same; masking
   // them cost one v_or per tail pair per column (-1.6 % dedup step without it).
-#ifdef DK_LEV_TAILMASK
-  uint32_t tm[H + 1];
-#pragma unroll
-  for (int i = 1; i <= H; ++i)
-    tm[i] = (i > n1 ? 0x4000u : 0u) | (H + i > n1 ? 0x40000000u : 0u);
-#endif
   const bool bottom_result = n1 > H;
   int result = 0;  // |s2| == 1: Duke returns its initial `above` (0)
   bool live = act && n2 > 1;
@@ -509,11 +193,7 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
   // cost masks at the width the column needs: rows [0, H + 16) of a Peq entry, so 32 bits
   // up to 32 rows (a 32-bit LDS read leaves no dead half whose register reuse would force
   // the read's wait in the column that issues it)
-#ifdef DK_LEV_NE64
-  constexpr bool kNarrow = false;  // A/B: 64-bit Peq reads at every row count
-#else
   constexpr bool kNarrow = H <= 16;
-#endif
   using NT = typename std::conditional<kNarrow, uint32_t, uint64_t>::type;
   auto ne_of = [&](uint32_t x) -> NT {
     if constexpr (sizeof(NT) == 4) return (NT)~peq_eq_t<uint32_t, CT>(peq, x);
@@ -544,12 +224,7 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
       diag = Pin[i];
       Pout[i] = v;
       above = v;
-#ifdef DK_LEV_TAILMASK
-      if (H + i > R - TAIL) acc &= v | tm[i];
-      else acc &= v;
-#else
       acc &= v;  // rows past n1 in the cutoff AND: see above
-#endif
     }
     h2 = h1;
     if (live) {
@@ -589,14 +264,6 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
 // [Duke 1.2] comparators.Levenshtein.compare.  RMAX: the largest row bucket this kernel
 // variant instantiates (the host picks the variant from the longest Levenshtein value),
 // which bounds the VGPRs of the whole fused kernel and so its occupancy.
-#if defined(DK_LEV_SCALAR)
-#define DK_LEV_DP compact_distance_peq
-#elif defined(DK_LEV_ROLLED)
-#define DK_LEV_DP compact_distance_pk
-#else
-#define DK_LEV_DP compact_distance_pp
-#endif
-
 template <int RMAX, typename CT>
 __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str<CT>& s1, int n1,
                                                   const Str<CT>& s2, int n2, bool act) {
@@ -613,32 +280,30 @@ __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str
   // row buckets of 2 up to 16 rows (a date "YYYY-MM-DD" takes 10 rows, not 12), of 4 up to
   // 32, of 8 above (n1 is wave-uniform: a scalar switch)
   int d;
-#ifndef DK_LEV_BUCKET4
   if (n1 <= 16) {
     switch ((n1 + 1) >> 1) {
-      case 1: case 2: d = DK_LEV_DP<4>(peq, n1, s2, n2, run); break;
-      case 3: d = DK_LEV_DP<6>(peq, n1, s2, n2, run); break;
-      case 4: d = DK_LEV_DP<8>(peq, n1, s2, n2, run); break;
-      case 5: d = DK_LEV_DP<10>(peq, n1, s2, n2, run); break;
-      case 6: d = DK_LEV_DP<12>(peq, n1, s2, n2, run); break;
-      case 7: d = DK_LEV_DP<14>(peq, n1, s2, n2, run); break;
-      default: d = DK_LEV_DP<16>(peq, n1, s2, n2, run); break;
+      case 1: case 2: d = compact_distance_pp<4>(peq, n1, s2, n2, run); break;
+      case 3: d = compact_distance_pp<6>(peq, n1, s2, n2, run); break;
+      case 4: d = compact_distance_pp<8>(peq, n1, s2, n2, run); break;
+      case 5: d = compact_distance_pp<10>(peq, n1, s2, n2, run); break;
+      case 6: d = compact_distance_pp<12>(peq, n1, s2, n2, run); break;
+      case 7: d = compact_distance_pp<14>(peq, n1, s2, n2, run); break;
+      default: d = compact_distance_pp<16>(peq, n1, s2, n2, run); break;
     }
   } else
-#endif
   switch ((n1 + 3) >> 2) {
-    case 1: d = DK_LEV_DP<4>(peq, n1, s2, n2, run); break;
-    case 2: d = DK_LEV_DP<8>(peq, n1, s2, n2, run); break;
-    case 3: d = DK_LEV_DP<12>(peq, n1, s2, n2, run); break;
-    case 4: d = DK_LEV_DP<16>(peq, n1, s2, n2, run); break;
-    case 5: d = DK_LEV_DP<20>(peq, n1, s2, n2, run); break;
-    case 6: d = DK_LEV_DP<24>(peq, n1, s2, n2, run); break;
-    case 7: d = DK_LEV_DP<28>(peq, n1, s2, n2, run); break;
-    case 8: d = DK_LEV_DP<32>(peq, n1, s2, n2, run); break;
-    case 9: case 10: d = DK_LEV_DP<(RMAX < 40 ? 4 : 40)>(peq, n1, s2, n2, run); break;
-    case 11: case 12: d = DK_LEV_DP<(RMAX < 48 ? 4 : 48)>(peq, n1, s2, n2, run); break;
-    case 13: case 14: d = DK_LEV_DP<(RMAX < 56 ? 4 : 56)>(peq, n1, s2, n2, run); break;
-    default: d = DK_LEV_DP<(RMAX < 64 ? 4 : 64)>(peq, n1, s2, n2, run); break;
+    case 1: d = compact_distance_pp<4>(peq, n1, s2, n2, run); break;
+    case 2: d = compact_distance_pp<8>(peq, n1, s2, n2, run); break;
+    case 3: d = compact_distance_pp<12>(peq, n1, s2, n2, run); break;
+    case 4: d = compact_distance_pp<16>(peq, n1, s2, n2, run); break;
+    case 5: d = compact_distance_pp<20>(peq, n1, s2, n2, run); break;
+    case 6: d = compact_distance_pp<24>(peq, n1, s2, n2, run); break;
+    case 7: d = compact_distance_pp<28>(peq, n1, s2, n2, run); break;
+    case 8: d = compact_distance_pp<32>(peq, n1, s2, n2, run); break;
+    case 9: case 10: d = compact_distance_pp<(RMAX < 40 ? 4 : 40)>(peq, n1, s2, n2, run); break;
+    case 11: case 12: d = compact_distance_pp<(RMAX < 48 ? 4 : 48)>(peq, n1, s2, n2, run); break;
+    case 13: case 14: d = compact_distance_pp<(RMAX < 56 ? 4 : 56)>(peq, n1, s2, n2, run); break;
+    default: d = compact_distance_pp<(RMAX < 64 ? 4 : 64)>(peq, n1, s2, n2, run); break;
   }
   if (run) {
     const int dist = min(d, len);
@@ -1212,13 +877,6 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
   return score;
 }
 
-// [Duke 1.2] comparators.QGramComparator.compare over precomputed sorted unique gram sets
-__device__ __forceinline__ double qgram_formula(int common, int m1, int m2, int formula) {
-  if (formula == DK_QGRAM_JACCARD) return (double)common / (double)(m1 + m2 - common);
-  if (formula == DK_QGRAM_DICE) return (2.0 * (double)common) / (double)(m1 + m2);
-  return (double)common / fmin((double)m1, (double)m2);
-}
-
 // [Duke 1.2, recalled] DiceCoefficientComparator / JaccardIndexComparator with the
 // ExactComparator sub-comparator: the tokens of the shorter list (s1 on a tie) that occur
 // in the other, counted with multiplicity (sorted token ids, duplicates kept)
@@ -1232,72 +890,6 @@ __device__ __forceinline__ int count_members(const uint64_t* __restrict__ g1, in
     j += (y < x);
   }
   return hit;
-}
-
-// |Q ∩ C| with the query's gram set Q in a per-wave LDS hash table (open addressing,
-// load <= 1/2, key + 1 stored so 0 marks an empty slot; the caller excludes a set holding
-// the all-ones code) and each lane probing its candidate's grams in order — the loads of a
-// lane's own list are independent of the probes, so they are issued one gram ahead instead
-// of the data-dependent two-list merge.  Wave-uniform call; the table is cleared on exit
-// (the LDS slice is the query's Peq table between properties, all zero).
-constexpr int kQgramHashMax = 128;  // grams of a query held in the table (<= 256 slots)
-
-__device__ __forceinline__ uint32_t gram_hash(uint64_t code, int lt) {
-  return (((uint32_t)code ^ (uint32_t)(code >> 32)) * 0x9E3779B1u) >> (32 - lt);
-}
-
-template <typename GT>
-__device__ __forceinline__ int qgram_common_hashed(uint64_t* tab, const uint64_t* __restrict__ g1, int m1,
-                                                   const GT* __restrict__ g2, uint64_t gstride,
-                                                   int gmax, int m2) {
-  const int lt = m1 <= 32 ? 6 : (m1 <= 64 ? 7 : 8);
-  const uint32_t tmask = (1u << lt) - 1u;
-  for (int i = (int)lane_id(); i < m1; i += 64) {
-    const uint64_t key = g1[i] + 1ull;
-    uint32_t h = gram_hash(g1[i], lt);
-    while (atomicCAS((unsigned long long*)&tab[h], 0ull, (unsigned long long)key) != 0ull)
-      h = (h + 1u) & tmask;  // the set is unique: a taken slot holds another gram
-  }
-  wave_lds_sync();
-  // the lane's grams in chunks of 8 independent loads (clamped indices: no branch around a
-  // load), the next chunk in flight while the current one probes
-  int common = 0;
-  constexpr int CH = 8;
-  uint64_t cur[CH], nxt[CH];
-#pragma unroll
-  for (int u = 0; u < CH; ++u) cur[u] = (uint64_t)g2[(uint64_t)min(u, gmax) * gstride];
-  for (int k0 = 0; k0 < m2; k0 += CH) {
-#pragma unroll
-    for (int u = 0; u < CH; ++u) nxt[u] = (uint64_t)g2[(uint64_t)min(k0 + CH + u, gmax) * gstride];
-    // first probes of the chunk issued together (one LDS latency for 8 grams); a slot
-    // holding another gram sends that gram down its probe sequence
-    uint32_t h[CH];
-    uint64_t v[CH];
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      h[u] = gram_hash(cur[u], lt);
-      v[u] = tab[h[u]];
-    }
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      if (k0 + u < m2) {
-        const uint64_t key = cur[u] + 1ull;
-        uint64_t x = v[u];
-        uint32_t hh = h[u];
-        while (x != key && x != 0ull) {
-          hh = (hh + 1u) & tmask;
-          x = tab[hh];
-        }
-        common += x == key ? 1 : 0;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < CH; ++u) cur[u] = nxt[u];
-  }
-  wave_lds_sync();
-  for (int e = (int)lane_id(); e <= (int)tmask; e += 64) tab[e] = 0ull;
-  wave_lds_sync();
-  return common;
 }
 
 // |Q ∩ C| for Latin-1 bigram sets (DevProp::g16).  The query's keys go to their slots of a
@@ -1315,16 +907,11 @@ __device__ __forceinline__ int qgram_common_perfect(uint32_t* tab, const uint64_
   const int sh = 32 - lt;
   const int lane = (int)lane_id();
   if (lane == 0) tab[0] = ~0u;  // a real key landing in slot 0 overwrites the sentinel below
-  uint32_t s0 = 0u, s1 = 0u;    // this lane's query slots (m1 <= kGramPerfectMax = 128)
+  uint32_t s0 = 0u;             // this lane's query slot (m1 <= kGramPerfectMax = 64)
   if (lane < m1) {
     const uint32_t key = gram_key(g1[lane]);
     s0 = (uint32_t)__umul24(key, mult) >> sh;
     tab[s0] = key;
-  }
-  if (lane + 64 < m1) {
-    const uint32_t key = gram_key(g1[lane + 64]);
-    s1 = (uint32_t)__umul24(key, mult) >> sh;
-    tab[s1] = key;
   }
   wave_lds_sync();
   int njw = (m2 + 3) >> 2;  // word rows: this lane's, then the wave's most (the trip count)
@@ -1361,32 +948,9 @@ __device__ __forceinline__ int qgram_common_perfect(uint32_t* tab, const uint64_
   }
   wave_lds_sync();
   if (lane < m1) tab[s0] = 0u;
-  if (lane + 64 < m1) tab[s1] = 0u;
   if (lane == 0) tab[0] = 0u;
   wave_lds_sync();
   return common;
-}
-
-__device__ __forceinline__ int intersect_sorted(const uint64_t* __restrict__ g1, int m1,
-                                                const uint64_t* __restrict__ g2, int m2) {
-  int i = 0, j = 0, common = 0;
-  while (i < m1 && j < m2) {
-    const uint64_t x = g1[i], y = g2[j];
-    common += (x == y);
-    i += (x <= y);
-    j += (y <= x);
-  }
-  return common;
-}
-
-// [Duke 1.2] comparators.NumericComparator.compare on host-parsed values
-__device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool ok2, double minratio) {
-  if (!ok1 || !ok2) return 0.5;
-  if (d1 == 0.0 && d2 == 0.0) return 1.0;
-  if (d2 < d1) { const double t = d2; d2 = d1; d1 = t; }
-  const double ratio = d1 / d2;
-  if (ratio < minratio) return 0.0;
-  return ratio;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1563,20 +1127,6 @@ __device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, d
                                            uint32_t crow, uint32_t qi, uint32_t scored,
                                            uint32_t bytes) {
   block_emit_at(out, blockIdx.x, kind, prob, crow, qi, scored, bytes);
-}
-
-// [Duke 1.2] Processor.compareCandidatesSimple: strict thresholds
-__device__ __forceinline__ uint32_t decide(double prob, double threshold, double maybe) {
-  if (prob > threshold) return DK_KIND_MATCH;
-  if (maybe != 0.0 && prob > maybe) return DK_KIND_MAYBE;
-  return 0;
-}
-
-// [Duke 1.2] PropertyImpl.compare then the start of Processor.compare's java_max
-__device__ __forceinline__ double property_prob(const DevProp& D, double sim) {
-  const double v = D.op == DK_CMP_NONE ? 0.5
-                   : (sim < 0.5 ? D.low : ((D.high - 0.5) * (sim * sim)) + 0.5);
-  return java_max(0.0, v);
 }
 
 // SYM: the owner slots of the symmetric dedup schedule (PairSource::sym): every owned pair
@@ -2001,7 +1551,7 @@ __global__ __launch_bounds__(256) void k_gram_seed(const uint64_t* __restrict__ 
                                                    const uint16_t* __restrict__ gcnt,
                                                    const uint16_t* __restrict__ len, uint64_t row0,
                                                    uint64_t n, uint16_t* __restrict__ seed) {
-  __shared__ uint32_t occ[256][33];  // 1024 bits per thread (+1 word: rows spread over banks)
+  __shared__ uint32_t occ[256][17];  // 512 bits per thread (+1 word: rows spread over banks)
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t row = row0 + i;
@@ -2009,7 +1559,7 @@ __global__ __launch_bounds__(256) void k_gram_seed(const uint64_t* __restrict__ 
   uint16_t out = kGramSeedNone;
   if (m > 0 && m <= kGramPerfectMax) {
     const uint64_t* g = grams + goff[row];
-    const int lt = m <= 32 ? 8 : (m <= 64 ? 9 : 10);
+    const int lt = m <= 32 ? 8 : 9;  // m <= kGramPerfectMax = 64
     const int words = 1 << (lt - 5);
     uint32_t* bits = occ[threadIdx.x];
     bool zero = false;
@@ -2100,7 +1650,7 @@ __device__ __forceinline__ uint64_t upper_bound_u64(const uint64_t* a, uint64_t 
 // query's own key is looked up by value, so a superseded or deleted query still finds
 // its block.  LINKAGE keeps only the other group's sub-range (rows are sorted by
 // (key, group, row) and groups are 1 and 2; IncrementalDataSource.java:80-84).
-template <bool PAD>
+template <int PAD>  // 0: exact counts; else rounded up to PAD slots
 __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const BlockTables T,
                         uint2* __restrict__ ranges, uint64_t* __restrict__ counts,
                         uint64_t* __restrict__ real) {
@@ -2124,7 +1674,7 @@ __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const
       ranges[(uint64_t)k * nq + i] = make_uint2((uint32_t)a, (uint32_t)b);
       total += b - a;
     }
-    counts[i] = PAD ? (total + 63) & ~(uint64_t)63 : total;
+    counts[i] = PAD ? (total + PAD - 1) / PAD * PAD : total;
   }
   if (!PAD) return;
   uint64_t w = total;
@@ -2562,16 +2112,18 @@ hipError_t launch_mark_dead(const BlockTables& T, const uint32_t* rows, uint64_t
 }
 
 hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint2* ranges,
-                        uint64_t* counts, uint64_t* real, hipStream_t s) {
+                        uint64_t* counts, uint64_t* real, int pad, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_count<true><<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, real);
+  if (pad == kScoreBlock) k_count<kScoreBlock><<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, real);
+  else if (pad == 64) k_count<64><<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, real);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
 hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockTables& T,
                               uint2* ranges, uint64_t* counts, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_count<false><<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, nullptr);
+  k_count<0><<<grid1d(nq), 256, 0, s>>>(queries, nq, T, ranges, counts, nullptr);
   return hipGetLastError();
 }
 
@@ -2729,6 +2281,12 @@ hipError_t launch_iota_u32(uint32_t* p, uint64_t n, hipStream_t s) {
 hipError_t sort_pairs_u64_u32(void* tmp, size_t& tmp_bytes, const uint64_t* kin, uint64_t* kout,
                               const uint32_t* vin, uint32_t* vout, uint64_t n, hipStream_t s) {
   return rocprim::radix_sort_pairs(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)n, 0, 64, s);
+}
+
+hipError_t sort_pairs_u64_u32_bits(void* tmp, size_t& tmp_bytes, const uint64_t* kin, uint64_t* kout,
+                                   const uint32_t* vin, uint32_t* vout, uint64_t n, int end_bit,
+                                   hipStream_t s) {
+  return rocprim::radix_sort_pairs(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)n, 0, end_bit, s);
 }
 
 hipError_t exclusive_scan_u64(void* tmp, size_t& tmp_bytes, const uint64_t* in, uint64_t* out,
