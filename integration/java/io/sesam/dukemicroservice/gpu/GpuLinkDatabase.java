@@ -15,20 +15,31 @@ import no.priv.garshol.duke.LinkStatus;
  * dk_linkdb_apply after the replay -- what BaseLinkDatabaseMatchListener's wrapped
  * LinkDatabaseMatchListener does per callback (BaseLinkDatabaseMatchListener.java:50,
  * 53-109) -- instead of one assertLink per link.  That per-callback path still runs (the
- * listener is unchanged) but its INFERRED assertions are ignored here: the bulk write is
- * authoritative.  The reads the routes make stay: getChangesSince for the GET ?since= feed
- * (App.java:742, 843), getAllLinksFor + a retracted assertLink for deleted records
- * (App.java:994-999, dk_linkdb_retract_all).  Links carry record ID strings as in Duke; the
+ * listener is unchanged), but GpuProcessor opens a listener window around each batch
+ * (batchReady .. batchDone) in which every write reaching this database is dropped -- the
+ * listener's INFERRED assertions and its own retractions of links a record no longer
+ * produced alike -- so the bulk write alone changes the database, as the Python host's
+ * GpuProcessor.set_link_database does (tests/test_linkdb.py::test_java_wiring_*).  Outside
+ * the window the routes' writes stay: getChangesSince for the GET ?since= feed (App.java:742,
+ * 843), getAllLinksFor + a retracted assertLink for deleted records (App.java:994-999,
+ * dk_linkdb_retract).  Links carry record ID strings as in Duke; the
  * natives work on the database's interned IDs (GpuBlockingDatabase.ids()).
  */
 public class GpuLinkDatabase extends SinceAwareInMemoryLinkDatabase {
     private final long ids;
     private final long db;
     private boolean nativeMode = true;   // false after handOver(): the Java superclass serves
+    private boolean listenerWindow;      // GpuProcessor is inside a batch: listener writes dropped
 
     public GpuLinkDatabase(GpuBlockingDatabase database) {
         this.ids = database.ids();
         this.db = DukeHip.linkdbCreate(ids);
+    }
+
+    /** GpuProcessor, around a batch's batchReady .. batchDone: the per-callback listener's
+     *  writes (assertLink of INFERRED and of RETRACTED links) are dropped while it is open. */
+    void setListenerWindow(boolean open) {
+        listenerWindow = open;
     }
 
     /** One batch's match list (dk_result arrays) for query records of the given IDs. */
@@ -41,6 +52,7 @@ public class GpuLinkDatabase extends SinceAwareInMemoryLinkDatabase {
      *  reference's own SinceAwareInMemoryLinkDatabase), which the per-callback listener then
      *  writes as in the reference. */
     void handOver() {
+        listenerWindow = false;
         if (!nativeMode) return;
         List<Link> all = getChangesSince(Long.MIN_VALUE);
         nativeMode = false;
@@ -53,12 +65,16 @@ public class GpuLinkDatabase extends SinceAwareInMemoryLinkDatabase {
             super.assertLink(link);
             return;
         }
+        // inside a batch: the listener's writes -- applyBatch has written (or will write) the
+        // batch's links and retractions itself
+        if (listenerWindow) return;
         // the deleted-record branch (App.java:994-999): link.retract() then assertLink, per link
         if (link.getStatus() == LinkStatus.RETRACTED) {
             long a = DukeHip.internerFind(ids, link.getID1()), b = DukeHip.internerFind(ids, link.getID2());
             if (a >= 0 && b >= 0) DukeHip.linkdbRetract(db, a, b, link.getTimestamp());
         }
-        // INFERRED links from the per-callback listener: already written by applyBatch
+        // an INFERRED link outside a batch: no route writes one (the listener runs only
+        // inside deduplicate)
     }
 
     @Override

@@ -81,9 +81,14 @@ public class GpuProcessor extends Processor {
         }
         int[] rows = new int[batch.size()];
         System.arraycopy(allRows, pending.size(), rows, 0, rows.length);
-        for (MatchListener l : listeners) l.batchReady(batch.size());
-        matchAndReplay(rows, batch);
-        for (MatchListener l : listeners) l.batchDone();
+        if (links != null) links.setListenerWindow(true);
+        try {
+            for (MatchListener l : listeners) l.batchReady(batch.size());
+            matchAndReplay(rows, batch);
+            for (MatchListener l : listeners) l.batchDone();
+        } finally {
+            if (links != null) links.setListenerWindow(false);
+        }
         db.releaseDeferred();
         if (db.indexingIsDisabled()) db.dropTransient();   // the batch never entered the index
     }
@@ -105,9 +110,14 @@ public class GpuProcessor extends Processor {
             if (e.code() != DukeHip.E_UNSUPPORTED) throw e;
             return false;
         }
-        for (MatchListener l : listeners) l.batchReady(rows.length);
-        matchAndReplay(rows, null);
-        for (MatchListener l : listeners) l.batchDone();
+        if (links != null) links.setListenerWindow(true);
+        try {
+            for (MatchListener l : listeners) l.batchReady(rows.length);
+            matchAndReplay(rows, null);
+            for (MatchListener l : listeners) l.batchDone();
+        } finally {
+            if (links != null) links.setListenerWindow(false);
+        }
         db.releaseDeferred();
         if (db.indexingIsDisabled()) db.dropTransient();
         return true;

@@ -190,3 +190,101 @@ def test_deleted_record_retraction_and_links_for(seed):
     assert got == [(l.id1, l.id2, l.status) for l in ref.all_links_for(some)] and got
     ldb.close()
     ids.close()
+
+
+class _JavaWiring:
+    """GpuLinkDatabase + GpuProcessor as wired in integration/java: the unchanged per-callback
+    listener (linkdb_ref.LinkDBListener, the reference's LinkDatabaseMatchListener) writes into
+    this database, which drops every write while GpuProcessor's listener window is open
+    (batchReady .. batchDone) and forwards a RETRACTED link outside it (the deleted-record
+    branch, App.java:994-999) to dk_linkdb_retract; getAllLinksFor reads the native links."""
+
+    def __init__(self, ids, ldb):
+        self.ids, self.ldb, self.window = ids, ldb, False
+
+    def all_links_for(self, rid):
+        lf = self.ldb.links_for(self.ids.intern([rid])[0])
+        return [R.Link(interned_string(self.ids, a), interned_string(self.ids, b), int(s), int(k),
+                       float(c), int(t))
+                for a, b, s, k, c, t in zip(lf["id1"], lf["id2"], lf["status"], lf["kind"],
+                                            lf["confidence"], lf["timestamp"])]
+
+    def assert_link(self, link):
+        if self.window:
+            return False
+        if link.status == R.RETRACTED:
+            a, b = self.ids.intern([link.id1, link.id2])
+            self.ldb.retract(a, b, link.timestamp)
+        return True
+
+
+@pytest.mark.parametrize("seed", [7, 8, 9])
+def test_java_wiring_listener_plus_bulk_equals_per_callback(seed):
+    """the Java drop-in's link wiring -- listener replay into the window-
+    dropping GpuLinkDatabase, the bulk applyBatch inside the window (after the replay, before
+    batchDone), deleted-record retractions between batches through assertLink -- gives the
+    same links and ?since= feed as the reference's per-callback listener on a plain
+    SinceAwareInMemoryLinkDatabase, on batches that re-assert, change and retract links."""
+    batches = random_batches(seed)
+    rng = random.Random(seed)
+    ref = R.SinceAwareLinkDB()
+    ids = Interner()
+    ldb = LinkDatabase(ids)
+    wired = _JavaWiring(ids, ldb)
+    for t, (qs, entries) in enumerate(batches):
+        ts = 1000 + 10 * t
+        for db in (ref, wired):
+            if db is wired:
+                wired.window = True                              # GpuProcessor.deduplicate
+            L = R.LinkDBListener(db, lambda ts=ts: ts)
+            L.batch_ready(len(qs))
+            for i, (q, lst) in enumerate(zip(qs, entries)):
+                if not lst:
+                    L.no_match_for((i, q))
+                for c, p, kind in lst:
+                    (L.matches if kind == 1 else L.matches_perhaps)((i, q), c, p)
+            if db is wired:                                      # matchAndReplay's applyBatch
+                qid = ids.intern(qs)
+                first = np.zeros(len(qs) + 1, np.uint64)
+                first[1:] = np.cumsum([len(x) for x in entries])
+                flat = [e for lst in entries for e in lst]
+                cid = ids.intern([c for c, _, _ in flat]) if flat else np.zeros(0, np.uint64)
+                ldb.apply(qid, first, cid, [p for _, p, _ in flat], [k for _, _, k in flat], timestamp=ts)
+            L.batch_done()
+            wired.window = False
+        # the next POST's deleted records (App.java:994-999), per link through assertLink
+        for q in rng.sample(qs, min(2, len(qs))):
+            ref.retract(q, ts + 5)
+            for link in wired.all_links_for(q):
+                link.status, link.timestamp = R.RETRACTED, ts + 5    # Link.retract()
+                wired.assert_link(link)
+    for since in [0] + [1000 + 10 * t for t in range(len(batches))]:
+        ch = ldb.changes_since(since)
+        got = [(interned_string(ids, a), interned_string(ids, b), int(s), int(k), float(c), int(t))
+               for a, b, s, k, c, t in zip(ch["id1"], ch["id2"], ch["status"], ch["kind"],
+                                           ch["confidence"], ch["timestamp"])]
+        assert got == [(l.id1, l.id2, l.status, l.kind, l.confidence, l.timestamp)
+                       for l in ref.changes_since(since)]
+    assert any(l.status == R.RETRACTED for l in ref.links.values())
+    ldb.close()
+    ids.close()
+
+
+def test_java_wiring_without_window_diverges():
+    """The wiring the window replaced (listener retractions forwarded during the replay,
+    before applyBatch) is observably different: the retracted links carry the listener's
+    writes first, so the check above is not vacuous."""
+    ids = Interner()
+    ldb = LinkDatabase(ids)
+    wired = _JavaWiring(ids, ldb)
+    q, c = ids.intern(["ds__1", "ds__2"])
+    ldb.apply([q], np.array([0, 1], np.uint64), [c], [0.95], [1], timestamp=100)
+    L = R.LinkDBListener(wired, lambda: 150)                      # window left closed
+    L.batch_ready(1)
+    L.no_match_for((0, "ds__1"))                                  # retracts via assertLink now
+    ldb.apply([q], np.array([0, 0], np.uint64), [], [], [], timestamp=200)
+    L.batch_done()
+    ch = ldb.changes_since(0)
+    assert int(ch["status"][0]) == LINK_RETRACTED and int(ch["timestamp"][0]) == 150   # not 200
+    ldb.close()
+    ids.close()
