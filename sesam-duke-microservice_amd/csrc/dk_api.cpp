@@ -484,7 +484,7 @@ struct dk_ctx {
   uint64_t rstride = 0;               // replica positions
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
   // k_score_grouped's execution order: task sort keys / values (double-buffered), chunk starts
-  DevBuf task_key, task_val, task_cb;
+  DevBuf task_key, task_val, task_cb, gprops;
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
   DevBuf ocounts, oqoff, owq, obase, ores, mcounts, mqoff, mbase, mres, bidx, bval;
@@ -1171,9 +1171,15 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   const int np = c->schema.nprops, ntask = np + nk + (c->luc.on ? 1 : 0);
   {
     int rc = run_tasks(ntask, n >= 8192, [&](int t) {
-      if (t < np) return stage_column(c, t, &b->columns[t], n, cols[t]);
-      if (t < np + nk) return stage_key(c, b, style, t - np, kv.data());
-      return stage_lucene(c, b, n, row0, transient, ls);
+      const auto t0 = std::chrono::steady_clock::now();
+      const int r = t < np ? stage_column(c, t, &b->columns[t], n, cols[t])
+                    : t < np + nk ? stage_key(c, b, style, t - np, kv.data())
+                                  : stage_lucene(c, b, n, row0, transient, ls);
+      if (lap.on)
+        fprintf(stderr, "dk_upsert   task %s %d %.2f ms\n", t < np ? "column" : t < np + nk ? "key" : "lucene",
+                t < np ? t : t - np,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+      return r;
     });
     if (rc) return rc;
   }
@@ -1942,17 +1948,49 @@ static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
 static bool grouped_schema_ok(const ScoreParams& P) {
   const char* e = getenv("DK_GROUPED");
   if ((e && e[0] == '0') || P.has_dp || P.raw_prop >= 0 || P.nprops < 1) return false;
+  // every buffer offset of the kernel's raw buffer loads below 2^31
+  if (P.rstride * 8 >= (1ull << 31)) return false;
   int tabs = 0;
   for (int p = 0; p < P.nprops; ++p) {
     const DevProp& D = P.props[p];
     if (D.op == DK_CMP_QGRAM) {
       if (!D.g16 || D.rgrows < 1 || D.width != 1) return false;
+      if ((uint64_t)D.rgrows * P.rstride * 8 >= (1ull << 31)) return false;
       ++tabs;
     } else if (D.op != DK_CMP_NUMERIC && D.op != DK_CMP_NONE) {
       return false;
     }
   }
   return tabs <= kGroupedTabs;
+}
+
+// k_score_grouped's per-property operand sources (GroupedProp) for the current replica
+static std::vector<GroupedProp> grouped_props(const ScoreParams& P) {
+  std::vector<GroupedProp> gp(P.nprops);
+  const uint64_t n = P.rstride;
+  for (int p = 0; p < P.nprops; ++p) {
+    const DevProp& D = P.props[p];
+    GroupedProp& G = gp[p];
+    memset(&G, 0, sizeof G);
+    G.len = D.rlen;
+    G.len_n = (uint32_t)(n * 2);
+    G.x = G.w = D.rlen;  // size 0 below unless the comparator has them
+    if (D.op == DK_CMP_QGRAM) {
+      G.x = D.rgcnt;
+      G.x_n = (uint32_t)(n * 2);
+      G.xsh = 1;
+      G.w = D.rgrams;
+      G.w_n = (uint32_t)((uint64_t)D.rgrows * n * 8);
+      G.rowb = (uint32_t)(n * 8);
+    } else if (D.op == DK_CMP_NUMERIC) {
+      G.x = D.rnumok;
+      G.x_n = (uint32_t)n;
+      G.w = D.rnum;
+      G.w_n = (uint32_t)(n * 8);
+      G.rowb = 0x80000000u;
+    }
+  }
+  return gp;
 }
 
 // Lucene source, per dk_match: every query's hits (k_lucene_topk) become its candidate
@@ -2277,6 +2315,12 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   // k_score_grouped: the tasks of each chunk in the order of their first candidate's replica
   // position (bucket by bucket), DK_TASK_SORT=0: slot order (A/B)
   const uint32_t* perm = nullptr;
+  if (grouped) {
+    const std::vector<GroupedProp> gp = grouped_props(P);
+    HIPCHK(c->gprops.reserve(gp.size() * sizeof(GroupedProp), 0, s));
+    HIPCHK(hipMemcpyAsync(c->gprops.p, gp.data(), gp.size() * sizeof(GroupedProp), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));  // gp is a temporary
+  }
   if (grouped && !(getenv("DK_TASK_SORT") && getenv("DK_TASK_SORT")[0] == '0')) {
     const uint64_t ntask = total / kScoreBlock;
     const int nch = (int)bounds.size() - 1;
@@ -2388,7 +2432,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging b drained
       {
         Timer t_score(c, &c->prof.ms_score, s);
-        if (grouped) HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, st[b], s));
+        if (grouped)
+          HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), st[b], s));
         else HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
         t_score.stop();
       }

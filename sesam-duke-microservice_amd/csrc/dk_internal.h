@@ -176,6 +176,21 @@ constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 // query's slots are padded to kScoreBlock (one task = one wave = one staging block)
 constexpr int kGroupedTabs = 2;
 
+// k_score_grouped's per-property operand sources, built by the host for each match (raw
+// buffer resources: base + size in bytes; size 0 = nothing to read) and read by the kernel
+// with scalar loads -- the resources then cost no per-group arithmetic or SGPRs to keep.
+struct GroupedProp {
+  const void* len;    // rlen (u16 per position)
+  const void* x;      // QGram: rgcnt (u16; its low byte); Numeric: rnumok (u8)
+  const void* w;      // QGram: rgrams rows (u64 key words); Numeric: rnum
+  uint32_t len_n, x_n, w_n;
+  uint32_t rowb;      // bytes between key-word rows (QGram); 0x80000000 (Numeric: rows >= 1
+                      // are out of range)
+  uint32_t xsh;       // x element = 1 << xsh bytes
+  uint32_t pad[5];
+};
+static_assert(sizeof(GroupedProp) == 64, "two s_load_dwordx8");
+
 // The emission pass of the symmetric schedule: slots of the full candidate order (qoff /
 // wq / ranges as in PairSource) read their probability from the owner results.
 struct EmitSource {
@@ -350,8 +365,8 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
 // k_score_grouped: slot0 and nslots multiples of kScoreBlock, slots padded per query to it;
 // perm (or NULL: task order) = the tasks in execution order (k_task_keys, sorted)
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
-                                uint64_t nslots, const uint32_t* perm, const StageOut& out,
-                                hipStream_t s);
+                                uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
+                                const StageOut& out, hipStream_t s);
 // key[t] = chunk << 32 | first candidate's replica position of task t, val[t] = t;
 // cb[0..nchunks] = first task of each chunk
 hipError_t launch_task_keys(const PairSource& src, uint64_t ntask, const uint64_t* cb, int nchunks,

@@ -26,8 +26,14 @@
 #ifndef DK_WAVES_GROUPED
 #define DK_WAVES_GROUPED 8  // k_score_grouped waves per SIMD
 #endif
+#ifndef DK_GROUPED_KEYS
+#define DK_GROUPED_KEYS 1   // key functions whose filter operand is prefetched (+1: the first)
+#endif
+#ifndef DK_GROUPED_TAIL
+#define DK_GROUPED_TAIL 4   // rows per load batch past 2 * DK_GROUPED_ROWS
+#endif
 #ifndef DK_GROUPED_ROWS
-#define DK_GROUPED_ROWS 3   // key-word rows (4 bigram keys each) loaded one property ahead
+#define DK_GROUPED_ROWS 2   // key-word rows (4 bigram keys each) loaded one property ahead
 #endif
 
 namespace dk {
@@ -35,7 +41,8 @@ namespace dk {
 constexpr int kTaskGroups = kScoreBlock / 64;  // groups of 64 slots per task
 constexpr int kPreRows = DK_GROUPED_ROWS;
 constexpr int kTabWords = 512;  // u32 per bigram table (lt <= 9)
-constexpr int kPreKeys = 2;     // key-function filters loaded one step ahead (3 key functions)
+constexpr int kPreKeys = DK_GROUPED_KEYS;  // key-function filters loaded one step ahead
+constexpr int kTailRows = DK_GROUPED_TAIL;
 constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data format
 
 // Candidate operands are read with raw buffer loads: every load of the prefetch is issued
@@ -43,12 +50,6 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data fo
 // flight -- and a load past a resource's size (a row the property does not have) returns 0
 // without a memory access.
 using rsrc_t = __amdgpu_buffer_rsrc_t;
-__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint64_t bytes) {
-  // (a ternary: HIP's min<uint64_t> goes through doubles, on the VALU, which made the
-  // resource divergent -- a waterfall loop around every load)
-  const uint32_t n = bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bytes;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)n, kRsrcWord3);
-}
 
 // The query's per-property values, staged in LDS once per task (LDS reads wait on lgkmcnt
 // only; a vector load of a uniform u16 would wait on vmcnt, draining the prefetch).
@@ -66,33 +67,29 @@ struct PreOps {
   uint64_t w[kPreRows];   // bigram QGram: key-word rows 0..kPreRows-1; Numeric: w[0] = rnum's bits
 };
 
-// Per-property buffer resources of the candidate operands (wave-uniform).  Key-word row j
-// of a bigram property is at byte g * 8 + j * rowb of one resource sized rgrows rows, so a
-// row past the property's rows is out of range; a Numeric property's value is "row 0" and
-// its other rows are pushed out of range.  Every offset stays below 2^32 (the host checks
-// rgrows * positions * 8 < 2^31 and positions * 8 < 2^31).
+// Per-property buffer resources of the candidate operands (wave-uniform), from the host's
+// GroupedProp record.  Key-word row j of a bigram property is at byte g * 8 + j * rowb of one
+// resource sized rgrows rows, so a row past the property's rows is out of range; a Numeric
+// property's value is "row 0" and its other rows are pushed out of range.  Every offset
+// stays below 2^32 (the host checks the sizes).
 struct OpRes {
   rsrc_t len, x, w;
   uint32_t rowb, xsh;
-  bool isq;
 };
 
-__device__ __forceinline__ OpRes op_res(const DevProp& D, uint64_t rstride) {
+__device__ __forceinline__ OpRes op_res(const GroupedProp* gp, int p) {
+  const GroupedProp G = gp[p];
   OpRes r;
-  r.isq = D.op == DK_CMP_QGRAM;
-  const bool isn = D.op == DK_CMP_NUMERIC;
-  r.len = make_rsrc(D.rlen, rstride * 2);
-  r.x = make_rsrc(r.isq ? static_cast<const void*>(D.rgcnt) : static_cast<const void*>(D.rnumok),
-                  r.isq ? rstride * 2 : isn ? rstride : 0);
-  r.w = make_rsrc(r.isq ? D.rgrams : static_cast<const void*>(D.rnum),
-                  r.isq ? (uint64_t)D.rgrows * rstride * 8 : isn ? rstride * 8 : 0);
-  r.rowb = (uint32_t)(rstride * 8);
-  r.xsh = r.isq ? 1u : 0u;
+  r.len = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.len), (short)0, (int)G.len_n, kRsrcWord3);
+  r.x = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.x), (short)0, (int)G.x_n, kRsrcWord3);
+  r.w = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.w), (short)0, (int)G.w_n, kRsrcWord3);
+  r.rowb = G.rowb;
+  r.xsh = G.xsh;
   return r;
 }
 
 __device__ __forceinline__ uint64_t ld_row(const OpRes& R, int j, uint32_t g) {
-  const uint32_t jb = R.isq ? (uint32_t)j * R.rowb : (j == 0 ? 0u : 0x80000000u);
+  const uint32_t jb = (uint32_t)j * R.rowb;  // Numeric: rowb = 2^31, so rows >= 1 are out of range
   return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.w, g * 8u + jb, 0, 0));
 }
 
@@ -166,7 +163,8 @@ __device__ __forceinline__ uint64_t grouped_task(const uint32_t* perm, uint64_t 
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_GROUPED, 8)))
 void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots,
-                     const uint32_t* __restrict__ perm, StageOut out) {
+                     const uint32_t* __restrict__ perm, const GroupedProp* __restrict__ gp,
+                     StageOut out) {
   __shared__ uint32_t lds[kScoreBlock / 64][kGroupedTabs * kTabWords];
   __shared__ QueryVals qlds[kScoreBlock / 64][kMaxProps];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -252,7 +250,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
   uint32_t crow_n;
   load_filters(cn, rid_n, rk_n, crow_n);
   PreOps nx;
-  load_ops(op_res(P.props[0], P.rstride), cn.g, cn.valid, nx);
+  load_ops(op_res(gp, 0), cn.g, cn.valid, nx);
 
   // the query's bigram sets in its perfect-hash tables (one per bigram property)
   for (int e = (int)lane * 4; e < kGroupedTabs * kTabWords; e += 256)
@@ -317,7 +315,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
       // prefetch (loads complete in order: waiting for these then never waits for that)
       const int m2 = cmp ? (int)(o.x & 0xFFu) : 0;
       const int njw = perfect ? wave_max_i32((m2 + 3) >> 2) : 0;  // key-word rows the wave needs
-      const OpRes R = op_res(D, P.rstride);
+      const OpRes R = op_res(gp, p);
       uint64_t ex[kPreRows];
       if (njw > kPreRows) {
 #pragma unroll
@@ -326,11 +324,11 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
       // the next step's operands: property p+1 of this group, or the next group's
       // positions, filters and property 0
       if (p + 1 < P.nprops) {
-        load_ops(op_res(P.props[p + 1], P.rstride), c.g, c.valid, nx);
+        load_ops(op_res(gp, p + 1), c.g, c.valid, nx);
       } else if (grp + 1 < ngroups) {
         cn = resolve(grp + 1);
         load_filters(cn, rid_n, rk_n, crow_n);
-        load_ops(op_res(P.props[0], P.rstride), cn.g, cn.valid, nx);
+        load_ops(op_res(gp, 0), cn.g, cn.valid, nx);
       }
       const int tslot = ts;
       if (isq) ++ts;
@@ -357,11 +355,15 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
 #pragma unroll
             for (int j = 0; j < kPreRows; ++j)
               if (kPreRows + j < njw) common += probe_word(tab, ex[j], mult, sh);
-            // sets of more than 8 * kPreRows grams: the rest two rows at a time
-            for (int j = 2 * kPreRows; j < njw; j += 2) {
-              const uint64_t w0 = ld_row(R, j, c.g);
-              const uint64_t w1 = ld_row(R, j + 1, c.g);
-              common += probe_word(tab, w0, mult, sh) + probe_word(tab, w1, mult, sh);
+            // longer sets: the rest DK_GROUPED_TAIL rows at a time (loads issued together;
+            // rows past the property's rows are out of range, free)
+            for (int j = 2 * kPreRows; j < njw; j += kTailRows) {
+              uint64_t w[kTailRows];
+#pragma unroll
+              for (int i = 0; i < kTailRows; ++i) w[i] = ld_row(R, j + i, c.g);
+#pragma unroll
+              for (int i = 0; i < kTailRows; ++i)
+                if (j + i < njw) common += probe_word(tab, w[i], mult, sh);
             }
           }
           if (m2 > 0) sim = qgram_formula(common, m1, m2, D.formula);
@@ -399,13 +401,13 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
 }
 
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
-                                uint64_t nslots, const uint32_t* perm, const StageOut& out,
-                                hipStream_t s) {
+                                uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
+                                const StageOut& out, hipStream_t s) {
   if (nslots == 0) return hipSuccess;
   if (nslots % kScoreBlock || slot0 % kScoreBlock) return hipErrorInvalidValue;
   const uint64_t ntask = nslots / kScoreBlock;
   const uint64_t grid = (ntask + kScoreBlock / 64 - 1) / (kScoreBlock / 64);
-  k_score_grouped<<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, out);
+  k_score_grouped<<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
   return hipGetLastError();
 }
 
