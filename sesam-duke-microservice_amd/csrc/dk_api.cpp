@@ -346,6 +346,41 @@ static void qgram_codes(const uint16_t* u0, int n0, int q, int tokenizer, std::v
   g.erase(std::unique(g.begin(), g.end()), g.end());
 }
 
+// The same for q <= 2 without POSITIONAL (codes fit 32 bits: configs[2]'s bigrams), straight
+// from the column's units into `out` (sorted unique codes appended; returns their count):
+// a stack array of u32 codes instead of a vector of u64, no widening copy of the value.
+template <typename UT>
+static int qgram_codes32(const UT* u0, int n0, int q, int tokenizer, std::vector<uint64_t>& out) {
+  uint32_t stackbuf[256];
+  std::vector<uint32_t> heap;
+  const int n = n0 + (tokenizer == DK_QGRAM_ENDS ? 2 : 0);
+  const int m = n - q + 1;
+  if (m <= 0) return 0;
+  uint32_t* c = m <= 256 ? stackbuf : (heap.resize(m), heap.data());
+  auto unit = [&](int i) -> uint32_t {  // unit i of "^" + s + "$" (ENDS) or of s
+    if (tokenizer != DK_QGRAM_ENDS) return u0[i];
+    return i == 0 ? (uint32_t)'^' : i == n0 + 1 ? (uint32_t)'$' : (uint32_t)u0[i - 1];
+  };
+  if (q == 2) {
+    if (tokenizer == DK_QGRAM_ENDS) {
+      for (int ix = 0; ix < m; ++ix) c[ix] = (unit(ix) << 16) | unit(ix + 1);
+    } else {
+      for (int ix = 0; ix < m; ++ix) c[ix] = ((uint32_t)u0[ix] << 16) | (uint32_t)u0[ix + 1];
+    }
+  } else {
+    for (int ix = 0; ix < m; ++ix) c[ix] = unit(ix);
+  }
+  std::sort(c, c + m);
+  const size_t at = out.size();
+  out.resize(at + m);
+  uint64_t* o = out.data() + at;
+  int k = 0;
+  for (int i = 0; i < m; ++i)
+    if (i == 0 || c[i] != c[i - 1]) o[k++] = c[i];
+  out.resize(at + k);
+  return k;
+}
+
 // [Duke 1.2, recalled] utils.StringUtils.split — the maximal runs of non-' ' units — as
 // exact token ids (interned per property across batches), sorted with duplicates kept:
 // the token comparators count, per token of the shorter list, membership in the other.
@@ -485,6 +520,7 @@ struct dk_ctx {
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
   // k_score_grouped's execution order: task sort keys / values (double-buffered), chunk starts
   DevBuf task_key, task_val, task_cb, gprops;
+  DevBuf gram_tmp, gram_scratch;  // dk_upsert's device q-gram sets (dk_grams.hip)
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
   DevBuf ocounts, oqoff, owq, obase, ores, mcounts, mqoff, mbase, mres, bidx, bval;
@@ -799,7 +835,18 @@ struct ColStage {
   std::vector<uint16_t> gcnt;
   std::vector<uint64_t> grams;
   uint64_t units = 0;               // code units appended (padded)
+  // QGram sets built on the device (dk_grams.hip): per batch row its scratch run (values of
+  // more than 64 raw grams), the raw-gram total (the arena's growth bound), the runs' total
+  bool dev_grams = false;
+  std::vector<uint64_t> soff;
+  uint64_t rawtot = 0, longtot = 0;
 };
+
+// DK_DEV_GRAMS=0: QGram sets built on the host (qgram_codes) instead of the device (A/B)
+static bool dev_grams_enabled() {
+  const char* e = getenv("DK_DEV_GRAMS");
+  return !(e && e[0] == '0');
+}
 
 static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, ColStage& S) {
   PropState& P = c->P[pidx];
@@ -864,6 +911,28 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
     }
   });
   if (!is_num && !is_qg) return DK_OK;
+  if (is_qg && !is_tok && dev_grams_enabled()) {
+    // the sets are built on the device from the units (commit_column); here only their
+    // bounds: raw grams per value (an upper bound of its set), scratch runs of long values
+    const int q = P.cfg.qgram_q, ends = P.cfg.qgram_tokenizer == DK_QGRAM_ENDS ? 2 : 0;
+    S.dev_grams = true;
+    S.soff.assign(n, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+      if (S.len[i] == kMissing) continue;
+      const int64_t m = std::max<int64_t>(0, (int64_t)S.len[i] + ends - q + 1);
+      if (m >= (int64_t)kMissing)
+        return fail(DK_E_UNSUPPORTED, "property %d: row %llu has too many q-grams", pidx,
+                    (unsigned long long)i);
+      S.rawtot += (uint64_t)m;
+      if (m > 64) {
+        S.soff[i] = S.longtot;
+        S.longtot += (uint64_t)m;
+      }
+    }
+    if (P.grams_used + S.rawtot >= (1ull << 32))
+      return fail(DK_E_UNSUPPORTED, "property %d: over 4G q-gram codes", pidx);
+    return DK_OK;
+  }
   // numeric values / q-gram and token codes (per value, in row order).  Numeric parses and
   // q-gram sets run over row ranges on their own threads (serial staging was
   // most of a 1M-row linkage upsert); each range fills a gram buffer of its own, merged in
@@ -875,13 +944,34 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
   std::vector<std::vector<uint64_t>> pg(parts);
   std::vector<int> pmax(parts, 0);
   std::vector<uint64_t> pbad(parts, ~0ull);  // first row of a range with too many codes
+  const bool fast32 = is_qg && !is_tok && P.cfg.qgram_q <= 2 && P.cfg.qgram_tokenizer != DK_QGRAM_POSITIONAL;
   dk_run_parts(parts, [&](int t) {
     const uint64_t lo = n * t / parts, hi = n * (t + 1) / parts;
     std::vector<uint16_t> v16;
     std::vector<uint64_t> g;
     std::vector<uint64_t>& out = pg[t];
+    if (fast32) {  // at most L + 1 codes per value
+      uint64_t cap = 0;
+      for (uint64_t i = lo; i < hi; ++i)
+        if (S.len[i] != kMissing) cap += S.len[i] + 2;
+      out.reserve(cap);
+    }
     for (uint64_t i = lo; i < hi; ++i) {
       if (S.len[i] == kMissing) continue;
+      if (fast32 && !is_num) {
+        const uint64_t a = col->offsets[i], L = S.len[i];
+        const uint64_t at = out.size();
+        const int k = col->width == 1 ? qgram_codes32(u8 + a, (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, out)
+                                      : qgram_codes32(u16 + a, (int)L, P.cfg.qgram_q, P.cfg.qgram_tokenizer, out);
+        if (k >= (int)kMissing) {
+          pbad[t] = i;
+          return;
+        }
+        S.goff[i] = (uint32_t)at;
+        S.gcnt[i] = (uint16_t)k;
+        pmax[t] = std::max(pmax[t], k);
+        continue;
+      }
       const uint64_t a = col->offsets[i], L = S.len[i];
       v16.resize(L);
       if (col->width == 1) for (uint64_t k = 0; k < L; ++k) v16[k] = u8[a + k];
@@ -951,10 +1041,19 @@ static int reserve_column(dk_ctx* c, int pidx, const ColStage& S) {
     P.width = 2;  // same strings, wider units: the index content is unchanged
   }
   HIPCHK(P.units.reserve(used_b + S.bytes.size() + 512, used_b, s));
-  if (!S.grams.empty() || uses_codes(P.cfg.comparator))
+  if (S.dev_grams) {
+    HIPCHK(P.grams.reserve((P.grams_used + S.rawtot + 64) * 8, P.grams_used * 8, s));
+    const uint64_t n = S.len.size();
+    HIPCHK(c->gram_tmp.reserve(n * 16 + 64, 0, s));   // soff, gcnt32, gpos, maxg
+    HIPCHK(c->gram_scratch.reserve(S.longtot * 8 + 8, 0, s));
+  } else if (!S.grams.empty() || uses_codes(P.cfg.comparator)) {
     HIPCHK(P.grams.reserve((P.grams_used + S.grams.size() + 64) * 8, P.grams_used * 8, s));
+  }
   return DK_OK;
 }
+
+template <typename F>
+static hipError_t with_tmp(dk_ctx* c, F&& f);
 
 static int commit_column(dk_ctx* c, int pidx, ColStage& S, uint64_t n, uint64_t row0) {
   PropState& P = c->P[pidx];
@@ -983,6 +1082,44 @@ static int commit_column(dk_ctx* c, int pidx, ColStage& S, uint64_t n, uint64_t 
       HIPCHK(hipMemcpyAsync(P.grams.as<uint64_t>() + P.grams_used, S.grams.data(), S.grams.size() * 8,
                             hipMemcpyHostToDevice, s));
     P.grams_used += S.grams.size();
+  }
+  if (S.dev_grams && n) {
+    // the sets on the device: count pass, scan, write pass; then the arena's fill and the
+    // longest set are read back (the host needs both before the next batch / match)
+    uint64_t* d_soff = c->gram_tmp.as<uint64_t>();
+    uint32_t* d_cnt = reinterpret_cast<uint32_t*>(d_soff + n);
+    uint32_t* d_pos = d_cnt + n;
+    uint32_t* d_max = d_pos + n;
+    if (S.longtot) HIPCHK(hipMemcpyAsync(d_soff, S.soff.data(), n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_max, 0, 4, s));
+    GramJob J{};
+    J.units = P.units.p;
+    J.width = W;
+    J.q = P.cfg.qgram_q;
+    J.tokenizer = P.cfg.qgram_tokenizer;
+    J.off = P.off.as<uint32_t>();
+    J.len = P.len.as<uint16_t>();
+    J.row0 = row0;
+    J.n = n;
+    J.soff = d_soff;
+    J.scratch = c->gram_scratch.as<uint64_t>();
+    J.gcnt = P.gcnt.as<uint16_t>();
+    J.gcnt32 = d_cnt;
+    J.maxg = d_max;
+    J.gpos = d_pos;
+    J.gbase = (uint32_t)P.grams_used;
+    J.goff = P.goff.as<uint32_t>();
+    J.grams = P.grams.as<uint64_t>();
+    HIPCHK(launch_qgram_sets(J, false, s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) { return exclusive_scan_u32_dev(t, b, d_cnt, d_pos, n, s); }));
+    HIPCHK(launch_qgram_sets(J, true, s));
+    uint32_t* hs = c->h_small.as<uint32_t>();
+    HIPCHK(hipMemcpyAsync(hs, d_pos + n - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hs + 1, d_cnt + n - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hs + 2, d_max, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    P.grams_used += (uint64_t)hs[0] + hs[1];
+    P.maxgrams = std::max<int>(P.maxgrams, (int)hs[2]);
   }
   return DK_OK;
 }

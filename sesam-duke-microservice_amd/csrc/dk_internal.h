@@ -314,6 +314,28 @@ struct LuceneParams {
   uint64_t* real;           // += nhits
 };
 
+// The q-gram sets of a batch built on the device (dk_grams.hip): rows [row0, row0 + n) of a
+// QGram property whose units, off and len are in place.
+struct GramJob {
+  const void* units;
+  int32_t width, q, tokenizer;
+  const uint32_t* off;
+  const uint16_t* len;
+  uint64_t row0, n;
+  const uint64_t* soff;  // per batch row: its scratch run (values of more than 64 raw grams)
+  uint64_t* scratch;
+  uint16_t* gcnt;        // count pass: [row0 + i] = the set's size
+  uint32_t* gcnt32;      // count pass: [i] = the same (scanned into gpos)
+  uint32_t* maxg;        // count pass: atomicMax of the sizes
+  const uint32_t* gpos;  // write pass: [i] = exclusive prefix of the sizes
+  uint32_t gbase;        // write pass: the arena's fill before the batch
+  uint32_t* goff;        // write pass: [row0 + i] = gbase + gpos[i]
+  uint64_t* grams;       // write pass: the arena
+};
+hipError_t launch_qgram_sets(const GramJob& J, bool write, hipStream_t s);
+hipError_t exclusive_scan_u32_dev(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint32_t* out,
+                                  uint64_t n, hipStream_t s);
+
 // ---- launchers (dk_kernels.hip) ----
 // postings of rows that are in the index (kAlive): key kept, others set to ~0 (sorted last);
 // counts[0] += entries kept, counts[1] += rows in the index among [0, nrows)
