@@ -340,8 +340,10 @@ def main():
     from dukehip import dist as dshard
     t0 = time.time()
     shared_batch = None
+    t_synth = 0.0
     if dist is None:
         w = build_workload(args)
+        t_synth = time.time() - t0
         # records/sec deduped: the batch's host pack (strings -> SoA columns)
         # and dk_upsert, plus one dk_match of the batch (the step below)
         t_pack = time.perf_counter()
@@ -354,6 +356,7 @@ def main():
         meta, arrays, t_pack = [None], None, 0.0
         if rank == 0:
             w = build_workload(args)
+            t_synth = time.time() - t0
             t_pack = time.perf_counter()
             cols = [synth.column(w["values"][p["name"]]) for p in w["props"]]
             kcols = [synth.column(k) for k in w["keys"]]
@@ -380,7 +383,7 @@ def main():
                deleted=w.get("deleted"), key_columns=kcols)
     t_upsert = time.perf_counter() - t_up
     del cols, kcols
-    t_index = time.time() - t0
+    t_index = time.time() - t0 - t_synth   # shared-batch mapping + pack + upsert (no synthesis)
     # this rank's contiguous query tile: equal estimated cost (blocking's candidate counts,
     # identical on every rank's replica of the index), SURVEY §8e
     allq = w["queries"]
@@ -523,6 +526,13 @@ def main():
         pairs_launch = prof["pairs_scored"] / launches
         avg_launch_s = score_s / launches
         achieved = bpair * pairs_launch / avg_launch_s if avg_launch_s > 0 and bpair else 0.0
+        # a true lower bound of this schedule's bytes: every pair's CANDIDATE
+        # operands at their stored width (the kernel's own count, score_bytes) plus each
+        # query's operands once -- B_pair above charges the query side to every pair, which a
+        # kernel holding the query in LDS / registers does not read, so its fraction can pass 1
+        qbytes = sum(d["bytes"] / 2.0 for d in bdetail.values()) if bdetail else 0.0
+        bound_launch = (prof["score_bytes"] + qbytes * len(queries) * args.steps) / launches
+        frac_bound = bound_launch / avg_launch_s / HBM_PEAK if avg_launch_s > 0 else None
         # the kernel's own operand bytes (the query side LDS-resident, the symmetric schedule's
         # candidate operands read once per pair): what the schedule actually has to move
         sched = prof["score_bytes"] / score_s if score_s > 0 else 0.0
@@ -591,9 +601,13 @@ def main():
                                  else sum(c[0] for c in holder["counts"]) if "counts" in holder
                                  else int(last.n) if last is not None else 0),
             "index_build_s": t_index,
+            "synth_s": t_synth,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "frac_s8d": achieved / HBM_PEAK,
+                         "frac_bound": frac_bound,
+                         "bound_bytes_per_launch": bound_launch,
+                         "query_bytes_per_query": qbytes,
                          "traffic": traffic,
                          "kernel": "k_score", "launches": prof["score_launches"],
                          "avg_launch_ms": prof["ms_score"] / launches,

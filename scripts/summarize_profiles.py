@@ -7,9 +7,10 @@ Writes OUT_DIR/kernel_stats.csv (copy of rocprofv3's stats), OUT_DIR/pmc_k_score
 profiles/pmc_k_score.json (read by bench.py for roofline.traffic).
 
 HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
-KiB, and on gfx950 FETCH_SIZE reads exactly half the bytes of a wide coalesced stream, so
-the read side is doubled (an upper bound for the k_score access mix, whose candidate-replica
-reads are 4-byte words coalesced across a wave).
+KiB, and on gfx950 FETCH_SIZE reads exactly half the bytes of a coalesced row read -- the
+guide calibrates 16 B per lane; scripts/micro/fetch_calib.hip calibrates the scoring kernels'
+own widths (4- and 8-B-per-lane row reads: factor 2.000, profiles/r04/fetch_calib.json) --
+so the read side is doubled.
 """
 import collections
 import csv
@@ -38,7 +39,7 @@ def main():
     if stats:
         shutil.copy(stats[0], os.path.join(out, "kernel_stats.csv"))
     res = {}
-    for name in ("valu", "fetch", "write", "stall"):
+    for name in ("valu", "fetch", "write", "stall", "l2"):
         agg, n = pmc(os.path.join(pmcdir, name))
         res[name] = (dict(agg), n)
     fetch_kb, n = res["fetch"][0].get("FETCH_SIZE", 0.0), max(1, res["fetch"][1])
@@ -70,6 +71,9 @@ def main():
         "pairs_profiled": pairs,
         "hbm_bytes_per_pair": (2.0 * fetch_kb + write_kb) * 1024.0 / pairs if pairs else None,
         "valu_insts_per_wave": v.get("SQ_INSTS_VALU", 0) / max(1.0, v.get("SQ_WAVES", 1)),
+        # per 64 scored pairs (a wave of k_score, a quarter task of k_score_grouped)
+        "valu_insts_per_64_pairs": v.get("SQ_INSTS_VALU", 0) * 64.0 / pairs if pairs else None,
+        "fetch_calibration": "profiles/r04/fetch_calib.json (4/8/16 B per lane: x2.000)",
         "valu_thread_utilization": v.get("SQ_THREAD_CYCLES_VALU", 0) /
                                    max(1.0, v.get("SQ_ACTIVE_INST_VALU", 1) * 64),
         "wait_any_frac": s.get("SQ_WAIT_ANY", 0) / max(1.0, s.get("SQ_WAVE_CYCLES", 1)),
