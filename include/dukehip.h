@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DK_ABI_VERSION 6
+#define DK_ABI_VERSION 7
 
 /* status codes */
 #define DK_OK 0
@@ -109,6 +109,8 @@ typedef struct dk_lucene {
   float min_relevance;        /* setMinRelevance */
 } dk_lucene;
 
+#define DK_MAX_ORDER_CLASSES 4
+
 typedef struct dk_schema {
   int32_t nprops;           /* scored properties, in Processor.compare iteration order */
   const dk_property* props;
@@ -118,6 +120,16 @@ typedef struct dk_schema {
   int32_t nkeys;            /* key functions (blocking); ignored in ALLPAIRS mode; <= 8 */
   const dk_lucene* lucene;  /* non-NULL: Lucene-compatible candidates instead of key
                                functions (nkeys 0; DEDUP or LINKAGE) */
+  /* Processor.compare visits r1's properties in its RecordImpl HashMap's iteration order,
+   * which depends on the map's capacity -- 16 up to 12 keys, 32 up to 24, 64 up to 48 --
+   * i.e. on how many properties the record holds values for (IncrementalDataSource.java:
+   * 67-98 adds its columns' values and the synthetic ID / dukeOriginalEntityId /
+   * dukeDatasetId / dukeGroupNo / dukeDeleted).  norders <= DK_MAX_ORDER_CLASSES order
+   * classes: orders[c * nprops + k] = the k-th property visited for a query record of class
+   * c (a permutation of 0..nprops-1; a record's missing properties are skipped).  norders 0
+   * = one class, the props' own order.  The batch gives each record's class. */
+  int32_t norders;
+  const int32_t* orders;
 } dk_schema;
 
 /* One property's values for the n records of a batch. */
@@ -138,6 +150,7 @@ typedef struct dk_batch {
    * string) or key_columns (nkeys strings per record, interned exactly by the library) */
   const uint64_t* keys;
   const dk_column* key_columns;
+  const uint8_t* order_class; /* n: the record's order class (dk_schema.orders); NULL = 0 */
 } dk_batch;
 
 /* dk_match flags */

@@ -25,6 +25,7 @@ public final class DukeHip {
     public static final int MODE_DEDUP = 0, MODE_LINKAGE = 1, MODE_ALLPAIRS = 2;
     public static final int KIND_MATCH = 1, KIND_MAYBE = 2;
     public static final int E_INVALID = -1, E_UNSUPPORTED = -2, E_NOMEM = -3, E_DEVICE = -4, E_STATE = -5;
+    public static final int MAX_ORDER_CLASSES = 4;                                 // DK_MAX_ORDER_CLASSES
     public static final int CLEAN_NONE = 0, CLEAN_LOWERCASE_NORMALIZE = 1, CLEAN_COUNTRY_NAME = 2,
             CLEAN_CAPITAL = 3;
     public static final int LINK_INFERRED = 1, LINK_RETRACTED = 2, LINK_SAME = 1, LINK_MAYBE = 2;
@@ -44,7 +45,7 @@ public final class DukeHip {
                                      double[] low, double[] high, double[] minRatio,
                                      double threshold, double maybeThreshold, int mode, int nkeys,
                                      int[] lookupProps, int maxSearchHits, float minRelevance,
-                                     int[] devices);
+                                     int[] devices, int[] orders);   // orders: dk_schema.orders or null
 
     public static native void destroy(long ctx);                                    // dk_destroy
 
@@ -59,7 +60,7 @@ public final class DukeHip {
      */
     public static native int[] upsert(long ctx, boolean transient, int n, long[] ident, byte[] group,
                                       byte[] deleted, int[][] offsets, char[][] units, byte[][] present,
-                                      int[][] keyOffsets, char[][] keyUnits);
+                                      int[][] keyOffsets, char[][] keyUnits, byte[] orderClass);
 
     public static native void dropTransient(long ctx);                              // dk_drop_transient
 

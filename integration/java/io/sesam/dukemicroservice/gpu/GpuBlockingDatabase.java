@@ -45,6 +45,7 @@ public class GpuBlockingDatabase implements Database {
     private boolean overwrite;
     private int transientRow0 = -1;
     private Configuration config;
+    private int[] caps = {16};                     // HashMap capacities -> order classes
 
     /**
      * @param scoredProps  the scored properties in Processor.compare's iteration order
@@ -56,8 +57,16 @@ public class GpuBlockingDatabase implements Database {
      */
     public GpuBlockingDatabase(Configuration config, List<Property> scoredProps,
                                List<KeyFunction> keyFunctions, boolean linkage, int[] devices) {
+        this(config, new OrderClasses(scoredProps), keyFunctions, linkage, devices);
+    }
+
+    /** The same with the pipeline's Processor.compare order classes (orderClasses). */
+    public GpuBlockingDatabase(Configuration config, OrderClasses oc,
+                               List<KeyFunction> keyFunctions, boolean linkage, int[] devices) {
         this.config = config;
+        List<Property> scoredProps = oc.props;
         this.props = scoredProps;
+        this.caps = oc.caps;
         this.keyFunctions = keyFunctions;
         this.linkage = linkage;
         this.idProp = config.getIdentityProperties().iterator().next().getName();
@@ -95,7 +104,8 @@ public class GpuBlockingDatabase implements Database {
         this.ctx = DukeHip.create(cmp, q, formula, tok, low, high, minRatio, config.getThreshold(),
                                   config.getMaybeThreshold(), linkage ? DukeHip.MODE_LINKAGE : DukeHip.MODE_DEDUP,
                                   keyFunctions.size(), lookup, maxHits, minRelevance,
-                                  devices == null || devices.length == 0 ? new int[] {0} : devices);
+                                  devices == null || devices.length == 0 ? new int[] {0} : devices,
+                                  oc.flatOrders());
         if (opts != null && opts.unmergedStats) DukeHip.luceneSetStats(ctx, DukeHip.LUCENE_STATS_UNMERGED);
     }
 
@@ -109,21 +119,92 @@ public class GpuBlockingDatabase implements Database {
      * Processor.compare iterates r1.getProperties(): RecordImpl's HashMap key order.  The keys a
      * data source's RecordBuilder inserts -- its columns' properties in column order, then
      * dukeGroupNo (linkage), ID, dukeOriginalEntityId, dukeDatasetId, dukeDeleted
-     * (IncrementalDataSource.java:67-98) -- put into a HashMap the same way give that order;
-     * at most 12 keys keep the table at 16 buckets, so a record missing some values iterates
-     * the rest in the same relative order.  Returns the scored properties in it.
+     * (IncrementalDataSource.java:67-98) -- put into a HashMap of the record's capacity give that
+     * order; a record missing some values iterates the rest in the same relative order.  The
+     * capacity follows the number of keys the record holds (16 up to 12, 32 up to 24, 64 up to
+     * 48), so a pipeline whose records can hold more than 12 has several order classes, and
+     * each record's class is its capacity's (dk_schema.orders, dk_batch.order_class).
      */
-    public static List<Property> comparisonOrder(Configuration config, List<String> recordKeys) {
-        if (recordKeys.size() > 12)
-            throw new IllegalArgumentException("more than 12 record properties: HashMap order varies");
-        Map<String, Boolean> m = new HashMap<>();
-        for (String k : recordKeys) m.put(k, Boolean.TRUE);
-        List<Property> out = new ArrayList<>();
-        for (String k : m.keySet()) {
-            Property p = config.getPropertyByName(k);
-            if (p != null && !p.isIdProperty() && !p.isIgnoreProperty()) out.add(p);
+    public static final class OrderClasses {
+        final List<Property> props;   // class 0's order: the schema's property order
+        final int[] caps;             // ascending capacities, one per class
+        final int[][] orders;         // orders[c][k] = index into props of class c's k-th
+
+        OrderClasses(List<Property> props) {
+            this.props = props;
+            this.caps = new int[] {16};
+            int[] id = new int[props.size()];
+            for (int i = 0; i < id.length; i++) id[i] = i;
+            this.orders = new int[][] {id};
         }
-        return out;
+
+        OrderClasses(List<Property> props, int[] caps, int[][] orders) {
+            this.props = props;
+            this.caps = caps;
+            this.orders = orders;
+        }
+
+        /** dk_schema.orders (class-major), or null for one class. */
+        int[] flatOrders() {
+            if (orders.length <= 1) return null;
+            int n = props.size();
+            int[] f = new int[orders.length * n];
+            for (int c = 0; c < orders.length; c++) System.arraycopy(orders[c], 0, f, c * n, n);
+            return f;
+        }
+
+        /** the order class of a record holding `keys` properties */
+        int classOf(int keys) {
+            int cap = 16;
+            while (keys > cap * 3 / 4) cap *= 2;
+            for (int c = 0; c < caps.length; c++) if (caps[c] == cap) return c;
+            throw new DukeHipException(DukeHip.E_UNSUPPORTED, "record of " + keys + " properties");
+        }
+    }
+
+    /**
+     * The order classes of a data source's records: `recordKeys` = every key its records can
+     * hold in insertion order (columns' properties, then the synthetic ones incl. dukeDeleted),
+     * `minKeys` / `maxKeys` = the fewest / most a record holds (the synthetic ones / all).
+     */
+    public static OrderClasses orderClasses(Configuration config, List<String> recordKeys, int minKeys, int maxKeys) {
+        if (maxKeys > 48)
+            throw new IllegalArgumentException("more than 48 record properties: HashMap capacity past 64");
+        List<Integer> capList = new ArrayList<>();
+        for (int k = minKeys; k <= maxKeys; k++) {
+            int cap = 16;
+            while (k > cap * 3 / 4) cap *= 2;
+            if (!capList.contains(cap)) capList.add(cap);
+        }
+        if (capList.size() > DukeHip.MAX_ORDER_CLASSES)
+            throw new IllegalArgumentException("too many HashMap order classes");
+        List<List<Property>> byClass = new ArrayList<>();
+        for (int cap : capList) {
+            // a table of exactly `cap` buckets that never resizes (load factor 100), holding
+            // every key a record can have: a record's own keys iterate in this relative order
+            Map<String, Boolean> m = new HashMap<>(cap, 100f);
+            for (String k : recordKeys) m.put(k, Boolean.TRUE);
+            List<Property> out = new ArrayList<>();
+            for (String k : m.keySet()) {
+                Property p = config.getPropertyByName(k);
+                if (p != null && !p.isIdProperty() && !p.isIgnoreProperty()) out.add(p);
+            }
+            byClass.add(out);
+        }
+        List<Property> props = byClass.get(0);
+        int[] caps = new int[capList.size()];
+        int[][] orders = new int[capList.size()][];
+        for (int c = 0; c < caps.length; c++) {
+            caps[c] = capList.get(c);
+            orders[c] = new int[props.size()];
+            for (int k = 0; k < props.size(); k++) orders[c][k] = props.indexOf(byClass.get(c).get(k));
+        }
+        return new OrderClasses(props, caps, orders);
+    }
+
+    /** Pipelines whose records hold at most 12 properties: the one order. */
+    public static List<Property> comparisonOrder(Configuration config, List<String> recordKeys) {
+        return orderClasses(config, recordKeys, recordKeys.size(), recordKeys.size()).props;
     }
 
     long ctx() { return ctx; }
@@ -286,9 +367,15 @@ public class GpuBlockingDatabase implements Database {
             keyOffsets[k] = new int[n + 1];
             keyUnits[k] = arena(keys, keyOffsets[k], null);
         }
+        byte[] orderClass = null;
+        if (caps.length > 1) {   // Processor.compare follows each query record's HashMap order
+            OrderClasses oc = new OrderClasses(props, caps, null);
+            orderClass = new byte[n];
+            for (int i = 0; i < n; i++) orderClass[i] = (byte) oc.classOf(batch.get(i).getProperties().size());
+        }
         int[] prev = asTransient ? new int[0] : previousRows(ident);
         int[] assigned = DukeHip.upsert(ctx, asTransient, n, ident, group, deleted, offsets, units,
-                                        present, keyOffsets, keyUnits);
+                                        present, keyOffsets, keyUnits, orderClass);
         if (asTransient && transientRow0 < 0) transientRow0 = rows.size();
         rows.appendRecords(batch);
         afterUpsert(ident, prev, assigned, asTransient);
@@ -301,6 +388,8 @@ public class GpuBlockingDatabase implements Database {
      * when the native reader declines the body (the caller then takes the Record path).
      */
     int[] indexJson(byte[] body, JsonSource src, boolean asTransient) {
+        if (caps.length > 1)   // the native packer does not count a record's properties
+            throw new DukeHipException(DukeHip.E_UNSUPPORTED, "several HashMap order classes");
         long packed = DukeHip.packJson(ids, body, src.datasetId, src.groupNo, src.columnNames,
                                        src.columnProp, src.columnCleaner, props.size(), src.keyParts);
         int n = DukeHip.packedSize(packed);

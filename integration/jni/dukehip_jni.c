@@ -52,9 +52,14 @@ JNIEXPORT jlong JFN(create)(JNIEnv* env, jclass cls, jintArray cmp, jintArray q,
                             jintArray tok, jdoubleArray low, jdoubleArray high, jdoubleArray minRatio,
                             jdouble threshold, jdouble maybe, jint mode, jint nkeys,
                             jintArray lookupProps, jint maxSearchHits, jfloat minRelevance,
-                            jintArray devices) {
+                            jintArray devices, jintArray orders) {
   (void)cls;
   const jsize n = (*env)->GetArrayLength(env, cmp);
+  const jsize no = orders ? (*env)->GetArrayLength(env, orders) : 0;
+  if (no % (n ? n : 1) != 0 || no > DK_MAX_ORDER_CLASSES * 16) {
+    throw_msg(env, "orders must hold norders x nprops entries (norders <= DK_MAX_ORDER_CLASSES)");
+    return 0;
+  }
   const jsize nl = lookupProps ? (*env)->GetArrayLength(env, lookupProps) : 0;
   const jsize nd = devices ? (*env)->GetArrayLength(env, devices) : 0;
   if (n > 16 || nl > 16 || nd > 64) {
@@ -90,6 +95,12 @@ JNIEXPORT jlong JFN(create)(JNIEnv* env, jclass cls, jintArray cmp, jintArray q,
   s.maybe_threshold = maybe;
   s.mode = mode;
   s.nkeys = nkeys;
+  int32_t ord[DK_MAX_ORDER_CLASSES * 16];
+  if (no) {  /* Processor.compare's HashMap order classes */
+    (*env)->GetIntArrayRegion(env, orders, 0, no, (jint*)ord);
+    s.norders = (int32_t)(no / (n ? n : 1));
+    s.orders = ord;
+  }
   int32_t lookup[16];
   dk_lucene luc;
   if (lookupProps) {  /* IncrementalLuceneDatabase semantics on the device */
@@ -165,9 +176,13 @@ static jintArray rows_array(JNIEnv* env, const uint32_t* rows, uint64_t n) {
 JNIEXPORT jintArray JFN(upsert)(JNIEnv* env, jclass cls, jlong ctx, jboolean transient_, jint n,
                                 jlongArray ident, jbyteArray group, jbyteArray deleted,
                                 jobjectArray offsets, jobjectArray units, jobjectArray present,
-                                jobjectArray keyOffsets, jobjectArray keyUnits) {
+                                jobjectArray keyOffsets, jobjectArray keyUnits, jbyteArray orderClass) {
   (void)cls;
   const jsize np = (*env)->GetArrayLength(env, offsets);
+  if (orderClass && (*env)->GetArrayLength(env, orderClass) != n) {
+    throw_msg(env, "orderClass must hold one class per record");
+    return NULL;
+  }
   const jsize nk = keyOffsets ? (*env)->GetArrayLength(env, keyOffsets) : 0;
   if (np > 16 || nk > 8) {
     throw_msg(env, "too many properties / key functions");
@@ -185,6 +200,7 @@ JNIEXPORT jintArray JFN(upsert)(JNIEnv* env, jclass cls, jlong ctx, jboolean tra
   jlong* id = (*env)->GetLongArrayElements(env, ident, NULL);
   jbyte* g = group ? (*env)->GetByteArrayElements(env, group, NULL) : NULL;
   jbyte* d = deleted ? (*env)->GetByteArrayElements(env, deleted, NULL) : NULL;
+  jbyte* oc = orderClass ? (*env)->GetByteArrayElements(env, orderClass, NULL) : NULL;
   dk_batch b;
   memset(&b, 0, sizeof b);
   b.n = (uint64_t)n;
@@ -193,8 +209,10 @@ JNIEXPORT jintArray JFN(upsert)(JNIEnv* env, jclass cls, jlong ctx, jboolean tra
   b.deleted = (const uint8_t*)d;
   b.columns = cols;
   b.key_columns = nk ? kcols : NULL;
+  b.order_class = (const uint8_t*)oc;
   uint32_t* rows = (uint32_t*)malloc((size_t)n * 4 + 4);
   const int rc = transient_ ? dk_upsert_transient(CTX(ctx), &b, rows) : dk_upsert(CTX(ctx), &b, rows);
+  if (oc) (*env)->ReleaseByteArrayElements(env, orderClass, oc, JNI_ABORT);
   for (jsize p = 0; p < np; ++p) unpin_column(env, &pc[p]);
   for (jsize k = 0; k < nk; ++k) unpin_column(env, &pk[k]);
   (*env)->ReleaseLongArrayElements(env, ident, id, JNI_ABORT);

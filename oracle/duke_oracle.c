@@ -413,14 +413,18 @@ double dko_property_compare(const dko_prop* p, const uint16_t* s1, int n1,
   return ((p->high - 0.5) * (sim * sim)) + 0.5;
 }
 
-/* [Duke 1.2] Processor.compare(r1, r2): prob = 0.5; per property of r1 (in the schema's
- * iteration order; ID / ignored properties are not in the schema, App.java:309-323):
- * skip if either side has no value; high = 0.0, raised by Math.max with
- * PropertyImpl.compare over the non-empty value pairs (a record holds <= 1 value per
- * property, IncrementalDataSource.java:69-72); prob = computeBayes(prob, high). */
+/* [Duke 1.2] Processor.compare(r1, r2): prob = 0.5; per property of r1 (in r1's RecordImpl
+ * HashMap iteration order: the schema's order, or with order classes the one of r1's class,
+ * which follows the map's capacity, IncrementalDataSource.java:67-98; ID / ignored
+ * properties are not in the schema, App.java:309-323): skip if either side has no value;
+ * high = 0.0, raised by Math.max with PropertyImpl.compare over the non-empty value pairs
+ * (a record holds <= 1 value per property, IncrementalDataSource.java:69-72);
+ * prob = computeBayes(prob, high). */
 double dko_compare_rows(const dko_schema* s, const dko_table* t, uint32_t a, uint32_t b) {
   double prob = 0.5;
-  for (int p = 0; p < s->nprops; p++) {
+  const int oc = s->norders > 1 && t->oclass ? t->oclass[a] : 0;
+  for (int k = 0; k < s->nprops; k++) {
+    const int p = s->norders > 0 ? s->orders[oc * s->nprops + k] : k;
     if (!t->present[p][a] || !t->present[p][b]) continue;
     const uint32_t* off = t->off[p];
     const uint16_t* ch = t->chars[p];

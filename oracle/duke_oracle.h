@@ -75,6 +75,8 @@ typedef struct dko_schema {
   double maybe_threshold;
   int mode;                    /* DKO_MODE_* */
   int nkeys;                   /* key functions (blocking); 0 in ALLPAIRS mode */
+  int norders;                 /* order classes (0: one, the props' order) */
+  const int* orders;           /* norders x nprops: class c visits orders[c * nprops + k] */
 } dko_schema;
 
 /* Column-packed records.  Every array has n entries unless noted.
@@ -93,6 +95,7 @@ typedef struct dko_table {
   const uint8_t* const* present;
   const uint32_t* const* key_off;
   const uint16_t* const* key_chars;
+  const uint8_t* oclass;       /* per row: its order class (NULL: 0) */
 } dko_table;
 
 /* [Duke 1.2] Processor.compare(r1, r2) over rows a (r1) and b (r2) */

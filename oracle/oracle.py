@@ -27,7 +27,8 @@ class Prop(C.Structure):
 
 class Schema(C.Structure):
     _fields_ = [("nprops", C.c_int), ("props", C.POINTER(Prop)), ("threshold", C.c_double),
-                ("maybe_threshold", C.c_double), ("mode", C.c_int), ("nkeys", C.c_int)]
+                ("maybe_threshold", C.c_double), ("mode", C.c_int), ("nkeys", C.c_int),
+                ("norders", C.c_int), ("orders", C.POINTER(C.c_int))]
 
 
 class Table(C.Structure):
@@ -35,7 +36,7 @@ class Table(C.Structure):
                 ("deleted", C.c_void_p), ("alive", C.c_void_p),
                 ("off", C.POINTER(C.c_void_p)), ("chars", C.POINTER(C.c_void_p)),
                 ("present", C.POINTER(C.c_void_p)), ("key_off", C.POINTER(C.c_void_p)),
-                ("key_chars", C.POINTER(C.c_void_p))]
+                ("key_chars", C.POINTER(C.c_void_p)), ("oclass", C.c_void_p)]
 
 
 class Result(C.Structure):
@@ -164,7 +165,9 @@ class OracleTable:
     a str.  All strings stored as UTF-16 code units."""
 
     def __init__(self, props, values, keys=(), ident=None, group=None, deleted=None,
-                 alive=None, threshold=0.9, maybe=0.0, mode="dedup"):
+                 alive=None, threshold=0.9, maybe=0.0, mode="dedup", orders=None, oclass=None):
+        """orders: per order class the visiting order of the props (indices); oclass: per
+        record its class (Processor.compare follows the query record's HashMap order)."""
         n = len(values[0]) if values else len(keys[0])
         self.n = n
         self._keep = []
@@ -174,6 +177,11 @@ class OracleTable:
                                  pr.get("formula", 0), pr.get("tokenizer", 0),
                                  pr.get("min_ratio", 0.0))
         self.schema = Schema(len(props), self.props, threshold, maybe, MODE[mode], len(keys))
+        if orders:
+            flat = (C.c_int * (len(orders) * len(props)))(*[int(x) for o in orders for x in o])
+            self._orders = flat
+            self.schema.norders = len(orders)
+            self.schema.orders = flat
 
         def pack(col):
             if all(v is not None for v in col):
@@ -227,7 +235,7 @@ class OracleTable:
         ident = np.arange(n, dtype=np.uint64) if ident is None else ident
         self.table = Table(n, arr(ident, np.uint64), arr(group, np.uint8), arr(deleted, np.uint8),
                            arr(alive, np.uint8), self.off, self.chars, self.present,
-                           self.key_off, self.key_chars)
+                           self.key_off, self.key_chars, arr(oclass, np.uint8))
 
     def compare_rows(self, a, b):
         return lib().dko_compare_rows(C.byref(self.schema), C.byref(self.table), a, b)

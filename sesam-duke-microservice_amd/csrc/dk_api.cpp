@@ -482,6 +482,8 @@ struct dk_ctx {
   hipEvent_t chunk_done = nullptr;
   uint64_t nrows = 0, cap = 0;
   DevBuf ident, flags, group;
+  DevBuf oclass;                 // per row: Processor.compare order class (dk_schema.orders)
+  std::vector<int32_t> orders;   // norders x nprops (empty: one class, the props' order)
   DevBuf keys[kMaxKeys];
   IdentMap ident_row;
   std::vector<U16Table> intern;  // key strings per key function (key style 2)
@@ -580,6 +582,7 @@ static hipError_t grow_rows(dk_ctx* c, uint64_t need) {
   GROW(c->ident, uint64_t);
   GROW(c->flags, uint8_t);
   GROW(c->group, uint8_t);
+  GROW(c->oclass, uint8_t);
   for (int k = 0; k < c->schema.nkeys; ++k) GROW(c->keys[k], uint64_t);
   if (c->luc.on) {
     const uint64_t nf = c->luc.fields.size();
@@ -629,6 +632,18 @@ static int validate_schema(const dk_schema* s) {
                   "limit adaptively, EstimateResultTracker)", L.max_hits, kLuceneMaxHits);
   } else if (s->mode != DK_MODE_ALLPAIRS && (s->nkeys < 1 || s->nkeys > kMaxKeys)) {
     return fail(DK_E_INVALID, "nkeys %d out of range [1, %d]", s->nkeys, kMaxKeys);
+  }
+  if (s->norders < 0 || s->norders > kMaxOrders)
+    return fail(DK_E_UNSUPPORTED, "norders %d out of range [0, %d]", s->norders, kMaxOrders);
+  if (s->norders > 0 && !s->orders) return fail(DK_E_INVALID, "orders is NULL");
+  for (int o = 0; o < s->norders; ++o) {
+    uint32_t seen = 0;
+    for (int k = 0; k < s->nprops; ++k) {
+      const int32_t v = s->orders[o * s->nprops + k];
+      if (v < 0 || v >= s->nprops || (seen >> v) & 1u)
+        return fail(DK_E_INVALID, "orders[%d] is not a permutation of the properties", o);
+      seen |= 1u << v;
+    }
   }
   for (int i = 0; i < s->nprops; ++i) {
     const dk_property& p = s->props[i];
@@ -687,6 +702,9 @@ static int create_impl(const dk_schema* schema, int device, dk_ctx** out) {
   c->schema = *schema;
   c->schema.props = nullptr;
   c->schema.lucene = nullptr;
+  c->schema.orders = nullptr;
+  if (schema->norders > 0)
+    c->orders.assign(schema->orders, schema->orders + (size_t)schema->norders * schema->nprops);
   if (schema->lucene) {
     c->luc.on = true;
     c->luc.fields.assign(schema->lucene->lookup_prop, schema->lucene->lookup_prop + schema->lucene->nlookup);
@@ -1274,6 +1292,13 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
         return fail(DK_E_INVALID, "record %llu: dukeGroupNo %u (1 or 2 in LINKAGE mode)",
                     (unsigned long long)i, (unsigned)b->group[i]);
   }
+  if (b->order_class) {
+    const uint32_t no = c->orders.empty() ? 1u : (uint32_t)(c->orders.size() / std::max(1, c->schema.nprops));
+    for (uint64_t i = 0; i < n; ++i)
+      if (b->order_class[i] >= no)
+        return fail(DK_E_INVALID, "record %llu: order class %u (the schema has %u)",
+                    (unsigned long long)i, (unsigned)b->order_class[i], no);
+  }
   const int nk = c->schema.nkeys;
   int style = 0;
   if (nk > 0) {
@@ -1399,6 +1424,10 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     HIPCHK(hipMemcpyAsync(c->group.as<uint8_t>() + row0, b->group, n, hipMemcpyHostToDevice, s));
   else
     HIPCHK(hipMemsetAsync(c->group.as<uint8_t>() + row0, 0, n, s));
+  if (b->order_class)
+    HIPCHK(hipMemcpyAsync(c->oclass.as<uint8_t>() + row0, b->order_class, n, hipMemcpyHostToDevice, s));
+  else
+    HIPCHK(hipMemsetAsync(c->oclass.as<uint8_t>() + row0, 0, n, s));
   // the arena fill marks are restored if a device step below fails (Rollback)
   for (auto& p : c->P) rollback.marks.push_back({p.units_used, p.grams_used, p.maxlen, p.maxgrams, p.width});
   for (int p = 0; p < c->schema.nprops; ++p) {
@@ -1602,6 +1631,11 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
   P.long_rows = 0;
   P.raw_prop = -1;
   P.has_dp = 0;
+  P.norders = c->orders.empty() ? 1 : (int32_t)(c->orders.size() / std::max(1, P.nprops));
+  for (int o = 0; o < P.norders; ++o)
+    for (int k = 0; k < P.nprops; ++k)
+      P.order[o][k] = (uint8_t)(c->orders.empty() ? k : c->orders[(size_t)o * P.nprops + k]);
+  P.oclass = c->oclass.as<uint8_t>();
   for (const auto& S : c->P) {
     const int op = S.cfg.comparator;
     if (op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER || op == DK_CMP_WEIGHTED_LEVENSHTEIN) P.has_dp = 1;
@@ -2070,7 +2104,8 @@ static bool sym_enabled() {
 // WeightedLevenshtein's stride aliasing and the token comparators' "shorter list first"
 // are orientation dependent; the long-value kernels are not instantiated for it.
 static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
-  if (c->schema.mode != DK_MODE_DEDUP || P.long_rows > 0) return false;
+  // several order classes: compare(candidate, query) would follow the candidate's order
+  if (c->schema.mode != DK_MODE_DEDUP || P.long_rows > 0 || P.norders > 1) return false;
   for (const auto& S : c->P) {
     const int op = S.cfg.comparator;
     if (op == DK_CMP_WEIGHTED_LEVENSHTEIN || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS)
@@ -2105,10 +2140,12 @@ static bool grouped_schema_ok(const ScoreParams& P) {
 static std::vector<GroupedProp> grouped_props(const ScoreParams& P) {
   std::vector<GroupedProp> gp(P.nprops);
   const uint64_t n = P.rstride;
+  uint32_t ts = 0;
   for (int p = 0; p < P.nprops; ++p) {
     const DevProp& D = P.props[p];
     GroupedProp& G = gp[p];
     memset(&G, 0, sizeof G);
+    if (D.op == DK_CMP_QGRAM) G.tslot = ts++;
     G.len = D.rlen;
     G.len_n = (uint32_t)(n * 2);
     G.x = G.w = D.rlen;  // size 0 below unless the comparator has them
@@ -2916,6 +2953,7 @@ static int compare_values_impl(dk_ctx* c, const dk_batch* pair, double* prob) {
     for (size_t i = 0; i < c->P.size(); ++i) props[i] = c->P[i].cfg;
     dk_schema sc = c->schema;
     sc.props = props.data();
+    sc.orders = c->orders.empty() ? nullptr : c->orders.data();
     sc.mode = DK_MODE_ALLPAIRS;
     sc.nkeys = 0;
     int rc = dk_create(&sc, c->device, &c->pair_ctx);

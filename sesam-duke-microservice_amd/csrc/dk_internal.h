@@ -10,6 +10,7 @@
 namespace dk {
 
 constexpr int kMaxProps = 16;
+constexpr int kMaxOrders = DK_MAX_ORDER_CLASSES;  // Processor.compare visiting orders (dk_schema)
 constexpr int kMaxKeys = 8;
 constexpr int kMaxSegs = 2 * kMaxKeys;  // per key function: sorted base + sorted delta
 constexpr uint16_t kMissing = 0xFFFF;  // length sentinel: record has no value
@@ -121,6 +122,11 @@ struct ScoreParams {
   const uint64_t* ident;
   const uint32_t* rowof;  // replica position -> row
   uint64_t rstride;       // replica positions (K * M)
+  // Processor.compare's visiting order of a query row: order[oclass[q]][k] = the k-th
+  // property (dk_schema.orders); norders 1: order[0] is the identity
+  int32_t norders;
+  uint8_t order[kMaxOrders][kMaxProps];
+  const uint8_t* oclass;  // per row: its order class (norders > 1)
   DevProp props[kMaxProps];
 };
 
@@ -187,7 +193,8 @@ struct GroupedProp {
   uint32_t rowb;      // bytes between key-word rows (QGram); 0x80000000 (Numeric: rows >= 1
                       // are out of range)
   uint32_t xsh;       // x element = 1 << xsh bytes
-  uint32_t pad[5];
+  uint32_t tslot;     // QGram: the query table of this property (rank among the QGram ones)
+  uint32_t pad[4];
 };
 static_assert(sizeof(GroupedProp) == 64, "two s_load_dwordx8");
 

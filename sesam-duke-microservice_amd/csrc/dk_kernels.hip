@@ -1250,13 +1250,17 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   };
   int lq_n = 0, lc_n = (int)kMissing;
   uint32_t qch_n = 0u;
-  if (P.nprops > 0) prefetch(0, lq_n, qch_n, lc_n);
+  // Processor.compare visits r1's (the query's) properties in its RecordImpl HashMap order,
+  // which depends on the map's capacity: the query row's order class (dk_schema.orders)
+  const int oc = P.norders > 1 ? (int)__builtin_amdgcn_readfirstlane((uint32_t)P.oclass[q]) : 0;
+  if (P.nprops > 0) prefetch(P.order[oc][0], lq_n, qch_n, lc_n);
   for (int p = 0; p < P.nprops; ++p) {
-    const DevProp& D = P.props[p];
+    const int pp = P.order[oc][p];
+    const DevProp& D = P.props[pp];
     const int lq = lq_n;
     const int lc = lc_n;
     const uint32_t qch = qch_n;
-    if (p + 1 < P.nprops) prefetch(p + 1, lq_n, qch_n, lc_n);
+    if (p + 1 < P.nprops) prefetch(P.order[oc][p + 1], lq_n, qch_n, lc_n);
     if (lq == (int)kMissing) continue;  // r1 has no value: property skipped for the wave
     const bool present = lc != (int)kMissing;
     const bool cmp = present && lq > 0 && lc > 0;
@@ -1284,7 +1288,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       }
     }
     if (SYM && D.op == DK_CMP_JAROWINKLER) asym = true;  // wave-uniform
-    if (p == P.raw_prop) {  // Comparator.compare(v1, v2) itself (wave-uniform branch)
+    if (pp == P.raw_prop) {  // Comparator.compare(v1, v2) itself (wave-uniform branch)
       if (cmp) prob = sim;
       break;
     }

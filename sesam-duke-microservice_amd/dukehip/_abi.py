@@ -21,11 +21,12 @@ DK_E_INVALID, DK_E_UNSUPPORTED, DK_E_NOMEM, DK_E_DEVICE, DK_E_STATE = -1, -2, -3
 QGRAM_OVERLAP, QGRAM_JACCARD, QGRAM_DICE = 0, 1, 2
 QGRAM_BASIC, QGRAM_POSITIONAL, QGRAM_ENDS = 0, 1, 2
 MODE_DEDUP, MODE_LINKAGE, MODE_ALLPAIRS = 0, 1, 2
+MAX_ORDER_CLASSES = 4   # DK_MAX_ORDER_CLASSES
 KIND_MATCH, KIND_MAYBE = 1, 2
 
 MATCH_HOST, MATCH_DEVICE = 0, 1
 LUCENE_STATS_MERGED, LUCENE_STATS_UNMERGED = 0, 1
-ABI_VERSION = 6   # include/dukehip.h DK_ABI_VERSION
+ABI_VERSION = 7   # include/dukehip.h DK_ABI_VERSION
 
 EXPORTS = ("dk_create", "dk_create_multi", "dk_num_devices", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
            "dk_lucene_set_stats", "dk_lucene_merge",
@@ -60,7 +61,19 @@ class dk_lucene(C.Structure):
 class dk_schema(C.Structure):
     _fields_ = [("nprops", C.c_int32), ("props", C.POINTER(dk_property)),
                 ("threshold", C.c_double), ("maybe_threshold", C.c_double),
-                ("mode", C.c_int32), ("nkeys", C.c_int32), ("lucene", C.POINTER(dk_lucene))]
+                ("mode", C.c_int32), ("nkeys", C.c_int32), ("lucene", C.POINTER(dk_lucene)),
+                ("norders", C.c_int32), ("orders", C.POINTER(C.c_int32))]
+
+
+def order_classes(schema, orders):
+    """Give `schema` (a dk_schema) per order class the visiting order of its properties
+    (dk_schema.orders; indices into schema.props)."""
+    n = schema.nprops
+    flat = (C.c_int32 * max(1, len(orders) * n))(*[int(x) for o in orders for x in o])
+    schema.norders = len(orders)
+    schema.orders = flat
+    schema._keep_orders = flat
+    return schema
 
 
 def lucene_source(schema, lookup_props, max_hits=10, min_relevance=0.9):
@@ -81,7 +94,8 @@ class dk_column(C.Structure):
 class dk_batch(C.Structure):
     _fields_ = [("n", C.c_uint64), ("ident", C.c_void_p), ("group", C.c_void_p),
                 ("deleted", C.c_void_p), ("columns", C.POINTER(dk_column)),
-                ("keys", C.c_void_p), ("key_columns", C.POINTER(dk_column))]
+                ("keys", C.c_void_p), ("key_columns", C.POINTER(dk_column)),
+                ("order_class", C.c_void_p)]
 
 
 class dk_result(C.Structure):

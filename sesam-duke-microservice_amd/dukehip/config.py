@@ -154,48 +154,76 @@ class DukeConfig:
         return cls(props, d["threshold"], d.get("maybe_threshold", 0.0), sources,
                    d.get("linkage", False))
 
-    def comparison_order(self):
-        """Scored properties in Processor.compare's visiting order: the key order of the
-        record's java.util.HashMap (RecordImpl), whose keys are the data source's column
-        properties followed by the synthetic ones IncrementalDataSource adds
-        (IncrementalDataSource.java:76-98)."""
+    def _record_keys(self, ds=None):
+        """A record's possible HashMap keys in insertion order (IncrementalDataSource.java:
+        67-98): the data source's column properties, then the synthetic ones (dukeDeleted,
+        added last for deleted entities, is left to the caller), plus scored properties no
+        column fills (never present; kept so every scored property has a place)."""
         names = []
-        cols = self.data_sources[0].columns if self.data_sources else []
-        for c in cols:
+        cols = (ds or (self.data_sources[0] if self.data_sources else None))
+        for c in (cols.columns if cols else []):
             if c.property not in names:
                 names.append(c.property)
+        ncols = len(names)
         for p in self.scored_properties():
             if p.name not in names:
                 names.append(p.name)
+        if cols is None:   # no data source declared: any scored property may hold a value
+            ncols = len(names)
         synth = ([GROUP_NO_PROPERTY_NAME] if self.linkage else []) + [
             ID_PROPERTY, ORIGINAL_ENTITY_ID_PROPERTY_NAME, DATASET_ID_PROPERTY_NAME]
-        # A HashMap keeps capacity 16 up to 12 keys; past that its capacity (and so its
-        # iteration order) depends on how many values a record holds, and computeBayes is
-        # not associative: the GPU path runs one fixed order, so such schemas are not
-        # eligible.  (+1: dukeDeleted is added for deleted entities.)
-        if len(names + synth) + 1 > 12:
+        return names, synth, ncols
+
+    def order_classes(self):
+        """Processor.compare visits r1's properties in its RecordImpl HashMap's iteration
+        order, which depends on the map's capacity: 16 up to 12 keys, 32 up to 24, 64 up to
+        48 -- i.e. on how many properties the record holds values for.  Returns (caps,
+        orders): the capacities a record of this pipeline can have (ascending) and for each
+        the scored properties in visiting order (a record's missing ones are skipped)."""
+        names, synth, ncols = self._record_keys()
+        lo = len(synth)                      # no column value
+        hi = ncols + len(synth) + 1          # every column + dukeDeleted
+        if hi > 48:
             raise UnsupportedComparator(
-                f"{len(names + synth) + 1} record properties: past 12 a record's HashMap "
-                "order depends on its value count (not GPU-eligible)")
-        order = java_hashmap_order(names + synth)
+                f"up to {hi} record properties: past 48 a record's HashMap grows past "
+                "capacity 64 (not GPU-eligible)")
+        caps = sorted({hashmap_capacity(k) for k in range(lo, hi + 1)})
+        keys = names + synth + [DELETED_PROPERTY_NAME]
         scored = {p.name: p for p in self.scored_properties()}
-        out = [scored[n] for n in order if n in scored]
-        # every data source must give its records the same visiting order (a different
+        orders = []
+        for cap in caps:
+            order = java_hashmap_order(keys, cap)
+            orders.append([scored[n] for n in order if n in scored])
+        # every data source must give its records the same visiting orders (a different
         # column order only matters for keys sharing a HashMap bucket)
         for ds in self.data_sources[1:]:
-            alt = []
-            for c in ds.columns:
-                if c.property not in alt:
-                    alt.append(c.property)
-            alt += [p.name for p in self.scored_properties() if p.name not in alt]
-            if [n for n in java_hashmap_order(alt + synth) if n in scored] != [p.name for p in out]:
-                raise UnsupportedComparator(
-                    f"data source {ds.dataset_id!r} orders the record's properties differently "
-                    "(HashMap bucket collision): one fixed comparison order does not hold")
-        return out
+            alt, _, _ = self._record_keys(ds)
+            for cap, want in zip(caps, orders):
+                got = [n for n in java_hashmap_order(alt + synth + [DELETED_PROPERTY_NAME], cap)
+                       if n in scored]
+                if got != [p.name for p in want]:
+                    raise UnsupportedComparator(
+                        f"data source {ds.dataset_id!r} orders the record's properties "
+                        "differently (HashMap bucket collision): one fixed comparison order "
+                        "does not hold")
+        return caps, orders
+
+    def comparison_order(self):
+        """Scored properties in Processor.compare's visiting order for a record of the
+        smallest HashMap capacity the pipeline's records can have (the only one up to 12
+        record properties): the schema's property order (dk_schema.props)."""
+        return self.order_classes()[1][0]
+
+    def record_class(self, record, caps):
+        """The order class of a record (index into order_classes()[0]): its HashMap's
+        capacity from the number of properties it holds values for."""
+        return caps.index(hashmap_capacity(len(record.get_properties())))
 
     def to_schema(self, mode, nkeys):
-        props = self.comparison_order()
+        """(dk_schema, props in its order); with several order classes the schema carries
+        them (dk_schema.orders: class c visits props[orders[c][k]])."""
+        caps, orders = self.order_classes()
+        props = orders[0]
         arr = (A.dk_property * max(1, len(props)))()
         for i, p in enumerate(props):
             if p.comparator is None:
@@ -204,6 +232,11 @@ class DukeConfig:
                 arr[i] = p.comparator.to_c(p.low, p.high)
         s = A.dk_schema(len(props), arr, self.threshold, self.maybe_threshold, mode, nkeys)
         s._keep = arr
+        if len(orders) > 1:
+            if len(orders) > A.MAX_ORDER_CLASSES:
+                raise UnsupportedComparator(f"{len(orders)} HashMap order classes")
+            idx = {p.name: i for i, p in enumerate(props)}
+            A.order_classes(s, [[idx[p.name] for p in o] for o in orders])
         return s, props
 
 
@@ -215,18 +248,28 @@ def java_string_hash(s: str) -> int:
     return h
 
 
-def java_hashmap_order(keys):
-    """Iteration order of a java.util.HashMap<String,?> filled with `keys` in this order
-    (default capacity 16, doubled past 0.75 load; buckets by (h ^ h>>>16) & (cap-1),
-    insertion order inside a bucket)."""
+def hashmap_capacity(nkeys):
+    """java.util.HashMap's table size after `nkeys` puts (default 16, doubled when the size
+    passes 0.75 of it)."""
     cap = 16
-    while len(keys) > cap * 0.75:
+    while nkeys > cap * 0.75:
         cap *= 2
+    return cap
+
+
+def java_hashmap_order(keys, cap=None):
+    """Iteration order of a java.util.HashMap<String,?> filled with `keys` in this order
+    (capacity `cap`, default: the one those puts give; buckets by (h ^ h>>>16) & (cap-1),
+    insertion order inside a bucket -- a resize splits a bucket keeping its order).  A
+    bucket of 8 or more keys at capacity >= 64 would be a tree bin: refused."""
+    cap = hashmap_capacity(len(keys)) if cap is None else cap
     buckets = {}
     for k in keys:
         h = java_string_hash(k)
         idx = (h ^ (h >> 16)) & (cap - 1)
         buckets.setdefault(idx, []).append(k)
+    if cap >= 64 and any(len(b) >= 8 for b in buckets.values()):
+        raise UnsupportedComparator("HashMap tree bin (8 keys in one bucket): order not modelled")
     return [k for i in sorted(buckets) for k in buckets[i]]
 
 

@@ -149,11 +149,13 @@ class GpuEngine:
         return int(self.lib.dk_num_rows(self.ctx))
 
     def upsert(self, n, ident, columns, group=None, deleted=None, keys=None, key_columns=None,
-               transient=False):
+               transient=False, order_class=None):
         """columns: list of A.Column (schema order); keys: uint64 array [nkeys, n] or
         key_columns: list of A.Column.  Returns the assigned rows.  transient=True appends
-        query-only rows (dk_upsert_transient) that :meth:`drop_transient` removes."""
+        query-only rows (dk_upsert_transient) that :meth:`drop_transient` removes.
+        order_class: per record its Processor.compare order class (dk_schema.orders)."""
         ident = np.ascontiguousarray(ident, dtype=np.uint64)
+        oc = None if order_class is None else np.ascontiguousarray(order_class, dtype=np.uint8)
         group = None if group is None else np.ascontiguousarray(group, dtype=np.uint8)
         deleted = None if deleted is None else np.ascontiguousarray(deleted, dtype=np.uint8)
         cols = (A.dk_column * max(1, len(columns)))(*[c.c() for c in columns])
@@ -164,7 +166,7 @@ class GpuEngine:
             kptr = keys.ctypes.data
         if key_columns is not None:
             kc = (A.dk_column * max(1, len(key_columns)))(*[c.c() for c in key_columns])
-        b = A.dk_batch(n, ident.ctypes.data, A.ptr(group), A.ptr(deleted), cols, kptr, kc)
+        b = A.dk_batch(n, ident.ctypes.data, A.ptr(group), A.ptr(deleted), cols, kptr, kc, A.ptr(oc))
         rows = np.zeros(max(1, n), dtype=np.uint32)
         fn = self.lib.dk_upsert_transient if transient else self.lib.dk_upsert
         A.check(fn(self.ctx, C.byref(b), rows.ctypes.data))
@@ -230,12 +232,14 @@ class GpuEngine:
         A.check(self.lib.dk_compare_rows(self.ctx, int(r1), int(r2), C.byref(out)))
         return out.value
 
-    def compare_values(self, columns):
+    def compare_values(self, columns, order_class=(0, 0)):
         """dk_compare_values: Processor.compare(r1, r2) of two records given as columns of
-        two values each (schema order; None = no value).  The index is not touched."""
+        two values each (schema order; None = no value), r1's order class first.  The index
+        is not touched."""
         cols = (A.dk_column * max(1, len(columns)))(*[c.c() for c in columns])
         ident = np.zeros(2, np.uint64)
-        b = A.dk_batch(2, ident.ctypes.data, None, None, cols, None, None)
+        oc = np.ascontiguousarray(order_class, dtype=np.uint8)
+        b = A.dk_batch(2, ident.ctypes.data, None, None, cols, None, None, oc.ctypes.data)
         out = C.c_double()
         A.check(self.lib.dk_compare_values(self.ctx, C.byref(b), C.byref(out)))
         return out.value
@@ -352,6 +356,7 @@ class GpuBlockingDatabase:
         self.mode = mode
         nkeys = 0 if mode == A.MODE_ALLPAIRS else len(self.key_functions)
         self.schema, self.props = config.to_schema(mode, nkeys)
+        self.caps = config.order_classes()[0]   # HashMap capacities -> order classes
         self.lookup = None
         if mode != A.MODE_ALLPAIRS and not self.key_functions:
             from .lucene import LuceneOptions, lookup_properties
@@ -455,8 +460,11 @@ class GpuBlockingDatabase:
         if self.mode != A.MODE_ALLPAIRS and self.key_functions:
             key_cols = [A.Column.from_strings([kf.make_key(r) for r in records])
                         for kf in self.key_functions]
+        oc = None
+        if len(self.caps) > 1:   # Processor.compare follows each query record's HashMap order
+            oc = np.array([self.config.record_class(r, self.caps) for r in records], np.uint8)
         rows = self.engine.upsert(n, ident, cols, group=group, deleted=deleted,
-                                  key_columns=key_cols, transient=transient)
+                                  key_columns=key_cols, transient=transient, order_class=oc)
         if transient and self._transient_row0 is None:
             self._transient_row0 = len(self.rows)
         self.rows.append_records(records)
@@ -476,6 +484,9 @@ class GpuBlockingDatabase:
         packed).  Raises dukehip.ingest.NativeUnsupported for a batch the native reader
         declines (the caller then uses records_from_entities + index_batch)."""
         transient = self.indexing_disabled if transient is None else bool(transient)
+        if len(self.caps) > 1:   # the native packer does not count a record's properties
+            from .ingest import NativeUnsupported
+            raise NativeUnsupported("several HashMap order classes: records path")
         packed = self.native_source(source).pack(body, self.ids)
         if packed.n == 0:
             return np.zeros(0, np.uint32), packed

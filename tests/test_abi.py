@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
 
 def test_abi_version_and_error_text():
     lib = A.load()
-    assert lib.dk_abi_version() == A.ABI_VERSION == 6
+    assert lib.dk_abi_version() == A.ABI_VERSION == 7
     assert isinstance(lib.dk_last_error(), bytes)
 
 

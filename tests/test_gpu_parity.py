@@ -4,6 +4,7 @@ bit-exact as well (same operation order, no FMA) — the north star allows 1e-12
 
 Oracle: oracle/duke_oracle.c, PARITY UNPINNED against Duke 1.2 itself (see its header).
 """
+import ctypes as C
 import random
 
 import numpy as np
@@ -540,3 +541,68 @@ def test_qgram_bigram_keys_widened_arena():
     res, ref = run_both([prop], [vals2], keys=[keys2], threshold=0.5, maybe=0.3,
                         batches=[(0, n), (n, len(vals2))])
     assert_same(res, ref)
+
+
+@pytest.mark.parametrize("mode", ["dedup", "linkage"])
+def test_order_classes_wide_schema(mode):
+    """Past 12 record keys: 14 scored properties, rows missing values,
+    each row in the order class of its HashMap capacity (16 for <= 12 keys, 32 past that);
+    Processor.compare visits the QUERY record's order, so the kernels must pick the order
+    per query row.  Compared bit-exact with the oracle fed the same per-row classes, and
+    shown to matter: the same rows all in class 0 give different probabilities."""
+    from dukehip import config as cfgmod
+    rng = random.Random(14)
+    n = 700
+    kinds = [LEV, JW, EX, NUM, QG, LEV, JW, LEV, EX, QG, LEV, JW, NUM, LEV]
+    props = [{"comparator": c, "low": 0.2 + 0.01 * i, "high": 0.8 + 0.01 * i} for i, c in enumerate(kinds)]
+    pool = rand_strings(rng, 40, "abcde", 2, 9)
+    vals = []
+    for p in props:
+        col = []
+        for _ in range(n):
+            if rng.random() < 0.3:
+                col.append(None)
+            elif p["comparator"] == NUM:
+                col.append(str(rng.randint(1, 60)))
+            else:
+                col.append(rng.choice(pool))
+        vals.append(col)
+    names = [f"P{i}" for i in range(len(props))]
+    extra = [cfgmod.ID_PROPERTY, cfgmod.ORIGINAL_ENTITY_ID_PROPERTY_NAME, cfgmod.DATASET_ID_PROPERTY_NAME]
+    orders = []
+    for cap in (16, 32):
+        o = cfgmod.java_hashmap_order(names + extra + [cfgmod.DELETED_PROPERTY_NAME], cap)
+        orders.append([names.index(k) for k in o if k in names])
+    assert orders[0] != orders[1]
+    nvals = np.array([sum(v[r] is not None for v in vals) for r in range(n)])
+    oclass = (nvals + len(extra) > 12).astype(np.uint8)
+    assert 0 < oclass.sum() < n
+    keys = [[rng.choice("xyz") for _ in range(n)]]
+    group = [1 + (r % 2) for r in range(n)] if mode == "linkage" else None
+    ident = np.arange(n, dtype=np.uint64)
+
+    def run(oc):
+        s = schema_of(props, 0.7, 0.4, mode, len(keys))
+        flat = (C.c_int * (2 * len(props)))(*[x for o in orders for x in o])
+        s.norders, s.orders, s._orders = 2, flat, flat
+        eng = dh.GpuEngine(s)
+        eng.upsert(n, ident, [dh.Column.from_strings(v) for v in vals],
+                   group=None if group is None else np.asarray(group, np.uint8),
+                   key_columns=[dh.Column.from_strings(k) for k in keys], order_class=oc)
+        res = eng.match(np.arange(n, dtype=np.uint32))
+        cv = [eng.compare_values([dh.Column.from_strings([v[a], v[b]]) for v in vals],
+                                 order_class=(int(oc[a]), int(oc[b]))) for a, b in ((0, 1), (5, 9), (17, 3))]
+        eng.close()
+        return res, cv
+
+    res, cv = run(oclass)
+    ot = O.OracleTable(props, vals, keys=keys, ident=ident, group=group, threshold=0.7, maybe=0.4,
+                       mode=mode, orders=orders, oclass=oclass)
+    ref = ot.match(np.arange(n, dtype=np.uint32))
+    assert len(ref["query"]) > 50
+    assert_same(res, ref)
+    for (a, b), got in zip(((0, 1), (5, 9), (17, 3)), cv):
+        want = ot.compare_rows(a, b)
+        assert got == want or (np.isnan(got) and np.isnan(want))
+    flat, _ = run(np.zeros(n, np.uint8))
+    assert not (np.array_equal(flat.candidate, res.candidate) and np.array_equal(flat.prob, res.prob))

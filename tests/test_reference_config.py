@@ -86,12 +86,35 @@ def test_cleaners_recalled():
     assert R.capital_clean("Kingston (Jamaica)") == "kingston"
 
 
-def test_wide_schema_not_gpu_eligible():
-    """Past 12 record keys a HashMap's capacity depends on the record's value count."""
+def test_wide_schema_order_classes():
+    """Past 12 record keys a HashMap's capacity depends on the record's value count: one
+    order class per reachable capacity (dk_schema.orders), each the scored properties in
+    the iteration order of a HashMap of that capacity holding every possible key; a record's
+    class follows the number of properties it holds.  Past 48 keys: not GPU-eligible."""
     props = [cfgmod.Property(f"P{i}", cfgmod.Comparator(cfgmod.DUKE_CMP + "ExactComparator"), 0.3, 0.7)
-             for i in range(9)]
-    cfg = cfgmod.DukeConfig(props, 0.9)
+             for i in range(14)]
+    cols = [cfgmod.DataSourceColumn(f"c{i}", f"P{i}") for i in range(14)]
+    cfg = cfgmod.DukeConfig(props, 0.9, data_sources=[cfgmod.DataSource("ds", cols)])
+    caps, orders = cfg.order_classes()
+    assert caps == [16, 32]                      # 3 .. 14 + 3 + 1 = 18 keys
+    keys = [f"P{i}" for i in range(14)] + [cfgmod.ID_PROPERTY, cfgmod.ORIGINAL_ENTITY_ID_PROPERTY_NAME,
+                                            cfgmod.DATASET_ID_PROPERTY_NAME, cfgmod.DELETED_PROPERTY_NAME]
+    for cap, o in zip(caps, orders):
+        assert [p.name for p in o] == [k for k in cfgmod.java_hashmap_order(keys, cap) if k.startswith("P")]
+    assert [p.name for p in orders[0]] != [p.name for p in orders[1]]   # the classes differ here
+    s, sp = cfg.to_schema(A.MODE_DEDUP, 1)
+    assert s.nprops == 14 and s.norders == 2
+    got = [[sp[s.orders[c * 14 + k]].name for k in range(14)] for c in range(2)]
+    assert got == [[p.name for p in o] for o in orders]
+    from dukehip.records import Record
+    small = Record({"P0": "a", "ID": "x", "dukeOriginalEntityId": "1", "dukeDatasetId": "ds"})
+    big = Record({**{f"P{i}": "a" for i in range(11)}, "ID": "x", "dukeOriginalEntityId": "1",
+                  "dukeDatasetId": "ds"})
+    assert cfg.record_class(small, caps) == 0 and cfg.record_class(big, caps) == 1   # 4 / 14 keys
+    wide = [cfgmod.Property(f"W{i}", None, 0.3, 0.7) for i in range(46)]
+    wcfg = cfgmod.DukeConfig(wide, 0.9, data_sources=[cfgmod.DataSource(
+        "ds", [cfgmod.DataSourceColumn(f"w{i}", f"W{i}") for i in range(46)])])
     with pytest.raises(cfgmod.UnsupportedComparator):
-        cfg.to_schema(A.MODE_DEDUP, 1)
-    cfg = cfgmod.DukeConfig(props[:8], 0.9)
-    assert cfg.to_schema(A.MODE_DEDUP, 1)[0].nprops == 8
+        wcfg.to_schema(A.MODE_DEDUP, 1)
+    narrow = cfgmod.DukeConfig(props[:8], 0.9)
+    assert narrow.to_schema(A.MODE_DEDUP, 1)[0].norders == 0
