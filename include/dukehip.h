@@ -67,6 +67,8 @@ extern "C" {
 #define DK_CMP_WEIGHTED_LEVENSHTEIN 6 /* comparators.WeightedLevenshtein (default weights) */
 #define DK_CMP_DICE_TOKENS 7          /* comparators.DiceCoefficientComparator (Exact sub-comparator) */
 #define DK_CMP_JACCARD_TOKENS 8       /* comparators.JaccardIndexComparator (Exact sub-comparator) */
+#define DK_CMP_GEOPOSITION 9          /* comparators.GeopositionComparator ("lat,lng" degrees;
+                                         max-distance in meters in dk_property.min_ratio) */
 
 #define DK_QGRAM_OVERLAP 0 /* QGramComparator.Formula */
 #define DK_QGRAM_JACCARD 1
@@ -89,7 +91,8 @@ typedef struct dk_property {
   int32_t qgram_tokenizer; /* DK_QGRAM_BASIC/POSITIONAL/ENDS (POSITIONAL: q <= 3) */
   double low;              /* <low> */
   double high;             /* <high> */
-  double min_ratio;        /* NumericComparator.setMinRatio (default 0.0) */
+  double min_ratio;        /* the comparator's double parameter: NumericComparator.setMinRatio
+                              (default 0.0); GeopositionComparator.setMaxDistance (meters) */
 } dk_property;
 
 /* Lucene-compatible candidate source: the reference's own

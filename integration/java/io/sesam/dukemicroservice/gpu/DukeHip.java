@@ -21,7 +21,7 @@ public final class DukeHip {
 
     public static final int CMP_NONE = 0, CMP_LEVENSHTEIN = 1, CMP_JAROWINKLER = 2, CMP_QGRAM = 3,
             CMP_EXACT = 4, CMP_NUMERIC = 5, CMP_WEIGHTED_LEVENSHTEIN = 6, CMP_DICE_TOKENS = 7,
-            CMP_JACCARD_TOKENS = 8;
+            CMP_JACCARD_TOKENS = 8, CMP_GEOPOSITION = 9;
     public static final int MODE_DEDUP = 0, MODE_LINKAGE = 1, MODE_ALLPAIRS = 2;
     public static final int KIND_MATCH = 1, KIND_MAYBE = 2;
     public static final int E_INVALID = -1, E_UNSUPPORTED = -2, E_NOMEM = -3, E_DEVICE = -4, E_STATE = -5;

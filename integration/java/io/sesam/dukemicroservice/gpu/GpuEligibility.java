@@ -72,6 +72,13 @@ public final class GpuEligibility {
         if (System.getenv("MAX_SEARCH_HITS") != null) maxHits = Integer.parseInt(System.getenv("MAX_SEARCH_HITS"));
         if (maxHits < 1 || maxHits > 100) throw new IllegalArgumentException("MAX_SEARCH_HITS " + maxHits);
         if (config.getLookupProperties().isEmpty()) throw new IllegalArgumentException("no lookup properties");
+        // a GeopositionComparator as the only lookup property: the reference's geo search
+        // raises (IncrementalLuceneDatabase.java:433-441, 460-463) -- stock Duke keeps it
+        if (config.getLookupProperties().size() == 1) {
+            Comparator only = config.getLookupProperties().iterator().next().getComparator();
+            if (only != null && only.getClass().getName().equals("no.priv.garshol.duke.comparators.GeopositionComparator"))
+                throw new IllegalArgumentException("GeopositionComparator as the only lookup property");
+        }
         for (Property p : config.getLookupProperties()) {
             if (p.getLookupBehaviour() == Property.Lookup.REQUIRED)
                 throw new IllegalArgumentException("Lookup.REQUIRED: MUST clauses are not GPU-eligible");
@@ -97,6 +104,9 @@ public final class GpuEligibility {
                 return new Opcode(DukeHip.CMP_EXACT, 2, 0, 0, 0.0);
             case "no.priv.garshol.duke.comparators.WeightedLevenshtein":
                 return new Opcode(DukeHip.CMP_WEIGHTED_LEVENSHTEIN, 2, 0, 0, 0.0);
+            case "no.priv.garshol.duke.comparators.GeopositionComparator":
+                // max-distance (meters) travels in the double parameter (dk_property.min_ratio)
+                return new Opcode(DukeHip.CMP_GEOPOSITION, 2, 0, 0, ((Number) field(c, "maxdist")).doubleValue());
             case "no.priv.garshol.duke.comparators.NumericComparator":
                 return new Opcode(DukeHip.CMP_NUMERIC, 2, 0, 0, ((Number) field(c, "minratio")).doubleValue());
             case "no.priv.garshol.duke.comparators.QGramComparator": {

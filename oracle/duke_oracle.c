@@ -287,6 +287,35 @@ double dko_numeric(const uint16_t* s1, int n1, const uint16_t* s2, int n2, doubl
   return ratio;
 }
 
+/* [Duke 1.2, recalled, low confidence; parity unpinned: no Duke source or fixture here]
+ * utils.Geoposition.parse: split at the first ',', Double.parseDouble of each half (degrees);
+ * Geoposition.distance: haversine, R = 6371000 m, Math.toRadians as Java 8 (angdeg / 180.0 *
+ * PI); comparators.GeopositionComparator.compare: unparsable -> 0.5, dist > maxdist -> 0.0,
+ * else ((1.0 - (dist / maxdist)) * 0.5) + 0.5.  A value without ',' makes Geoposition.parse
+ * raise: returns -1 here (the GPU path refuses such a value at upsert). */
+int dko_parse_geoposition(const uint16_t* s, int n, double* lat, double* lng) {
+  int comma = 0;
+  while (comma < n && s[comma] != ',') comma++;
+  if (comma == n) return -1;
+  if (dko_parse_java_double(s, comma, lat) != 0) return 0;
+  if (dko_parse_java_double(s + comma + 1, n - comma - 1, lng) != 0) return 0;
+  return 1;
+}
+
+double dko_geoposition(const uint16_t* s1, int n1, const uint16_t* s2, int n2, double maxdist) {
+  double la1, ln1, la2, ln2;
+  if (dko_parse_geoposition(s1, n1, &la1, &ln1) != 1) return 0.5;
+  if (dko_parse_geoposition(s2, n2, &la2, &ln2) != 1) return 0.5;
+  const double pi = 3.141592653589793;
+  double lat1 = la1 / 180.0 * pi, lat2 = la2 / 180.0 * pi;
+  double dlat = (la2 - la1) / 180.0 * pi, dlng = (ln2 - ln1) / 180.0 * pi;
+  double sl = sin(dlat / 2), sg = sin(dlng / 2);
+  double a = sl * sl + sg * sg * cos(lat1) * cos(lat2);
+  double dist = 6371000.0 * (2 * atan2(sqrt(a), sqrt(1 - a)));
+  if (dist > maxdist) return 0.0;
+  return ((1.0 - (dist / maxdist)) * 0.5) + 0.5;
+}
+
 /* [Duke 1.2, recalled, medium confidence] comparators.DefaultWeightEstimator.singleChar */
 static double wl_weight(uint16_t ch) {
   if ((ch >= 'a' && ch <= 'z') || (ch >= 'A' && ch <= 'Z')) return 1.0;
@@ -407,6 +436,7 @@ double dko_property_compare(const dko_prop* p, const uint16_t* s1, int n1,
     case DKO_CMP_WEIGHTED_LEVENSHTEIN: sim = dko_weighted_levenshtein(s1, n1, s2, n2); break;
     case DKO_CMP_DICE_TOKENS: sim = dko_token_similarity(s1, n1, s2, n2, 0); break;
     case DKO_CMP_JACCARD_TOKENS: sim = dko_token_similarity(s1, n1, s2, n2, 1); break;
+    case DKO_CMP_GEOPOSITION: sim = dko_geoposition(s1, n1, s2, n2, p->min_ratio); break;
     default: return 0.5;
   }
   if (sim < 0.5) return p->low;

@@ -33,7 +33,8 @@ enum {
   DKO_CMP_NUMERIC = 5,
   DKO_CMP_WEIGHTED_LEVENSHTEIN = 6,
   DKO_CMP_DICE_TOKENS = 7,   /* DiceCoefficientComparator (ExactComparator sub-comparator) */
-  DKO_CMP_JACCARD_TOKENS = 8 /* JaccardIndexComparator (ExactComparator sub-comparator) */
+  DKO_CMP_JACCARD_TOKENS = 8, /* JaccardIndexComparator (ExactComparator sub-comparator) */
+  DKO_CMP_GEOPOSITION = 9     /* GeopositionComparator (max-distance in min_ratio) */
 };
 enum { DKO_QF_OVERLAP = 0, DKO_QF_JACCARD = 1, DKO_QF_DICE = 2 };
 enum { DKO_QT_BASIC = 0, DKO_QT_POSITIONAL = 1, DKO_QT_ENDS = 2 };
@@ -50,6 +51,8 @@ double dko_exact(const uint16_t* s1, int n1, const uint16_t* s2, int n2);
 /* Double.parseDouble; returns 0 and stores the value, or -1 for NumberFormatException */
 int    dko_parse_java_double(const uint16_t* s, int n, double* out);
 double dko_numeric(const uint16_t* s1, int n1, const uint16_t* s2, int n2, double min_ratio);
+int dko_parse_geoposition(const uint16_t* s, int n, double* lat, double* lng);
+double dko_geoposition(const uint16_t* s1, int n1, const uint16_t* s2, int n2, double maxdist);
 double dko_weighted_levenshtein(const uint16_t* s1, int n1, const uint16_t* s2, int n2);
 double dko_token_similarity(const uint16_t* s1, int n1, const uint16_t* s2, int n2, int jaccard);
 
@@ -61,7 +64,7 @@ typedef struct dko_prop {
   int comparator;
   double low, high;
   int q, formula, tokenizer;   /* QGramComparator */
-  double min_ratio;            /* NumericComparator */
+  double min_ratio;            /* NumericComparator min-ratio; GeopositionComparator max-distance */
 } dko_prop;
 
 /* [Duke 1.2] PropertyImpl.compare(v1, v2) */

@@ -17,7 +17,7 @@ import math
 import re
 
 LEVENSHTEIN, JAROWINKLER, QGRAM, EXACT, NUMERIC, WEIGHTED_LEVENSHTEIN = 1, 2, 3, 4, 5, 6
-DICE_TOKENS, JACCARD_TOKENS = 7, 8
+DICE_TOKENS, JACCARD_TOKENS, GEOPOSITION = 7, 8, 9
 OVERLAP, JACCARD, DICE = 0, 1, 2
 BASIC, POSITIONAL, ENDS = 0, 1, 2
 _CARET, _DOLLAR = ord("^"), ord("$")
@@ -283,6 +283,33 @@ def numeric(s1, s2, min_ratio=0.0) -> float:
     return ratio
 
 
+def geoposition(s1, s2, max_distance) -> float:
+    """[Duke 1.2, recalled, low confidence; parity unpinned] GeopositionComparator.compare:
+    Geoposition.parse ("lat,lng" split at the first ','; Double.parseDouble each half;
+    no ',' raises), haversine distance on a 6371000 m sphere with Java 8's Math.toRadians
+    (angdeg / 180.0 * PI); unparsable -> 0.5; dist > max-distance -> 0.0; else
+    ((1 - dist / max) * 0.5) + 0.5."""
+    pos = []
+    for s in (s1, s2):   # code units (or a str)
+        u = [ord(ch) for ch in s] if isinstance(s, str) else list(s)
+        if 0x2C not in u:
+            raise ValueError(f"no comma in position {s!r}")
+        c = u.index(0x2C)
+        la, ln = parse_java_double(u[:c]), parse_java_double(u[c + 1:])
+        if la is None or ln is None:
+            return 0.5
+        pos.append((la, ln))
+    (la1, ln1), (la2, ln2) = pos
+    lat1, lat2 = la1 / 180.0 * math.pi, la2 / 180.0 * math.pi
+    dlat, dlng = (la2 - la1) / 180.0 * math.pi, (ln2 - ln1) / 180.0 * math.pi
+    sl, sg = math.sin(dlat / 2), math.sin(dlng / 2)
+    a = sl * sl + sg * sg * math.cos(lat1) * math.cos(lat2)
+    dist = 6371000.0 * (2 * math.atan2(math.sqrt(a), math.sqrt(1 - a)))
+    if dist > max_distance:
+        return 0.0
+    return ((1.0 - (dist / max_distance)) * 0.5) + 0.5
+
+
 def java_max(a, b):
     if a != a:
         return a
@@ -319,6 +346,8 @@ def property_compare(prop, v1, v2):
         sim = weighted_levenshtein(v1, v2)
     elif c in (DICE_TOKENS, JACCARD_TOKENS):
         sim = token_set_similarity(v1, v2, c == JACCARD_TOKENS)
+    elif c == GEOPOSITION:
+        sim = geoposition(v1, v2, prop.get("min_ratio", 0.0))
     else:
         return 0.5
     if sim < 0.5:

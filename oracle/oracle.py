@@ -72,6 +72,8 @@ def lib():
         L.dko_qgram.argtypes = [u16p, C.c_int, u16p, C.c_int, C.c_int, C.c_int, C.c_int]
         L.dko_numeric.restype = C.c_double
         L.dko_numeric.argtypes = [u16p, C.c_int, u16p, C.c_int, C.c_double]
+        L.dko_geoposition.restype = C.c_double
+        L.dko_geoposition.argtypes = [u16p, C.c_int, u16p, C.c_int, C.c_double]
         L.dko_parse_java_double.restype = C.c_int
         L.dko_parse_java_double.argtypes = [u16p, C.c_int, C.POINTER(C.c_double)]
         L.dko_compute_bayes.restype = C.c_double
@@ -131,6 +133,10 @@ def exact(s1, s2):
 
 def numeric(s1, s2, min_ratio=0.0):
     return _call2("dko_numeric", s1, s2, min_ratio)
+
+
+def geoposition(s1, s2, max_distance):
+    return _call2("dko_geoposition", s1, s2, max_distance)
 
 
 def weighted_levenshtein(s1, s2):

@@ -319,6 +319,28 @@ static bool java_parse_double(const uint16_t* u, size_t n, double* out) {
   return true;
 }
 
+// doubles per row a property keeps in num / rnum: NumericComparator's value, or
+// GeopositionComparator's (latitude, longitude)
+static int num_words(int op) { return op == DK_CMP_NUMERIC ? 1 : op == DK_CMP_GEOPOSITION ? 2 : 0; }
+
+// [Duke 1.2, recalled] utils.Geoposition.parse: the value split at its first ',', each half
+// through Double.parseDouble (latitude, longitude in degrees).  Returns 1 when both parse,
+// 0 when either half is not a Java double (GeopositionComparator.compare -> 0.5), -1 when the
+// value has no ',' (stock Duke raises when it compares such a value).
+static int parse_geoposition(const uint16_t* u, size_t n, double* lat, double* lng) {
+  size_t comma = 0;
+  while (comma < n && u[comma] != ',') ++comma;
+  if (comma == n) return -1;
+  *lat = 0.0;
+  *lng = 0.0;
+  if (!java_parse_double(u, comma, lat) || !java_parse_double(u + comma + 1, n - comma - 1, lng)) {
+    *lat = 0.0;
+    *lng = 0.0;
+    return 0;
+  }
+  return 1;
+}
+
 // q-gram set of one value: sorted unique 64-bit codes, 16 bits per code unit
 // (QGramComparator's HashSet<String> of substrings; POSITIONAL adds the index; ENDS
 // [recalled] adds the start gram "^" + s[0, q-1) and the end gram s[n-q+1, n) + "$",
@@ -592,8 +614,8 @@ static hipError_t grow_rows(dk_ctx* c, uint64_t need) {
   for (auto& p : c->P) {
     GROW(p.off, uint32_t);
     GROW(p.len, uint16_t);
-    if (p.cfg.comparator == DK_CMP_NUMERIC) {
-      GROW(p.num, double);
+    if (const int nw = num_words(p.cfg.comparator)) {
+      if ((e = p.num.reserve(nc * 8 * nw, n * 8 * nw, s)) != hipSuccess) return e;
       GROW(p.numok, uint8_t);
     }
     if (uses_codes(p.cfg.comparator)) {
@@ -627,6 +649,12 @@ static int validate_schema(const dk_schema* s) {
       for (int j = 0; j < i; ++j)
         if (L.lookup_prop[j] == L.lookup_prop[i]) return fail(DK_E_INVALID, "lookup property repeated");
     }
+    // a GeopositionComparator as the only lookup property: the reference's database searches
+    // geo-spatially and raises (IncrementalLuceneDatabase.java:433-441, 460-463)
+    if (L.nlookup == 1 && s->props && L.lookup_prop[0] >= 0 && L.lookup_prop[0] < s->nprops &&
+        s->props[L.lookup_prop[0]].comparator == DK_CMP_GEOPOSITION)
+      return fail(DK_E_UNSUPPORTED, "a GeopositionComparator as the only lookup property "
+                  "(the reference's geo search raises, IncrementalLuceneDatabase.java:460-463)");
     if (L.max_hits < 1 || L.max_hits > kLuceneMaxHits)
       return fail(DK_E_UNSUPPORTED, "max_hits %d (supported 1..%d: larger values grow the search "
                   "limit adaptively, EstimateResultTracker)", L.max_hits, kLuceneMaxHits);
@@ -656,6 +684,7 @@ static int validate_schema(const dk_schema* s) {
       case DK_CMP_WEIGHTED_LEVENSHTEIN:
       case DK_CMP_DICE_TOKENS:
       case DK_CMP_JACCARD_TOKENS:
+      case DK_CMP_GEOPOSITION:
         break;
       case DK_CMP_QGRAM:
         if (p.qgram_q < 1 || p.qgram_q > 4)
@@ -883,7 +912,8 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
   // values on the DP comparators are bounded by the long-value DP (query rows <= 256)
   const bool is_dp = P.cfg.comparator == DK_CMP_LEVENSHTEIN ||
                      P.cfg.comparator == DK_CMP_WEIGHTED_LEVENSHTEIN;
-  const bool is_num = P.cfg.comparator == DK_CMP_NUMERIC;
+  const int nw = num_words(P.cfg.comparator);
+  const bool is_num = nw > 0;
   const bool is_qg = uses_codes(P.cfg.comparator);
   const bool is_tok = P.cfg.comparator != DK_CMP_QGRAM;
   // pass 1: validate, lay out (4-byte aligned values)
@@ -956,7 +986,7 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
   // most of a 1M-row linkage upsert); each range fills a gram buffer of its own, merged in
   // range order, so the code lists are in row order as before.  Token ids come from one
   // interner per property and stay serial.
-  if (is_num) { S.num.assign(n, 0.0); S.numok.assign(n, 0); }
+  if (is_num) { S.num.assign(n * nw, 0.0); S.numok.assign(n, 0); }
   if (is_qg) { S.goff.assign(n, 0); S.gcnt.assign(n, 0); }
   const int parts = is_tok || n < (1u << 15) ? 1 : 8;
   std::vector<std::vector<uint64_t>> pg(parts);
@@ -994,7 +1024,14 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
       v16.resize(L);
       if (col->width == 1) for (uint64_t k = 0; k < L; ++k) v16[k] = u8[a + k];
       else memcpy(v16.data(), u16 + a, L * 2);
-      if (is_num) {
+      if (nw == 2) {
+        const int r = parse_geoposition(v16.data(), L, &S.num[2 * i], &S.num[2 * i + 1]);
+        if (r < 0) {
+          pbad[t] = i | (1ull << 63);
+          return;
+        }
+        S.numok[i] = (uint8_t)r;
+      } else if (is_num) {
         double v = 0.0;
         S.numok[i] = java_parse_double(v16.data(), L, &v) ? 1 : 0;
         S.num[i] = v;
@@ -1015,10 +1052,15 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
       }
     }
   });
-  for (int t = 0; t < parts; ++t)
-    if (pbad[t] != ~0ull)
-      return fail(DK_E_UNSUPPORTED, "property %d: row %llu has too many q-grams / tokens", pidx,
-                  (unsigned long long)pbad[t]);
+  for (int t = 0; t < parts; ++t) {
+    if (pbad[t] == ~0ull) continue;
+    if (pbad[t] >> 63)
+      return fail(DK_E_UNSUPPORTED, "property %d: row %llu: GeopositionComparator value without ',' "
+                  "(Geoposition.parse raises in stock Duke)", pidx,
+                  (unsigned long long)(pbad[t] & ~(1ull << 63)));
+    return fail(DK_E_UNSUPPORTED, "property %d: row %llu has too many q-grams / tokens", pidx,
+                (unsigned long long)pbad[t]);
+  }
   if (is_qg) {
     std::vector<uint64_t> base(parts + 1, 0);
     for (int t = 0; t < parts; ++t) {
@@ -1090,7 +1132,8 @@ static int commit_column(dk_ctx* c, int pidx, ColStage& S, uint64_t n, uint64_t 
   HIPCHK(hipMemcpyAsync(P.off.as<uint32_t>() + row0, S.off.data(), n * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(P.len.as<uint16_t>() + row0, S.len.data(), n * 2, hipMemcpyHostToDevice, s));
   if (!S.num.empty()) {
-    HIPCHK(hipMemcpyAsync(P.num.as<double>() + row0, S.num.data(), n * 8, hipMemcpyHostToDevice, s));
+    const int nw = num_words(P.cfg.comparator);
+    HIPCHK(hipMemcpyAsync(P.num.as<double>() + row0 * nw, S.num.data(), n * 8 * nw, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(P.numok.as<uint8_t>() + row0, S.numok.data(), n, hipMemcpyHostToDevice, s));
   }
   if (!S.gcnt.empty()) {
@@ -1737,8 +1780,8 @@ static int layout_replica(dk_ctx* c, std::vector<Replica>& rep, uint64_t npos) {
     R.npos = npos;
     HIPCHK(R.rlen.reserve(npos * 2 + 8, 0, s));
     if (R.rlmax) HIPCHK(R.runits.reserve(npos * (uint64_t)R.rlmax * sh.width + 64, 0, s));
-    if (op == DK_CMP_NUMERIC) {
-      HIPCHK(R.rnum.reserve(npos * 8 + 8, 0, s));
+    if (const int nw = num_words(op)) {
+      HIPCHK(R.rnum.reserve(npos * 8 * nw + 16, 0, s));
       HIPCHK(R.rnumok.reserve(npos + 8, 0, s));
     }
     if (uses_codes(op)) {
@@ -1762,7 +1805,7 @@ static int fill_replica(dk_ctx* c, std::vector<Replica>& rep, const uint32_t* ro
     ReplicaJob J{};
     J.width = R.width;
     J.rlmax = R.rlmax;
-    J.has_num = op == DK_CMP_NUMERIC;
+    J.has_num = num_words(op);
     J.has_qgram = uses_codes(op);
     J.stride = R.npos;
     J.off = S.off.as<uint32_t>();
@@ -2108,7 +2151,8 @@ static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
   if (c->schema.mode != DK_MODE_DEDUP || P.long_rows > 0 || P.norders > 1) return false;
   for (const auto& S : c->P) {
     const int op = S.cfg.comparator;
-    if (op == DK_CMP_WEIGHTED_LEVENSHTEIN || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS)
+    if (op == DK_CMP_WEIGHTED_LEVENSHTEIN || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS ||
+        op == DK_CMP_GEOPOSITION)
       return false;
   }
   return true;

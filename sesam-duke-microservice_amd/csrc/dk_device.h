@@ -248,6 +248,25 @@ __device__ __forceinline__ double numeric(double d1, bool ok1, double d2, bool o
   return ratio;
 }
 
+// [Duke 1.2, recalled; parity unpinned] comparators.GeopositionComparator.compare with
+// utils.Geoposition.distance: haversine on a sphere of radius 6371000 m, Java 8's
+// Math.toRadians (angdeg / 180.0 * PI); an unparsable position -> 0.5; beyond max-distance
+// -> 0.0; else ((1 - dist / maxdist) * 0.5) + 0.5.  The same operation order as
+// oracle/duke_oracle.c dko_geoposition (no FMA contraction); sin / cos / atan2 may differ
+// from libm / Java by an ulp, hence the 1e-12 relative bar of the north star.
+__device__ __forceinline__ double geoposition(double lat1d, double lng1d, bool ok1, double lat2d, double lng2d,
+                                              bool ok2, double maxdist) {
+  if (!ok1 || !ok2) return 0.5;
+  const double pi = 3.141592653589793;
+  const double lat1 = lat1d / 180.0 * pi, lat2 = lat2d / 180.0 * pi;
+  const double dlat = (lat2d - lat1d) / 180.0 * pi, dlng = (lng2d - lng1d) / 180.0 * pi;
+  const double sl = sin(dlat / 2), sg = sin(dlng / 2);
+  const double a = sl * sl + sg * sg * cos(lat1) * cos(lat2);
+  const double dist = 6371000.0 * (2 * atan2(sqrt(a), sqrt(1 - a)));
+  if (dist > maxdist) return 0.0;
+  return ((1.0 - (dist / maxdist)) * 0.5) + 0.5;
+}
+
 // [Duke 1.2] Processor.compareCandidatesSimple: strict thresholds
 __device__ __forceinline__ uint32_t decide(double prob, double threshold, double maybe) {
   if (prob > threshold) return DK_KIND_MATCH;

@@ -266,7 +266,7 @@ struct BlockTables {
 struct ReplicaJob {
   int32_t width;
   int32_t rlmax;      // 0: no unit replica (long values, or non-string comparator)
-  int32_t has_num;
+  int32_t has_num;        // doubles per row in num / rnum (1 Numeric, 2 Geoposition; 0 none)
   int32_t has_qgram;
   int32_t rgmax;      // QGram replica rows (0: none)
   int32_t rg32;       // u32 replica codes

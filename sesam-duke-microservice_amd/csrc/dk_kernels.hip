@@ -1272,6 +1272,11 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
       if (cmp) bytes += 9u;   // rnum + rnumok
       rev = sim;
+    } else if (D.op == DK_CMP_GEOPOSITION) {
+      if (cmp) sim = geoposition(D.num[2 * q], D.num[2 * q + 1], D.numok[q] != 0, D.rnum[2 * g], D.rnum[2 * g + 1],
+                                 D.rnumok[g] != 0, D.min_ratio);
+      if (cmp) bytes += 17u;  // rnum pair + rnumok
+      rev = sim;
     } else if (D.op != DK_CMP_NONE) {
       rev = __builtin_nan("");  // marks "same as sim" unless the comparator sets it
       sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM, DP, GR>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch)
@@ -1599,7 +1604,11 @@ __global__ __launch_bounds__(256) void k_replicate(const ReplicaJob J, const uin
     if (J.width == 1) replicate_units<uint8_t>(J, g, row, l);
     else replicate_units<uint16_t>(J, g, row, l);
   }
-  if (J.has_num) {
+  if (J.has_num == 2) {  // (latitude, longitude): the 64 lanes of a score wave read 1 KiB
+    J.rnum[2 * g] = J.num[2 * (uint64_t)row];
+    J.rnum[2 * g + 1] = J.num[2 * (uint64_t)row + 1];
+    J.rnumok[g] = J.numok[row];
+  } else if (J.has_num) {
     J.rnum[g] = J.num[row];
     J.rnumok[g] = J.numok[row];
   }

@@ -17,7 +17,7 @@ DK_OK = 0
 DK_E_INVALID, DK_E_UNSUPPORTED, DK_E_NOMEM, DK_E_DEVICE, DK_E_STATE = -1, -2, -3, -4, -5
 
 (CMP_NONE, CMP_LEVENSHTEIN, CMP_JAROWINKLER, CMP_QGRAM, CMP_EXACT, CMP_NUMERIC,
- CMP_WEIGHTED_LEVENSHTEIN, CMP_DICE_TOKENS, CMP_JACCARD_TOKENS) = range(9)
+ CMP_WEIGHTED_LEVENSHTEIN, CMP_DICE_TOKENS, CMP_JACCARD_TOKENS, CMP_GEOPOSITION) = range(10)
 QGRAM_OVERLAP, QGRAM_JACCARD, QGRAM_DICE = 0, 1, 2
 QGRAM_BASIC, QGRAM_POSITIONAL, QGRAM_ENDS = 0, 1, 2
 MODE_DEDUP, MODE_LINKAGE, MODE_ALLPAIRS = 0, 1, 2

@@ -24,6 +24,7 @@ COMPARATOR_CLASSES = {
     DUKE_CMP + "WeightedLevenshtein": A.CMP_WEIGHTED_LEVENSHTEIN,
     DUKE_CMP + "DiceCoefficientComparator": A.CMP_DICE_TOKENS,
     DUKE_CMP + "JaccardIndexComparator": A.CMP_JACCARD_TOKENS,
+    DUKE_CMP + "GeopositionComparator": A.CMP_GEOPOSITION,
 }
 EXACT_CLASS = DUKE_CMP + "ExactComparator"
 FORMULAS = {"OVERLAP": A.QGRAM_OVERLAP, "JACCARD": A.QGRAM_JACCARD, "DICE": A.QGRAM_DICE}
@@ -55,6 +56,8 @@ class Comparator:
             key = name.replace("-", "").lower()   # bean setter: min-ratio -> setMinRatio
             if op == A.CMP_NUMERIC and key == "minratio":
                 p.min_ratio = float(value)
+            elif op == A.CMP_GEOPOSITION and key == "maxdistance":
+                p.min_ratio = float(value)      # setMaxDistance (meters), the double parameter
             elif op == A.CMP_QGRAM and key == "q":
                 p.qgram_q = int(value)
             elif op == A.CMP_QGRAM and key == "formula":

@@ -69,6 +69,13 @@ def lookup_properties(config, props):
     for p in props:
         if behaviour[p.name] == "true" and p.name not in out:
             out.append(p.name)
+    # a GeopositionComparator as the only lookup property: the reference's database searches
+    # geo-spatially and raises (IncrementalLuceneDatabase.java:433-441, 460-463)
+    if len(out) == 1:
+        only = next(p for p in props if p.name == out[0])
+        if only.comparator is not None and only.comparator.klass.endswith(".GeopositionComparator"):
+            raise UnsupportedComparator("GeopositionComparator as the only lookup property "
+                                        "(IncrementalLuceneDatabase.java:460-463 raises)")
     return out
 
 

@@ -74,3 +74,23 @@ def test_unknown_comparator_is_not_gpu_eligible():
                       "no.priv.garshol.duke.comparators.SoundexComparator")
     with pytest.raises(cfgmod.UnsupportedComparator):
         cfgmod.parse_duke_config(xml).to_schema(A.MODE_DEDUP, 1)
+
+
+def test_geoposition_comparator_maps_max_distance():
+    """GeopositionComparator (DK_CMP_GEOPOSITION): max-distance travels in the property's
+    double parameter; as the ONLY Lucene lookup property it stays on stock Duke, whose
+    database raises for it (IncrementalLuceneDatabase.java:433-441, 460-463)."""
+    from dukehip import lucene
+    xml = XML.replace("</schema>", """<property><name>POS</name><comparator>Geo</comparator>
+      <low>0.2</low><high>0.9</high></property></schema>""").replace(
+        "<schema>", """<object class="no.priv.garshol.duke.comparators.GeopositionComparator" name="Geo">
+    <param name="max-distance" value="2500"/></object><schema>""")
+    c = cfgmod.parse_duke_config(xml)
+    schema, props = c.to_schema(A.MODE_DEDUP, 1)
+    pos = schema.props[[p.name for p in props].index("POS")]
+    assert (pos.comparator, pos.min_ratio) == (A.CMP_GEOPOSITION, 2500.0)
+    geo = [p for p in props if p.name == "POS"]
+    geo[0].lookup = "true"
+    with pytest.raises(cfgmod.UnsupportedComparator):
+        lucene.lookup_properties(c, geo)
+    geo[0].lookup = "default"

@@ -606,3 +606,63 @@ def test_order_classes_wide_schema(mode):
         assert got == want or (np.isnan(got) and np.isnan(want))
     flat, _ = run(np.zeros(n, np.uint8))
     assert not (np.array_equal(flat.candidate, res.candidate) and np.array_equal(flat.prob, res.prob))
+
+
+def assert_close(res, ref, thresholds, rel=1e-12, edge=1e-9):
+    """The north star's floating-point bar for comparators on sin / cos / atan2: candidate
+    sets equal, probabilities within 1e-12 relative, decisions equal except for pairs within
+    1e-9 of a threshold."""
+    got = {(int(q), int(c)): (float(p), int(k)) for q, c, p, k in zip(res.query, res.candidate, res.prob, res.kind)}
+    want = {(int(q), int(c)): (float(p), int(k)) for q, c, p, k in
+            zip(ref["query"], ref["candidate"], ref["prob"], ref["kind"])}
+    assert res.pairs_scored == ref["pairs_scored"]
+    near = lambda p: any(abs(p - t) <= edge for t in thresholds)
+    for key in set(got) | set(want):
+        if key not in got or key not in want:
+            p = (got.get(key) or want.get(key))[0]
+            assert near(p), (key, got.get(key), want.get(key))
+            continue
+        (a, ka), (b, kb) = got[key], want[key]
+        assert abs(a - b) <= rel * abs(b), (key, a, b)
+        assert ka == kb or near(b), (key, ka, kb)
+
+
+@pytest.mark.parametrize("mode", ["dedup", "allpairs"])
+def test_geoposition(mode):
+    """GeopositionComparator (parity unpinned: the formula is recalled,
+    see oracle/duke_oracle.c dko_geoposition): positions scattered within a few km, some
+    unparsable ("x,1" -> 0.5) and some missing, next to a Levenshtein name; the GPU path
+    against the oracle at the north star's tolerance, and each similarity through
+    dk_property_similarity.  A value without ',' is refused at upsert (stock Duke raises)."""
+    rng = random.Random(31)
+    n = 600
+    pos = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.1:
+            pos.append(None)
+        elif r < 0.15:
+            pos.append(f"x{rng.randint(0, 9)},{rng.uniform(0, 1):.4f}")
+        else:
+            base = rng.choice([(59.91, 10.75), (60.39, 5.32), (-33.86, 151.2)])
+            pos.append(f"{base[0] + rng.uniform(-0.03, 0.03):.6f},{base[1] + rng.uniform(-0.03, 0.03):.6f}")
+    names = rand_strings(rng, n, "abc", 3, 6, none_frac=0.05)
+    props = [{"comparator": A.CMP_GEOPOSITION, "low": 0.1, "high": 0.95, "min_ratio": 4000.0},
+             {"comparator": LEV, "low": 0.3, "high": 0.8}]
+    keys = [[rng.choice("pq") for _ in range(n)]] if mode == "dedup" else []
+    res, ref = run_both(props, [pos, names], keys=keys, mode=mode, threshold=0.8, maybe=0.6)
+    assert len(ref["query"]) > 100
+    assert_close(res, ref, (0.8, 0.6))
+    eng = dh.GpuEngine(schema_of(props, 0.8, 0.6, "allpairs", 0))
+    eng.upsert(60, np.arange(60, dtype=np.uint64), [dh.Column.from_strings(v[:60]) for v in (pos, names)])
+    for a, b in [(i, j) for i in range(0, 60, 7) for j in range(1, 60, 5)]:
+        got = eng.property_similarity(0, a, b)
+        if pos[a] is None or pos[b] is None:
+            assert got != got
+            continue
+        want = O.geoposition(pos[a], pos[b], 4000.0)
+        assert abs(got - want) <= 1e-12 * abs(want), (pos[a], pos[b], got, want)
+    with pytest.raises(dh.DukeHipError) as e:
+        eng.upsert(1, np.array([99], np.uint64), [dh.Column.from_strings(["59.9"]), dh.Column.from_strings(["a"])])
+    assert e.value.code == A.DK_E_UNSUPPORTED
+    eng.close()
