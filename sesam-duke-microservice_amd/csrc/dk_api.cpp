@@ -211,7 +211,8 @@ struct PinnedBuf {
     if (nb <= bytes) return hipSuccess;
     size_t cap = std::max(nb, bytes * 2);
     void* q = nullptr;
-    hipError_t e = hipHostMalloc(&q, cap, hipHostMallocDefault);
+    // portable: a group list (dk_create_multi) is filled by copies from every member device
+    hipError_t e = hipHostMalloc(&q, cap, hipHostMallocPortable);
     if (e != hipSuccess) return e;
     if (keep && p) memcpy(q, p, keep);
     if (p) (void)hipHostFree(p);
@@ -1674,14 +1675,19 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
   P.long_rows = 0;
   P.raw_prop = -1;
   P.has_dp = 0;
+  P.has_geo = 0;
   P.norders = c->orders.empty() ? 1 : (int32_t)(c->orders.size() / std::max(1, P.nprops));
-  for (int o = 0; o < P.norders; ++o)
+  for (int o = 0; o < kMaxOrders; ++o) {
+    P.order[o] = 0;
+    if (o >= P.norders) continue;
     for (int k = 0; k < P.nprops; ++k)
-      P.order[o][k] = (uint8_t)(c->orders.empty() ? k : c->orders[(size_t)o * P.nprops + k]);
+      P.order[o] |= (uint64_t)(c->orders.empty() ? k : c->orders[(size_t)o * P.nprops + k]) << (4 * k);
+  }
   P.oclass = c->oclass.as<uint8_t>();
   for (const auto& S : c->P) {
     const int op = S.cfg.comparator;
     if (op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER || op == DK_CMP_WEIGHTED_LEVENSHTEIN) P.has_dp = 1;
+    if (op == DK_CMP_GEOPOSITION) P.has_geo = 1;
     if (op == DK_CMP_QGRAM || op == DK_CMP_DICE_TOKENS || op == DK_CMP_JACCARD_TOKENS) P.has_grams = 1;
     if (S.cfg.comparator == DK_CMP_LEVENSHTEIN) {
       P.lev_rows = std::max(P.lev_rows, std::min(S.maxlen, kMaxUnits));
@@ -2164,14 +2170,15 @@ static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
 static bool grouped_schema_ok(const ScoreParams& P) {
   const char* e = getenv("DK_GROUPED");
   if ((e && e[0] == '0') || P.has_dp || P.raw_prop >= 0 || P.nprops < 1) return false;
-  // every buffer offset of the kernel's raw buffer loads below 2^31
+  // every buffer offset of the kernel's raw buffer loads (u32) below 2^32, the rows a tail
+  // step reads past a property's last row included (they must stay out of range, not wrap)
   if (P.rstride * 8 >= (1ull << 31)) return false;
   int tabs = 0;
   for (int p = 0; p < P.nprops; ++p) {
     const DevProp& D = P.props[p];
     if (D.op == DK_CMP_QGRAM) {
       if (!D.g16 || D.rgrows < 1 || D.width != 1) return false;
-      if ((uint64_t)D.rgrows * P.rstride * 8 >= (1ull << 31)) return false;
+      if ((uint64_t)(D.rgrows + 8) * P.rstride * 8 >= (1ull << 32)) return false;
       ++tabs;
     } else if (D.op != DK_CMP_NUMERIC && D.op != DK_CMP_NONE) {
       return false;

@@ -267,6 +267,13 @@ __device__ __forceinline__ double geoposition(double lat1d, double lng1d, bool o
   return ((1.0 - (dist / maxdist)) * 0.5) + 0.5;
 }
 
+// the visiting order of order class oc (wave-uniform): ScoreParams::order[oc] by a select,
+// and its k-th property
+__device__ __forceinline__ uint64_t order_word(const ScoreParams& P, int oc) {
+  return oc == 0 ? P.order[0] : oc == 1 ? P.order[1] : oc == 2 ? P.order[2] : P.order[3];
+}
+__device__ __forceinline__ int order_at(uint64_t ow, int k) { return (int)((ow >> (4 * k)) & 15u); }
+
 // [Duke 1.2] Processor.compareCandidatesSimple: strict thresholds
 __device__ __forceinline__ uint32_t decide(double prob, double threshold, double maybe) {
   if (prob > threshold) return DK_KIND_MATCH;

@@ -11,6 +11,7 @@ namespace dk {
 
 constexpr int kMaxProps = 16;
 constexpr int kMaxOrders = DK_MAX_ORDER_CLASSES;  // Processor.compare visiting orders (dk_schema)
+static_assert(kMaxProps <= 16 && kMaxOrders == 4, "ScoreParams::order packs 4-bit positions");
 constexpr int kMaxKeys = 8;
 constexpr int kMaxSegs = 2 * kMaxKeys;  // per key function: sorted base + sorted delta
 constexpr uint16_t kMissing = 0xFFFF;  // length sentinel: record has no value
@@ -117,15 +118,20 @@ struct ScoreParams {
                           // (0: the DP-free kernel variant, no DP code or registers)
   int32_t has_grams;      // some property is QGram / Dice / Jaccard tokens (0: the short
                           // kernels' variant without the gram-set code or its registers)
+  int32_t has_geo;        // some property is GeopositionComparator: the GEO kernel variants
+                          // (libm's f64 sin / cos reduce large arguments in scratch memory,
+                          // which the other variants must not carry)
   double threshold;
   double maybe;
   const uint64_t* ident;
   const uint32_t* rowof;  // replica position -> row
   uint64_t rstride;       // replica positions (K * M)
-  // Processor.compare's visiting order of a query row: order[oclass[q]][k] = the k-th
-  // property (dk_schema.orders); norders 1: order[0] is the identity
+  // Processor.compare's visiting order of a query row: the k-th property of order class c
+  // is bits [4k, 4k + 4) of order[c] (dk_schema.orders); norders 1: order[0] is the
+  // identity.  Packed words, read by a uniform select (order_word): a dynamically indexed
+  // byte array in the kernel argument sends the whole ScoreParams to scratch.
   int32_t norders;
-  uint8_t order[kMaxOrders][kMaxProps];
+  uint64_t order[kMaxOrders];
   const uint8_t* oclass;  // per row: its order class (norders > 1)
   DevProp props[kMaxProps];
 };

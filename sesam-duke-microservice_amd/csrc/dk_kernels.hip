@@ -1132,7 +1132,7 @@ __device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, d
 // SYM: the owner slots of the symmetric dedup schedule (PairSource::sym): every owned pair
 // is scored in both directions in one pass and the two probabilities go to S.ores; the
 // emission pass (k_emit) turns them into the match list.
-template <int RMAX, int LR, bool SYM, bool DP, bool GR = true>
+template <int RMAX, int LR, bool SYM, bool DP, bool GR = true, bool GEO = false>
 __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
                                            uint64_t nslots, const StageOut& out) {
   uint64_t* peq = g_wave_tables[threadIdx.x >> 6];
@@ -1252,15 +1252,16 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   uint32_t qch_n = 0u;
   // Processor.compare visits r1's (the query's) properties in its RecordImpl HashMap order,
   // which depends on the map's capacity: the query row's order class (dk_schema.orders)
-  const int oc = P.norders > 1 ? (int)__builtin_amdgcn_readfirstlane((uint32_t)P.oclass[q]) : 0;
-  if (P.nprops > 0) prefetch(P.order[oc][0], lq_n, qch_n, lc_n);
+  const uint64_t ow =
+      order_word(P, P.norders > 1 ? (int)__builtin_amdgcn_readfirstlane((uint32_t)P.oclass[q]) : 0);
+  if (P.nprops > 0) prefetch(order_at(ow, 0), lq_n, qch_n, lc_n);
   for (int p = 0; p < P.nprops; ++p) {
-    const int pp = P.order[oc][p];
+    const int pp = order_at(ow, p);
     const DevProp& D = P.props[pp];
     const int lq = lq_n;
     const int lc = lc_n;
     const uint32_t qch = qch_n;
-    if (p + 1 < P.nprops) prefetch(P.order[oc][p + 1], lq_n, qch_n, lc_n);
+    if (p + 1 < P.nprops) prefetch(order_at(ow, p + 1), lq_n, qch_n, lc_n);
     if (lq == (int)kMissing) continue;  // r1 has no value: property skipped for the wave
     const bool present = lc != (int)kMissing;
     const bool cmp = present && lq > 0 && lc > 0;
@@ -1272,7 +1273,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
       if (cmp) bytes += 9u;   // rnum + rnumok
       rev = sim;
-    } else if (D.op == DK_CMP_GEOPOSITION) {
+    } else if (GEO && D.op == DK_CMP_GEOPOSITION) {
       if (cmp) sim = geoposition(D.num[2 * q], D.num[2 * q + 1], D.numok[q] != 0, D.rnum[2 * g], D.rnum[2 * g + 1],
                                  D.rnumok[g] != 0, D.min_ratio);
       if (cmp) bytes += 17u;  // rnum pair + rnumok
@@ -1347,6 +1348,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LR <= 8 ? D
 void k_score_long(const ScoreParams P, const PairSource S,
                                                     uint64_t slot0, uint64_t nslots, StageOut out) {
   score_body<RMAX, LR, false, true>(P, S, slot0, nslots, out);
+}
+
+// Schemas with a GeopositionComparator (P.has_geo; never the symmetric schedule): the direct
+// schedule's widest variants with the haversine compiled in -- the f64 sin / cos keep a
+// scratch frame for large-argument reduction, which only these variants carry.  Their
+// occupancy targets are the widest plain variants': long_dp is a called function, whose
+// register budget follows the most permissive of its callers.
+template <bool DP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_score_geo(const ScoreParams P, const PairSource S, uint64_t slot0,
+                                                   uint64_t nslots, StageOut out) {
+  score_body<64, 0, false, DP, true, true>(P, S, slot0, nslots, out);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_LONG16, 8))) void k_score_long_geo(const ScoreParams P, const PairSource S, uint64_t slot0,
+                                                        uint64_t nslots, StageOut out) {
+  score_body<64, 16, false, true, true, true>(P, S, slot0, nslots, out);
 }
 
 // Emission pass of the symmetric dedup schedule: the query's slots in Duke's candidate
@@ -1450,20 +1467,36 @@ __global__ __launch_bounds__(256) void k_reduce_blocks(const StageOut st, uint64
   }
 }
 
-// Concatenate the per-block staged entries in block order (one block per score block).
+// Concatenate the per-block staged entries in block order.  A wave takes kCompactRun
+// consecutive staging blocks at a time: their counts in one read, then only the non-empty
+// blocks' entries, 64 per step (a launch of one workgroup per staging block spent most of
+// its time dispatching workgroups with nothing to copy: sparse match lists, configs[2]).
+constexpr int kCompactRun = 16;
+
 __global__ __launch_bounds__(256) void k_compact(const StageOut st, const uint64_t* __restrict__ boff,
-                                                 uint64_t base, MatchList out) {
-  const uint32_t b = blockIdx.x;
-  const uint32_t n = st.bcnt[b];
-  const uint32_t i = threadIdx.x;
-  if (i >= n) return;
-  const uint64_t src = (uint64_t)b * kScoreBlock + i;
-  const uint64_t dst = base + boff[b] + i;
-  const uint32_t w = st.cand[src];
-  out.cand[dst] = w & ((1u << kKindShift) - 1u);
-  out.kind[dst] = (uint8_t)(w >> kKindShift);
-  out.prob[dst] = st.prob[src];
-  out.qidx[dst] = st.qidx[src];
+                                                 uint64_t nblocks, uint64_t base, MatchList out) {
+  const uint32_t lane = lane_id();
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t b0 = wave * kCompactRun; b0 < nblocks; b0 += nwaves * kCompactRun) {
+    const uint64_t b = b0 + lane;
+    const uint32_t n = lane < (uint32_t)kCompactRun && b < nblocks ? st.bcnt[b] : 0u;
+    uint64_t m = __ballot(n != 0u);
+    while (m) {  // wave-uniform
+      const int l = __builtin_ctzll(m);
+      m &= m - 1ull;
+      const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane((int)n, l);
+      const uint64_t src0 = (b0 + (uint64_t)l) * kScoreBlock;
+      const uint64_t dst0 = base + boff[b0 + (uint64_t)l];
+      for (uint32_t i = lane; i < cnt; i += 64) {
+        const uint32_t w = st.cand[src0 + i];
+        out.cand[dst0 + i] = w & ((1u << kKindShift) - 1u);
+        out.kind[dst0 + i] = (uint8_t)(w >> kKindShift);
+        out.prob[dst0 + i] = st.prob[src0 + i];
+        out.qidx[dst0 + i] = st.qidx[src0 + i];
+      }
+    }
+  }
 }
 
 // first[i] = first entry of query i (entries are grouped by query index, ascending)
@@ -2213,7 +2246,12 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
   } while (0)
 #define DK_LONG(RM, L) k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
   if (src.sym && P.long_rows > 0) return hipErrorInvalidValue;  // the host never schedules it
-  if (!P.has_dp) {
+  if (P.has_geo) {
+    if (src.sym) return hipErrorInvalidValue;  // the host never schedules it (sym_schema_ok)
+    if (!P.has_dp) k_score_geo<false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+    else if (P.long_rows > 0) k_score_long_geo<<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+    else k_score_geo<true><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  } else if (!P.has_dp) {
     if (src.sym) k_score_nodp<true><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
     else k_score_nodp<false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
   } else if (P.long_rows > 0) {
@@ -2241,7 +2279,9 @@ hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_
 hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nblocks,
                           uint64_t base, const MatchList& out, hipStream_t s) {
   DK_LAUNCH_GUARD(nblocks);
-  k_compact<<<(unsigned)nblocks, kScoreBlock, 0, s>>>(st, boff, base, out);
+  const uint64_t runs = (nblocks + kCompactRun - 1) / kCompactRun;   // one per wave
+  const unsigned grid = (unsigned)std::min<uint64_t>((runs + 3) / 4, 8192);
+  k_compact<<<grid, 256, 0, s>>>(st, boff, nblocks, base, out);
   return hipGetLastError();
 }
 

@@ -245,14 +245,15 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
     }
   }
   // Processor.compare's visiting order for this query (its RecordImpl HashMap's order class)
-  const int oc = P.norders > 1 ? (int)__builtin_amdgcn_readfirstlane((uint32_t)P.oclass[q]) : 0;
+  const uint64_t ow =
+      order_word(P, P.norders > 1 ? (int)__builtin_amdgcn_readfirstlane((uint32_t)P.oclass[q]) : 0);
   Cand cn = resolve(0);
   uint64_t rid_n;
   uint64_t rk_n[kPreKeys];
   uint32_t crow_n;
   load_filters(cn, rid_n, rk_n, crow_n);
   PreOps nx;
-  load_ops(op_res(gp, P.order[oc][0]), cn.g, cn.valid, nx);
+  load_ops(op_res(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
 
   // the query's bigram sets in its perfect-hash tables (one per bigram property)
   for (int e = (int)lane * 4; e < kGroupedTabs * kTabWords; e += 256)
@@ -301,7 +302,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
     double prob = 0.5;
     uint32_t by = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
     for (int k = 0; k < P.nprops; ++k) {
-      const int p = P.order[oc][k];
+      const int p = order_at(ow, k);
       const DevProp& D = P.props[p];
       const PreOps o = nx;
       const bool isq = D.op == DK_CMP_QGRAM;
@@ -326,11 +327,11 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
       // the next step's operands: property p+1 of this group, or the next group's
       // positions, filters and property 0
       if (k + 1 < P.nprops) {
-        load_ops(op_res(gp, P.order[oc][k + 1]), c.g, c.valid, nx);
+        load_ops(op_res(gp, order_at(ow, k + 1)), c.g, c.valid, nx);
       } else if (grp + 1 < ngroups) {
         cn = resolve(grp + 1);
         load_filters(cn, rid_n, rk_n, crow_n);
-        load_ops(op_res(gp, P.order[oc][0]), cn.g, cn.valid, nx);
+        load_ops(op_res(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
       }
       const int tslot = (int)gp[p].tslot;
       if (lq == kMissing) continue;  // r1 has no value: property skipped for the wave

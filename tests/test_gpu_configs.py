@@ -438,7 +438,24 @@ def test_two_engines_tiles_equal_single_engine():
 
 @pytest.mark.parametrize("mode,ndev", [("dedup", 2), ("dedup", 3), ("linkage", 2)])
 def test_multi_device_ctx_equals_single_ctx(mode, ndev):
-    """dk_create_multi over `ndev` entries of device 0 (one stream set each): the replicated
+    _multi_device_case(mode, [0] * ndev)
+
+
+@pytest.mark.parametrize("mode", ["dedup", "linkage"])
+def test_multi_device_distinct_gpus(mode):
+    """The same over two physically different GPUs: the group's pinned match list
+    (hipHostMallocPortable) is filled by copies from both devices' streams, and the
+    cost-balanced tiles run on separate devices.  Runs only where two GPUs are visible (the
+    round-end 8-GPU node; the 1-GPU box skips it)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs")
+    _multi_device_case(mode, [0, 1])
+
+
+def _multi_device_case(mode, devices):
+    """dk_create_multi over `devices` (one stream set each; repeated entries of device 0 on a
+    one-GPU box): the replicated
     index takes the same batches (re-posted IDs, deleted rows, a rejected batch, transient
     query rows), and every match -- its queries split into cost-balanced tiles matched
     concurrently -- equals the single-ctx list bit for bit, as do candidate counts, compare
@@ -452,8 +469,8 @@ def test_multi_device_ctx_equals_single_ctx(mode, ndev):
     group = np.where(np.arange(n) % 3 == 0, 1, 2).astype(np.uint8) if mode == "linkage" else None
     sch = schema_of(props, 0.9, 0.7, mode, 2)
     one = dh.GpuEngine(sch)
-    many = dh.GpuEngine(sch, devices=[0] * ndev)
-    assert many.num_devices == ndev and one.num_devices == 1
+    many = dh.GpuEngine(sch, devices=list(devices))
+    assert many.num_devices == len(devices) and one.num_devices == 1
 
     def up(e, a, b, transient=False, bad=False):
         cols = [dh.Column.from_strings(v[a:b]) for v in vals]

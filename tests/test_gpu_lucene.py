@@ -272,3 +272,33 @@ def test_lucene_stats_needs_lucene_source():
     assert eng.lib.dk_lucene_merge(eng.ctx) == A.DK_E_STATE
     assert eng.lib.dk_lucene_set_stats(eng.ctx, 7) == A.DK_E_INVALID
     eng.close()
+
+
+def test_reposted_id_ranks_differently_merged_vs_unmerged():
+    """tests/test_lucene.py's re-post case through the device: under MERGED (the
+    default) Q's second hit is A, under UNMERGED it is B -- the superseded "anna" versions
+    count in docFreq -- each equal to the restatement's pair list.  Which mode matches the
+    reference depends on when its IndexWriter merges: both are approximations (INTEGRATION.md
+    §5, parity unpinned)."""
+    from test_lucene import REPOST_NAMES, REPOST_CITY, REPOST_ALIVE
+    props = [{"comparator": A.CMP_EXACT, "low": 0.3, "high": 0.9},
+             {"comparator": A.CMP_EXACT, "low": 0.3, "high": 0.9}]
+    vals = [REPOST_NAMES, REPOST_CITY]
+    ident = np.array(list(range(9)) + [5, 6, 7, 8], np.uint64)
+    sch = schema_of(props, 0.01, 0.0, "dedup", 0)
+    A.lucene_source(sch, [0, 1], 2, 0.0)
+    eng = dh.GpuEngine(sch)
+    upsert(eng, vals, ident, 0, 9)
+    upsert(eng, vals, ident, 9, 13)
+    q = np.array([0], np.uint32)
+    got = {}
+    for unmerged in (False, True):
+        eng.lucene_stats(unmerged=unmerged)
+        ref = R.LuceneIndexRef(["f0", "f1"], 2, 0.0)
+        ref.set_docs(vals, REPOST_ALIVE, in_stats=[True] * 13 if unmerged else None)
+        res = eng.match(q)
+        check(res, *expected_with(ref, props, vals, [0, 1], ident, q, 0.01, 0.0))
+        got[unmerged] = list(res.candidate)
+        res.close()
+    assert got == {False: [1], True: [2]}
+    eng.close()

@@ -84,3 +84,26 @@ def test_options_from_environment():
     assert (o.max_hits, o.min_relevance) == (20, 0.5)
     with pytest.raises(Exception):
         LuceneOptions.from_env({"FUZZY_SEARCH": "true"}).check()
+
+
+# A re-posted ID under the two statistics modes: Q, A and B are indexed; four IDs
+# first posted with name "anna" are re-posted as "finn".  Live versions alone (MERGED, the
+# default): "anna" is in 2 documents and "oslo" in 4, so A (anna) outranks B (oslo) for Q.
+# Counting the superseded versions too (UNMERGED, Lucene 4's deleted-but-unmerged documents):
+# "anna" is in 6, so B outranks A, and with max_hits 2 the hit lists differ.
+REPOST_NAMES = ["anna", "anna", "berit", "dag", "erik", "anna", "anna", "anna", "anna",
+                "finn", "finn", "finn", "finn"]
+REPOST_CITY = ["oslo", "bergen", "oslo", "oslo", "oslo"] + ["trondheim"] * 8
+REPOST_ALIVE = [True] * 5 + [False] * 4 + [True] * 4       # rows 5..8 superseded by 9..12
+
+
+def repost_hits(unmerged):
+    ref = R.LuceneIndexRef(["name", "city"], max_hits=2, min_relevance=0.0)
+    ref.set_docs([REPOST_NAMES, REPOST_CITY], REPOST_ALIVE,
+                 in_stats=[True] * len(REPOST_NAMES) if unmerged else None)
+    return ref.candidates(0)
+
+
+def test_reposted_id_ranks_differently_merged_vs_unmerged():
+    assert repost_hits(unmerged=False) == [0, 1]   # Q itself, then A
+    assert repost_hits(unmerged=True) == [0, 2]    # Q itself, then B
