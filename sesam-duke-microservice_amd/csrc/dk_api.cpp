@@ -2170,15 +2170,14 @@ static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
 static bool grouped_schema_ok(const ScoreParams& P) {
   const char* e = getenv("DK_GROUPED");
   if ((e && e[0] == '0') || P.has_dp || P.raw_prop >= 0 || P.nprops < 1) return false;
-  // every buffer offset of the kernel's raw buffer loads (u32) below 2^32, the rows a tail
-  // step reads past a property's last row included (they must stay out of range, not wrap)
+  // every offset of the kernel's raw buffer loads below 2^31 (a row of w has its own
+  // buffer resource, so the replica's rows do not add up)
   if (P.rstride * 8 >= (1ull << 31)) return false;
   int tabs = 0;
   for (int p = 0; p < P.nprops; ++p) {
     const DevProp& D = P.props[p];
     if (D.op == DK_CMP_QGRAM) {
       if (!D.g16 || D.rgrows < 1 || D.width != 1) return false;
-      if ((uint64_t)(D.rgrows + 8) * P.rstride * 8 >= (1ull << 32)) return false;
       ++tabs;
     } else if (D.op != DK_CMP_NUMERIC && D.op != DK_CMP_NONE) {
       return false;
@@ -2205,14 +2204,14 @@ static std::vector<GroupedProp> grouped_props(const ScoreParams& P) {
       G.x_n = (uint32_t)(n * 2);
       G.xsh = 1;
       G.w = D.rgrams;
-      G.w_n = (uint32_t)((uint64_t)D.rgrows * n * 8);
+      G.w_rows = (uint32_t)D.rgrows;
       G.rowb = (uint32_t)(n * 8);
     } else if (D.op == DK_CMP_NUMERIC) {
       G.x = D.rnumok;
       G.x_n = (uint32_t)n;
       G.w = D.rnum;
-      G.w_n = (uint32_t)(n * 8);
-      G.rowb = 0x80000000u;
+      G.w_rows = 1;
+      G.rowb = (uint32_t)(n * 8);
     }
   }
   return gp;
@@ -2540,8 +2539,13 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   // k_score_grouped: the tasks of each chunk in the order of their first candidate's replica
   // position (bucket by bucket), DK_TASK_SORT=0: slot order (A/B)
   const uint32_t* perm = nullptr;
+  bool row_res = false;  // k_score_grouped<true>: a resource per key-word row
   if (grouped) {
     const std::vector<GroupedProp> gp = grouped_props(P);
+    // one resource per property while its rows (and the tail rows read past them) stay
+    // below 2^32 bytes of offset
+    for (const GroupedProp& G : gp)
+      if ((uint64_t)(G.w_rows + 8) * G.rowb >= (1ull << 32)) row_res = true;
     HIPCHK(c->gprops.reserve(gp.size() * sizeof(GroupedProp), 0, s));
     HIPCHK(hipMemcpyAsync(c->gprops.p, gp.data(), gp.size() * sizeof(GroupedProp), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));  // gp is a temporary
@@ -2658,7 +2662,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       {
         Timer t_score(c, &c->prof.ms_score, s);
         if (grouped)
-          HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), st[b], s));
+          HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), row_res, st[b], s));
         else HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
         t_score.stop();
       }

@@ -195,9 +195,9 @@ struct GroupedProp {
   const void* len;    // rlen (u16 per position)
   const void* x;      // QGram: rgcnt (u16; its low byte); Numeric: rnumok (u8)
   const void* w;      // QGram: rgrams rows (u64 key words); Numeric: rnum
-  uint32_t len_n, x_n, w_n;
-  uint32_t rowb;      // bytes between key-word rows (QGram); 0x80000000 (Numeric: rows >= 1
-                      // are out of range)
+  uint32_t len_n, x_n;
+  uint32_t w_rows;    // rows of w: QGram rgrows, Numeric 1 (rnum), none 0
+  uint32_t rowb;      // bytes per row of w (replica positions x 8)
   uint32_t xsh;       // x element = 1 << xsh bytes
   uint32_t tslot;     // QGram: the query table of this property (rank among the QGram ones)
   uint32_t pad[4];
@@ -399,9 +399,10 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
                         uint64_t nslots, const StageOut& out, hipStream_t s);
 // k_score_grouped: slot0 and nslots multiples of kScoreBlock, slots padded per query to it;
 // perm (or NULL: task order) = the tasks in execution order (k_task_keys, sorted)
+// row_res: one buffer resource per key-word row (replicas whose rows pass 2^32 bytes)
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                                 uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
-                                const StageOut& out, hipStream_t s);
+                                bool row_res, const StageOut& out, hipStream_t s);
 // key[t] = chunk << 32 | first candidate's replica position of task t, val[t] = t;
 // cb[0..nchunks] = first task of each chunk
 hipError_t launch_task_keys(const PairSource& src, uint64_t ntask, const uint64_t* cb, int nchunks,

@@ -68,13 +68,17 @@ struct PreOps {
 };
 
 // Per-property buffer resources of the candidate operands (wave-uniform), from the host's
-// GroupedProp record.  Key-word row j of a bigram property is at byte g * 8 + j * rowb of one
-// resource sized rgrows rows, so a row past the property's rows is out of range; a Numeric
-// property's value is "row 0" and its other rows are pushed out of range.  Every offset
-// stays below 2^32 (the host checks the sizes).
+// GroupedProp record.  Key-word row j of a bigram property (a Numeric property's value is
+// its row 0) sits at byte g * 8 + j * rowb of w.  ROW = false: one resource over the
+// property's rows, offsets below 2^32 (the host checks, tail rows included), so a row past
+// the property's rows is out of range (0, no data moved).  ROW = true (replicas past that,
+// configs[2] at 10M x 10M: 40M positions x 8 B per row): each row read through a resource
+// of its own, based at w + j * rowb, one row long or empty past the rows -- more scalar
+// work per load (1M x 1M: -9 %), offsets g * 8 < 2^31 however many rows.
 struct OpRes {
   rsrc_t len, x, w;
-  uint32_t rowb, xsh;
+  const char* wb;
+  uint32_t rowb, rows, xsh;
 };
 
 __device__ __forceinline__ OpRes op_res(const GroupedProp* gp, int p) {
@@ -82,25 +86,38 @@ __device__ __forceinline__ OpRes op_res(const GroupedProp* gp, int p) {
   OpRes r;
   r.len = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.len), (short)0, (int)G.len_n, kRsrcWord3);
   r.x = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.x), (short)0, (int)G.x_n, kRsrcWord3);
-  r.w = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.w), (short)0, (int)G.w_n, kRsrcWord3);
+  r.wb = static_cast<const char*>(G.w);
   r.rowb = G.rowb;
+  r.rows = G.w_rows;
+  r.w = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.w), (short)0, (int)(G.w_rows * G.rowb), kRsrcWord3);
   r.xsh = G.xsh;
   return r;
 }
 
+template <bool ROW>
 __device__ __forceinline__ uint64_t ld_row(const OpRes& R, int j, uint32_t g) {
-  const uint32_t jb = (uint32_t)j * R.rowb;  // Numeric: rowb = 2^31, so rows >= 1 are out of range
-  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.w, g * 8u + jb, 0, 0));
+  if (!ROW)
+    return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.w, g * 8u + (uint32_t)j * R.rowb, 0, 0));
+  // the row's base and size are wave-uniform (readfirstlane keeps the resource in SGPRs: a
+  // resource in VGPRs would make the load a waterfall loop)
+  const uint64_t at = (uint64_t)(uintptr_t)R.wb + (uint64_t)(uint32_t)j * R.rowb;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)at);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(at >> 32));
+  const uint32_t nb = __builtin_amdgcn_readfirstlane((uint32_t)j < R.rows ? R.rowb : 0u);
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((uintptr_t)(((uint64_t)hi << 32) | lo)), (short)0, (int)nb, kRsrcWord3);
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rs, g * 8u, 0, 0));
 }
 
 // property p's candidate operands at replica position g (lanes without a pair read
 // position 0), all loads unconditional
+template <bool ROW>
 __device__ __forceinline__ void load_ops(const OpRes& R, uint32_t g, bool valid, PreOps& o) {
   const uint32_t lc = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(R.len, g * 2u, 0, 0);
   o.lc = valid ? lc : (uint32_t)kMissing;
   o.x = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(R.x, g << R.xsh, 0, 0);
 #pragma unroll
-  for (int j = 0; j < kPreRows; ++j) o.w[j] = ld_row(R, j, g);
+  for (int j = 0; j < kPreRows; ++j) o.w[j] = ld_row<ROW>(R, j, g);
 }
 
 // |Q ∩ C| of one bigram key word (four 16-bit keys) against the query's perfect-hash table
@@ -161,6 +178,7 @@ __device__ __forceinline__ uint64_t grouped_task(const uint32_t* perm, uint64_t 
   return perm ? (uint64_t)perm[task0 + e] - task0 : e;
 }
 
+template <bool ROW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_GROUPED, 8)))
 void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots,
                      const uint32_t* __restrict__ perm, const GroupedProp* __restrict__ gp,
@@ -253,7 +271,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
   uint32_t crow_n;
   load_filters(cn, rid_n, rk_n, crow_n);
   PreOps nx;
-  load_ops(op_res(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
+  load_ops<ROW>(op_res(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
 
   // the query's bigram sets in its perfect-hash tables (one per bigram property)
   for (int e = (int)lane * 4; e < kGroupedTabs * kTabWords; e += 256)
@@ -322,16 +340,16 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
       uint64_t ex[kPreRows];
       if (njw > kPreRows) {
 #pragma unroll
-        for (int j = 0; j < kPreRows; ++j) ex[j] = ld_row(R, kPreRows + j, c.g);
+        for (int j = 0; j < kPreRows; ++j) ex[j] = ld_row<ROW>(R, kPreRows + j, c.g);
       }
       // the next step's operands: property p+1 of this group, or the next group's
       // positions, filters and property 0
       if (k + 1 < P.nprops) {
-        load_ops(op_res(gp, order_at(ow, k + 1)), c.g, c.valid, nx);
+        load_ops<ROW>(op_res(gp, order_at(ow, k + 1)), c.g, c.valid, nx);
       } else if (grp + 1 < ngroups) {
         cn = resolve(grp + 1);
         load_filters(cn, rid_n, rk_n, crow_n);
-        load_ops(op_res(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
+        load_ops<ROW>(op_res(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
       }
       const int tslot = (int)gp[p].tslot;
       if (lq == kMissing) continue;  // r1 has no value: property skipped for the wave
@@ -362,7 +380,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
             for (int j = 2 * kPreRows; j < njw; j += kTailRows) {
               uint64_t w[kTailRows];
 #pragma unroll
-              for (int i = 0; i < kTailRows; ++i) w[i] = ld_row(R, j + i, c.g);
+              for (int i = 0; i < kTailRows; ++i) w[i] = ld_row<ROW>(R, j + i, c.g);
 #pragma unroll
               for (int i = 0; i < kTailRows; ++i)
                 if (j + i < njw) common += probe_word(tab, w[i], mult, sh);
@@ -404,12 +422,13 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
 
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                                 uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
-                                const StageOut& out, hipStream_t s) {
+                                bool row_res, const StageOut& out, hipStream_t s) {
   if (nslots == 0) return hipSuccess;
   if (nslots % kScoreBlock || slot0 % kScoreBlock) return hipErrorInvalidValue;
   const uint64_t ntask = nslots / kScoreBlock;
   const uint64_t grid = (ntask + kScoreBlock / 64 - 1) / (kScoreBlock / 64);
-  k_score_grouped<<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
+  if (row_res) k_score_grouped<true><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
+  else k_score_grouped<false><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
   return hipGetLastError();
 }
 
