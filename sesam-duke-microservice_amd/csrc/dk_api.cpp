@@ -2546,6 +2546,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     // below 2^32 bytes of offset
     for (const GroupedProp& G : gp)
       if ((uint64_t)(G.w_rows + 8) * G.rowb >= (1ull << 32)) row_res = true;
+    const char* er = getenv("DK_GROUPED_ROW");  // 1: the per-row form at any size (tests)
+    if (er && er[0] == '1') row_res = true;
     HIPCHK(c->gprops.reserve(gp.size() * sizeof(GroupedProp), 0, s));
     HIPCHK(hipMemcpyAsync(c->gprops.p, gp.data(), gp.size() * sizeof(GroupedProp), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));  // gp is a temporary
