@@ -71,17 +71,23 @@ __device__ __forceinline__ void qgram_row(const GramJob& J, uint64_t i) {
       u += first ? 1 : 0;
     }
   } else {
-    // a long value: its raw codes in its scratch run, insertion-sorted there
+    // a long value: its raw codes in its scratch run, Shell-sorted there (Ciura's gaps:
+    // a 254-gram text value takes ~2k compares instead of insertion sort's ~16k)
     uint64_t* r = J.scratch + J.soff[i];
     if (!WRITE) {
-      for (int ix = 0; ix < m; ++ix) {
-        const uint64_t x = gram_code(s, L, ix, J.q, J.tokenizer);
-        int k = ix - 1;
-        while (k >= 0 && r[k] > x) {
-          r[k + 1] = r[k];
-          --k;
+      for (int ix = 0; ix < m; ++ix) r[ix] = gram_code(s, L, ix, J.q, J.tokenizer);
+      constexpr int kGaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
+      for (int gi = 0; gi < 8; ++gi) {
+        const int gap = kGaps[gi];
+        for (int ix = gap; ix < m; ++ix) {
+          const uint64_t x = r[ix];
+          int k = ix;
+          while (k >= gap && r[k - gap] > x) {
+            r[k] = r[k - gap];
+            k -= gap;
+          }
+          r[k] = x;
         }
-        r[k + 1] = x;
       }
     }
     for (int ix = 0; ix < m; ++ix) {
