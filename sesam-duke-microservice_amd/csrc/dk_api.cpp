@@ -2170,9 +2170,11 @@ static bool sym_schema_ok(const dk_ctx* c, const ScoreParams& P) {
 static bool grouped_schema_ok(const ScoreParams& P) {
   const char* e = getenv("DK_GROUPED");
   if ((e && e[0] == '0') || P.has_dp || P.raw_prop >= 0 || P.nprops < 1) return false;
-  // every offset of the kernel's raw buffer loads below 2^31 (a row of w has its own
-  // buffer resource, so the replica's rows do not add up)
+  // every offset of the kernel's raw buffer loads below 2^31 (a tail row of w has its own
+  // buffer resource, so the replica's rows do not add up), and the head rows (read for
+  // every pair through one resource) under 4 GiB
   if (P.rstride * 8 >= (1ull << 31)) return false;
+  if (P.rstride * 8 * kGroupedHeadRows >= (1ull << 32)) return false;
   int tabs = 0;
   for (int p = 0; p < P.nprops; ++p) {
     const DevProp& D = P.props[p];
@@ -2205,12 +2207,14 @@ static std::vector<GroupedProp> grouped_props(const ScoreParams& P) {
       G.xsh = 1;
       G.w = D.rgrams;
       G.w_rows = (uint32_t)D.rgrows;
+      G.w_head = G.w_rows;
       G.rowb = (uint32_t)(n * 8);
     } else if (D.op == DK_CMP_NUMERIC) {
       G.x = D.rnumok;
       G.x_n = (uint32_t)n;
       G.w = D.rnum;
       G.w_rows = 1;
+      G.w_head = 1;
       G.rowb = (uint32_t)(n * 8);
     }
   }
@@ -2541,13 +2545,19 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   const uint32_t* perm = nullptr;
   bool row_res = false;  // k_score_grouped<true>: a resource per key-word row
   if (grouped) {
-    const std::vector<GroupedProp> gp = grouped_props(P);
+    std::vector<GroupedProp> gp = grouped_props(P);
     // one resource per property while its rows (and the tail rows read past them) stay
     // below 2^32 bytes of offset
     for (const GroupedProp& G : gp)
       if ((uint64_t)(G.w_rows + 8) * G.rowb >= (1ull << 32)) row_res = true;
     const char* er = getenv("DK_GROUPED_ROW");  // 1: the per-row form at any size (tests)
     if (er && er[0] == '1') row_res = true;
+    if (row_res) {  // the head rows' resource: the rows under 4 GiB
+      for (GroupedProp& G : gp) {  // >= kGroupedHeadRows of them (grouped_schema_ok)
+        const uint64_t fit = G.rowb ? ((1ull << 32) - 1) / G.rowb : 0;
+        G.w_head = (uint32_t)std::min<uint64_t>(G.w_rows, fit);
+      }
+    }
     HIPCHK(c->gprops.reserve(gp.size() * sizeof(GroupedProp), 0, s));
     HIPCHK(hipMemcpyAsync(c->gprops.p, gp.data(), gp.size() * sizeof(GroupedProp), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));  // gp is a temporary

@@ -200,9 +200,11 @@ struct GroupedProp {
   uint32_t rowb;      // bytes per row of w (replica positions x 8)
   uint32_t xsh;       // x element = 1 << xsh bytes
   uint32_t tslot;     // QGram: the query table of this property (rank among the QGram ones)
-  uint32_t pad[4];
+  uint32_t w_head;    // rows of w under the first resource (all of them unless they pass 4 GiB)
+  uint32_t pad[3];
 };
 static_assert(sizeof(GroupedProp) == 64, "two s_load_dwordx8");
+constexpr int kGroupedHeadRows = 4;  // k_score_grouped reads rows [0, 2 DK_GROUPED_ROWS) per pair
 
 // The emission pass of the symmetric schedule: slots of the full candidate order (qoff /
 // wq / ranges as in PairSource) read their probability from the owner results.

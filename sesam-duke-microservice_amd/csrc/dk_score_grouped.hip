@@ -40,6 +40,7 @@ namespace dk {
 
 constexpr int kTaskGroups = kScoreBlock / 64;  // groups of 64 slots per task
 constexpr int kPreRows = DK_GROUPED_ROWS;
+static_assert(2 * kPreRows <= kGroupedHeadRows, "the head rows' resource covers rows < kGroupedHeadRows");
 constexpr int kTabWords = 512;  // u32 per bigram table (lt <= 9)
 constexpr int kPreKeys = DK_GROUPED_KEYS;  // key-function filters loaded one step ahead
 constexpr int kTailRows = DK_GROUPED_TAIL;
@@ -74,7 +75,9 @@ struct PreOps {
 // the property's rows is out of range (0, no data moved).  ROW = true (replicas past that,
 // configs[2] at 10M x 10M: 40M positions x 8 B per row): each row read through a resource
 // of its own, based at w + j * rowb, one row long or empty past the rows -- more scalar
-// work per load (1M x 1M: -9 %), offsets g * 8 < 2^31 however many rows.
+// work per load, offsets g * 8 < 2^31 however many rows -- only for the tail rows: the
+// head rows (the first 2 kPreRows, read for every pair) come from one resource over the
+// rows that fit under 4 GiB (w_head >= 2 kPreRows, host-checked).
 struct OpRes {
   rsrc_t len, x, w;
   const char* wb;
@@ -89,9 +92,14 @@ __device__ __forceinline__ OpRes op_res(const GroupedProp* gp, int p) {
   r.wb = static_cast<const char*>(G.w);
   r.rowb = G.rowb;
   r.rows = G.w_rows;
-  r.w = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.w), (short)0, (int)(G.w_rows * G.rowb), kRsrcWord3);
+  r.w = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.w), (short)0, (int)(G.w_head * G.rowb), kRsrcWord3);
   r.xsh = G.xsh;
   return r;
+}
+
+// head rows j < 2 kPreRows: the first resource, in either form
+__device__ __forceinline__ uint64_t ld_row_head(const OpRes& R, int j, uint32_t g) {
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.w, g * 8u + (uint32_t)j * R.rowb, 0, 0));
 }
 
 template <bool ROW>
@@ -117,7 +125,7 @@ __device__ __forceinline__ void load_ops(const OpRes& R, uint32_t g, bool valid,
   o.lc = valid ? lc : (uint32_t)kMissing;
   o.x = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(R.x, g << R.xsh, 0, 0);
 #pragma unroll
-  for (int j = 0; j < kPreRows; ++j) o.w[j] = ld_row<ROW>(R, j, g);
+  for (int j = 0; j < kPreRows; ++j) o.w[j] = ld_row_head(R, j, g);
 }
 
 // |Q ∩ C| of one bigram key word (four 16-bit keys) against the query's perfect-hash table
@@ -340,7 +348,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
       uint64_t ex[kPreRows];
       if (njw > kPreRows) {
 #pragma unroll
-        for (int j = 0; j < kPreRows; ++j) ex[j] = ld_row<ROW>(R, kPreRows + j, c.g);
+        for (int j = 0; j < kPreRows; ++j) ex[j] = ld_row_head(R, kPreRows + j, c.g);
       }
       // the next step's operands: property p+1 of this group, or the next group's
       // positions, filters and property 0
