@@ -2543,19 +2543,24 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   // k_score_grouped: the tasks of each chunk in the order of their first candidate's replica
   // position (bucket by bucket), DK_TASK_SORT=0: slot order (A/B)
   const uint32_t* perm = nullptr;
-  bool row_res = false;  // k_score_grouped<true>: a resource per key-word row
+  int gmode = 0;  // k_score_grouped<MODE>: how the key-word rows are addressed
   if (grouped) {
     std::vector<GroupedProp> gp = grouped_props(P);
     // one resource per property while its rows (and the tail rows read past them) stay
     // below 2^32 bytes of offset
     for (const GroupedProp& G : gp)
-      if ((uint64_t)(G.w_rows + 8) * G.rowb >= (1ull << 32)) row_res = true;
-    const char* er = getenv("DK_GROUPED_ROW");  // 1: the per-row form at any size (tests)
-    if (er && er[0] == '1') row_res = true;
-    if (row_res) {  // the head rows' resource: the rows under 4 GiB
-      for (GroupedProp& G : gp) {  // >= kGroupedHeadRows of them (grouped_schema_ok)
+      if ((uint64_t)(G.w_rows + 8) * G.rowb >= (1ull << 32)) gmode = 1;
+    const char* er = getenv("DK_GROUPED_ROW");  // 1 / 2: that form at any size (tests)
+    if (er && (er[0] == '1' || er[0] == '2')) gmode = er[0] - '0';
+    if (gmode) {
+      for (GroupedProp& G : gp) {
+        // the head rows' resource: the rows under 4 GiB (>= kGroupedHeadRows of them,
+        // grouped_schema_ok); the tail rows' one, or a resource per tail row past 4 GiB
         const uint64_t fit = G.rowb ? ((1ull << 32) - 1) / G.rowb : 0;
         G.w_head = (uint32_t)std::min<uint64_t>(G.w_rows, fit);
+        const uint64_t tail = G.w_rows > (uint32_t)kGroupedHeadRows ? (uint64_t)(G.w_rows - kGroupedHeadRows) * G.rowb : 0;
+        if (tail >= (1ull << 32)) gmode = 2;
+        G.w_tailb = (uint32_t)std::min<uint64_t>(tail, 0xFFFFFFFFull);
       }
     }
     HIPCHK(c->gprops.reserve(gp.size() * sizeof(GroupedProp), 0, s));
@@ -2674,7 +2679,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       {
         Timer t_score(c, &c->prof.ms_score, s);
         if (grouped)
-          HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), row_res, st[b], s));
+          HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), gmode, st[b], s));
         else HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
         t_score.stop();
       }

@@ -201,7 +201,9 @@ struct GroupedProp {
   uint32_t xsh;       // x element = 1 << xsh bytes
   uint32_t tslot;     // QGram: the query table of this property (rank among the QGram ones)
   uint32_t w_head;    // rows of w under the first resource (all of them unless they pass 4 GiB)
-  uint32_t pad[3];
+  uint32_t w_tailb;   // k_score_grouped<1>: bytes of the tail rows' resource (rows past the
+                      // first kGroupedHeadRows)
+  uint32_t pad[2];
 };
 static_assert(sizeof(GroupedProp) == 64, "two s_load_dwordx8");
 constexpr int kGroupedHeadRows = 4;  // k_score_grouped reads rows [0, 2 DK_GROUPED_ROWS) per pair
@@ -401,10 +403,11 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
                         uint64_t nslots, const StageOut& out, hipStream_t s);
 // k_score_grouped: slot0 and nslots multiples of kScoreBlock, slots padded per query to it;
 // perm (or NULL: task order) = the tasks in execution order (k_task_keys, sorted)
-// row_res: one buffer resource per key-word row (replicas whose rows pass 2^32 bytes)
+// mode (replicas whose key-word rows pass 2^32 bytes): 0 one buffer resource per property;
+// 1 a head and a tail resource; 2 a resource per tail row (k_score_grouped<MODE>)
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                                 uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
-                                bool row_res, const StageOut& out, hipStream_t s);
+                                int mode, const StageOut& out, hipStream_t s);
 // key[t] = chunk << 32 | first candidate's replica position of task t, val[t] = t;
 // cb[0..nchunks] = first task of each chunk
 hipError_t launch_task_keys(const PairSource& src, uint64_t ntask, const uint64_t* cb, int nchunks,

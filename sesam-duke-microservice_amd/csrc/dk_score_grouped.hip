@@ -70,20 +70,22 @@ struct PreOps {
 
 // Per-property buffer resources of the candidate operands (wave-uniform), from the host's
 // GroupedProp record.  Key-word row j of a bigram property (a Numeric property's value is
-// its row 0) sits at byte g * 8 + j * rowb of w.  ROW = false: one resource over the
-// property's rows, offsets below 2^32 (the host checks, tail rows included), so a row past
-// the property's rows is out of range (0, no data moved).  ROW = true (replicas past that,
-// configs[2] at 10M x 10M: 40M positions x 8 B per row): each row read through a resource
-// of its own, based at w + j * rowb, one row long or empty past the rows -- more scalar
-// work per load, offsets g * 8 < 2^31 however many rows -- only for the tail rows: the
-// head rows (the first 2 kPreRows, read for every pair) come from one resource over the
-// rows that fit under 4 GiB (w_head >= 2 kPreRows, host-checked).
+// its row 0) sits at byte g * 8 + j * rowb of w.  MODE 0: one resource over the property's
+// rows, offsets below 2^32 (the host checks, tail rows included), so a row past the
+// property's rows is out of range (0, no data moved).  Replicas past that (configs[2] at
+// 10M x 10M: 40M positions x 8 B per row): the head rows (the first 2 kPreRows, read for
+// every pair) through one resource over the rows that fit under 4 GiB, and the tail rows
+// MODE 1: through one resource over the rows past the head (under 4 GiB; a tail row index
+// is clamped to the property's last row and its word masked, so no offset passes the
+// resource), or MODE 2: a resource per tail row, based at w + j * rowb, one row long or
+// empty past the rows (any size; more scalar work per load: 3 % at 1M x 1M).
 struct OpRes {
-  rsrc_t len, x, w;
+  rsrc_t len, x, w, t;
   const char* wb;
   uint32_t rowb, rows, xsh;
 };
 
+template <int MODE>
 __device__ __forceinline__ OpRes op_res(const GroupedProp* gp, int p) {
   const GroupedProp G = gp[p];
   OpRes r;
@@ -93,6 +95,10 @@ __device__ __forceinline__ OpRes op_res(const GroupedProp* gp, int p) {
   r.rowb = G.rowb;
   r.rows = G.w_rows;
   r.w = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(G.w), (short)0, (int)(G.w_head * G.rowb), kRsrcWord3);
+  if (MODE == 1)
+    r.t = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(static_cast<const char*>(G.w) + (uint64_t)kGroupedHeadRows * G.rowb), (short)0,
+        (int)G.w_tailb, kRsrcWord3);
   r.xsh = G.xsh;
   return r;
 }
@@ -102,10 +108,17 @@ __device__ __forceinline__ uint64_t ld_row_head(const OpRes& R, int j, uint32_t 
   return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.w, g * 8u + (uint32_t)j * R.rowb, 0, 0));
 }
 
-template <bool ROW>
+// tail rows j >= kGroupedHeadRows
+template <int MODE>
 __device__ __forceinline__ uint64_t ld_row(const OpRes& R, int j, uint32_t g) {
-  if (!ROW)
+  if (MODE == 0)
     return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.w, g * 8u + (uint32_t)j * R.rowb, 0, 0));
+  if (MODE == 1) {
+    const int jj = min(j, (int)R.rows - 1);
+    const uint64_t v = __builtin_bit_cast(
+        uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.t, g * 8u + (uint32_t)(jj - kGroupedHeadRows) * R.rowb, 0, 0));
+    return j < (int)R.rows ? v : 0ull;
+  }
   // the row's base and size are wave-uniform (readfirstlane keeps the resource in SGPRs: a
   // resource in VGPRs would make the load a waterfall loop)
   const uint64_t at = (uint64_t)(uintptr_t)R.wb + (uint64_t)(uint32_t)j * R.rowb;
@@ -119,7 +132,6 @@ __device__ __forceinline__ uint64_t ld_row(const OpRes& R, int j, uint32_t g) {
 
 // property p's candidate operands at replica position g (lanes without a pair read
 // position 0), all loads unconditional
-template <bool ROW>
 __device__ __forceinline__ void load_ops(const OpRes& R, uint32_t g, bool valid, PreOps& o) {
   const uint32_t lc = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(R.len, g * 2u, 0, 0);
   o.lc = valid ? lc : (uint32_t)kMissing;
@@ -186,7 +198,7 @@ __device__ __forceinline__ uint64_t grouped_task(const uint32_t* perm, uint64_t 
   return perm ? (uint64_t)perm[task0 + e] - task0 : e;
 }
 
-template <bool ROW>
+template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_GROUPED, 8)))
 void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots,
                      const uint32_t* __restrict__ perm, const GroupedProp* __restrict__ gp,
@@ -279,7 +291,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
   uint32_t crow_n;
   load_filters(cn, rid_n, rk_n, crow_n);
   PreOps nx;
-  load_ops<ROW>(op_res(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
+  load_ops(op_res<MODE>(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
 
   // the query's bigram sets in its perfect-hash tables (one per bigram property)
   for (int e = (int)lane * 4; e < kGroupedTabs * kTabWords; e += 256)
@@ -344,7 +356,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
       // prefetch (loads complete in order: waiting for these then never waits for that)
       const int m2 = cmp ? (int)(o.x & 0xFFu) : 0;
       const int njw = perfect ? wave_max_i32((m2 + 3) >> 2) : 0;  // key-word rows the wave needs
-      const OpRes R = op_res(gp, p);
+      const OpRes R = op_res<MODE>(gp, p);
       uint64_t ex[kPreRows];
       if (njw > kPreRows) {
 #pragma unroll
@@ -353,11 +365,11 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
       // the next step's operands: property p+1 of this group, or the next group's
       // positions, filters and property 0
       if (k + 1 < P.nprops) {
-        load_ops<ROW>(op_res(gp, order_at(ow, k + 1)), c.g, c.valid, nx);
+        load_ops(op_res<MODE>(gp, order_at(ow, k + 1)), c.g, c.valid, nx);
       } else if (grp + 1 < ngroups) {
         cn = resolve(grp + 1);
         load_filters(cn, rid_n, rk_n, crow_n);
-        load_ops<ROW>(op_res(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
+        load_ops(op_res<MODE>(gp, order_at(ow, 0)), cn.g, cn.valid, nx);
       }
       const int tslot = (int)gp[p].tslot;
       if (lq == kMissing) continue;  // r1 has no value: property skipped for the wave
@@ -388,7 +400,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
             for (int j = 2 * kPreRows; j < njw; j += kTailRows) {
               uint64_t w[kTailRows];
 #pragma unroll
-              for (int i = 0; i < kTailRows; ++i) w[i] = ld_row<ROW>(R, j + i, c.g);
+              for (int i = 0; i < kTailRows; ++i) w[i] = ld_row<MODE>(R, j + i, c.g);
 #pragma unroll
               for (int i = 0; i < kTailRows; ++i)
                 if (j + i < njw) common += probe_word(tab, w[i], mult, sh);
@@ -430,13 +442,14 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
 
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                                 uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
-                                bool row_res, const StageOut& out, hipStream_t s) {
+                                int mode, const StageOut& out, hipStream_t s) {
   if (nslots == 0) return hipSuccess;
   if (nslots % kScoreBlock || slot0 % kScoreBlock) return hipErrorInvalidValue;
   const uint64_t ntask = nslots / kScoreBlock;
   const uint64_t grid = (ntask + kScoreBlock / 64 - 1) / (kScoreBlock / 64);
-  if (row_res) k_score_grouped<true><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
-  else k_score_grouped<false><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
+  if (mode == 2) k_score_grouped<2><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
+  else if (mode == 1) k_score_grouped<1><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
+  else k_score_grouped<0><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
   return hipGetLastError();
 }
 
