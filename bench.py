@@ -131,11 +131,16 @@ def build_workload(args):
                          (("NAME", 0, 0, 2), ("DOB", None, 5, 10))])
     elif args.workload == "linkage":
         p, group = synth.linkage_persons(n)
+        # BIRTHYEAR's min-ratio rejects every non-equal year of 1930..2010 (2009 / 2010 =
+        # 0.99950 < 0.9996): with 0.9 every same-bucket pair had a near-constant 0.69 factor and
+        # the list held ~10 % of the scored pairs; the low / high values
+        # (SURVEY §8d names the comparators, not them) put the list near one entry per query
         w.update(desc=f"BASELINE configs[2]: person record linkage {n} x {len(group) - n}, QGram "
-                      "q=2 DICE/JACCARD + Numeric min-ratio 0.9, cross-group key blocking",
-                 props=[prop("NAME", A.CMP_QGRAM, 0.1, 0.95, q=2, formula=A.QGRAM_DICE),
-                        prop("ADDRESS", A.CMP_QGRAM, 0.2, 0.8, q=2, formula=A.QGRAM_JACCARD),
-                        prop("BIRTHYEAR", A.CMP_NUMERIC, 0.3, 0.7, min_ratio=0.9),
+                      "q=2 DICE/JACCARD + Numeric BIRTHYEAR (min-ratio 0.9996: equal years) / ZIP "
+                      "(min-ratio 0.9), cross-group key blocking",
+                 props=[prop("NAME", A.CMP_QGRAM, 0.1, 0.9, q=2, formula=A.QGRAM_DICE),
+                        prop("ADDRESS", A.CMP_QGRAM, 0.1, 0.8, q=2, formula=A.QGRAM_JACCARD),
+                        prop("BIRTHYEAR", A.CMP_NUMERIC, 0.2, 0.6, min_ratio=0.9996),
                         prop("ZIP", A.CMP_NUMERIC, 0.4, 0.75, min_ratio=0.9)],
                  values={"NAME": p["name"], "ADDRESS": p["address"], "BIRTHYEAR": p["birthyear"],
                          "ZIP": p["zip"]},
@@ -184,6 +189,14 @@ def build_workload(args):
                  values={"TEXT": texts, "TEXTGRAMS": texts},
                  keys=synth.keys_first_two_tokens(texts), group=group, mode=A.MODE_LINKAGE,
                  queries=np.arange(n, len(group)))
+    # the committed PMC summary this line's roofline reads (profiles/pmc_<key>.json) and the
+    # dominant kernel of the workload
+    w["pmc_key"] = {"dedup": "dedup_utf16" if args.utf16_frac else "dedup",
+                    "allpairs": f"allpairs_{args.comparator}"}.get(args.workload, args.workload)
+    w["kernel"] = {"dedup": "k_score<40,true,false> (symmetric owner schedule)",
+                   "linkage": "k_score_gq<2,2>", "allpairs": "k_score<16,false,*>",
+                   "longtext": "k_score_long<16,16>",
+                   "reference": "k_score (Lucene candidates)"}[args.workload]
     w["n"] = len(next(iter(w["values"].values())))
     w["nkeys"] = len(w["keys"])
     w["queries"] = np.asarray(w["queries"], dtype=np.uint32)
@@ -526,51 +539,57 @@ def main():
         pairs_launch = prof["pairs_scored"] / launches
         avg_launch_s = score_s / launches
         achieved = bpair * pairs_launch / avg_launch_s if avg_launch_s > 0 and bpair else 0.0
-        # a true lower bound of this schedule's bytes: every pair's CANDIDATE
+        # the bytes this schedule REQUESTS (VERDICT r3's bound): every scored pair's candidate
         # operands at their stored width (the kernel's own count, score_bytes) plus each
-        # query's operands once -- B_pair above charges the query side to every pair, which a
-        # kernel holding the query in LDS / registers does not read, so its fraction can pass 1
+        # query's operands once -- L2 serves part of these (the PMC's TCC hit rate), so this is
+        # a request-bandwidth fraction, not an HBM one
         qbytes = sum(d["bytes"] / 2.0 for d in bdetail.values()) if bdetail else 0.0
-        bound_launch = (prof["score_bytes"] + qbytes * len(queries) * args.steps) / launches
-        frac_bound = bound_launch / avg_launch_s / HBM_PEAK if avg_launch_s > 0 else None
-        # the kernel's own operand bytes (the query side LDS-resident, the symmetric schedule's
-        # candidate operands read once per pair): what the schedule actually has to move
+        request_launch = (prof["score_bytes"] + qbytes * len(queries) * args.steps) / launches
+        frac_request = request_launch / avg_launch_s / HBM_PEAK if avg_launch_s > 0 else None
         sched = prof["score_bytes"] / score_s if score_s > 0 else 0.0
+        # roofline.frac: the CALIBRATED-COUNTER HBM fraction of the dominant kernel -- the
+        # committed PMC summary of the kernel this workload runs (scripts/summarize_profiles.py:
+        # FETCH_SIZE x 2 + WRITE_SIZE per scored pair, the factor from
+        # profiles/r05/fetch_calib.json), at this run's pairs per launch, over the launch's
+        # HIP-event time.  Measured bytes over measured time: <= 1 by construction.
         traffic = None
         valu = None
-        # the kept PMC summary of this workload's scoring kernel (scripts/summarize_profiles.py)
-        pmc = os.path.join(ROOT, "profiles", f"pmc_k_score_{w['name']}.json")
-        if not os.path.exists(pmc):
-            pmc = os.path.join(ROOT, "profiles", "pmc_k_score.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                pj = json.load(f)
-            if pj.get("workload", "dedup") == w["name"]:
-                # the PMC run's HBM bytes per scored pair, at this run's pairs per launch
-                if pj.get("hbm_bytes_per_pair"):
-                    traffic = pj["hbm_bytes_per_pair"] * prof["pairs_scored"] / launches
-                else:
-                    traffic = pj.get("hbm_bytes_per_launch")
-                # VALU issue: wave-instructions per scored pair (SQ_INSTS_VALU of the PMC run)
-                # at this run's pairs and k_score time, against the chip's issue rate
-                # (1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction)
-                ipp = pj["counters"]["SQ_INSTS_VALU"] / pj["pairs_profiled"]
-                rate = ipp * prof["pairs_scored"] / score_s if score_s > 0 else 0.0
-                valu = {"insts_per_pair": ipp, "achieved": rate / 1e9, "peak": VALU_PEAK / 1e9,
-                        "unit": "G wave-instructions/s", "frac": rate / VALU_PEAK,
-                        "source": os.path.relpath(pmc, ROOT) + " (" + pj.get("commit", "?") + ")"}
-                # the achievable issue rate: the kernel's instruction mix priced by the measured
-                # cycles per wave-instruction (scripts/valu_mix.py: VOP3 / packed / f64 ~4
-                # cycles, plain VOP1/VOP2 ~2.3), not the 2-cycle best case
-                vm = os.path.join(ROOT, "profiles", "valu_mix.json")
-                if os.path.exists(vm):
-                    with open(vm) as f:
-                        mx = json.load(f).get(w["name"])
-                    if mx and mx.get("avg_cycles_per_valu"):
-                        ach = 1024 * 2.4e9 / mx["avg_cycles_per_valu"]
-                        valu.update(avg_cycles_per_valu=mx["avg_cycles_per_valu"],
-                                    peak_achievable=ach / 1e9, frac_achievable=rate / ach,
-                                    mix_source="profiles/valu_mix.json (" + mx["kernel"][:40] + ")")
+        pmc_info = None
+        pj = None
+        for cand in (f"pmc_{w['pmc_key']}_{n}.json", f"pmc_{w['pmc_key']}.json"):
+            path = os.path.join(ROOT, "profiles", cand)
+            if os.path.exists(path):
+                with open(path) as f:
+                    pj = json.load(f)
+                pmc_path = path
+                break
+        if pj and pj.get("hbm_bytes_per_pair"):
+            traffic = pj["hbm_bytes_per_pair"] * prof["pairs_scored"] / launches
+            pmc_info = {"file": os.path.relpath(pmc_path, ROOT), "commit": pj.get("commit"),
+                        "kernel_symbol": pj.get("kernel_symbol"), "records": pj.get("records"),
+                        "hbm_bytes_per_pair": pj["hbm_bytes_per_pair"],
+                        "tcc_hit_rate": pj.get("tcc_hit_rate"),
+                        "wait_any_frac": pj.get("wait_any_frac"),
+                        "lds_conflict_cycles_per_lds_inst": pj.get("lds_conflicts_per_lds_inst")}
+            # VALU issue: wave-instructions per scored pair of the SAME PMC summary, at this
+            # run's pairs and k_score time, against the chip's 2-cycle issue rate (1,024 SIMDs x
+            # 2.4 GHz / 2) and against the achievable rate of that kernel's own instruction mix
+            ipp = pj["counters"]["SQ_INSTS_VALU"] / pj["pairs_profiled"]
+            rate = ipp * prof["pairs_scored"] / score_s if score_s > 0 else 0.0
+            valu = {"insts_per_pair": ipp, "achieved": rate / 1e9, "peak": VALU_PEAK / 1e9,
+                    "unit": "G wave-instructions/s", "frac": rate / VALU_PEAK,
+                    "source": pmc_info["file"] + " (" + str(pj.get("commit")) + ")"}
+            vm = os.path.join(ROOT, "profiles", "valu_mix.json")
+            if os.path.exists(vm):
+                with open(vm) as f:
+                    mx = json.load(f).get(w["pmc_key"])
+                if mx and mx.get("avg_cycles_per_valu"):
+                    ach = 1024 * 2.4e9 / mx["avg_cycles_per_valu"]
+                    valu.update(avg_cycles_per_valu=mx["avg_cycles_per_valu"],
+                                peak_achievable=ach / 1e9, frac_achievable=rate / ach,
+                                mix_kernel=mx["kernel"], mix_region=mx.get("region"),
+                                mix_source="profiles/valu_mix.json (" + str(mx.get("commit")) + ")")
+        hbm_rate = traffic / avg_launch_s if traffic and avg_launch_s > 0 else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -601,23 +620,39 @@ def main():
                                  else sum(c[0] for c in holder["counts"]) if "counts" in holder
                                  else int(last.n) if last is not None else 0),
             "index_build_s": t_index,
+            # the list: entries per query record, and its cost per step (device compaction of
+            # the staged entries, k_compact + scan), apart from the scoring kernel
+            "entries_per_query": ((sum(c[0] for c in shared.counts) if shared is not None
+                                   else sum(c[0] for c in holder["counts"]) if "counts" in holder
+                                   else int(last.n) if last is not None else 0) / max(1, len(allq))),
+            "list_ms_per_step": prof["ms_gather"] / args.steps,
             "synth_s": t_synth,
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "frac_s8d": achieved / HBM_PEAK,
-                         "frac_bound": frac_bound,
-                         "bound_bytes_per_launch": bound_launch,
-                         "query_bytes_per_query": qbytes,
+            "roofline": {"bound": "hbm",
+                         "achieved": hbm_rate / 1e9 if hbm_rate else None,
+                         "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": hbm_rate / HBM_PEAK if hbm_rate else None,
                          "traffic": traffic,
-                         "kernel": "k_score", "launches": prof["score_launches"],
+                         "frac_basis": ("calibrated HBM counter bytes of the dominant kernel (its "
+                                        "committed PMC pass, `pmc`) over its HIP-event launch time"
+                                        if hbm_rate else "no committed PMC summary for this "
+                                        "workload: frac unmeasured"),
+                         "kernel": prof.get("score_kernel") or w["kernel"],
+                         "pmc": pmc_info, "pmc_key": w["pmc_key"],
+                         "launches": prof["score_launches"],
                          "avg_launch_ms": prof["ms_score"] / launches,
                          "pairs_per_launch": pairs_launch,
+                         # SURVEY §8(d)'s algorithmic bytes (B_pair charges each pair both
+                         # sides' operands; a kernel holding the query in LDS can pass 1 here)
+                         "achieved_s8d": achieved / 1e9, "frac_s8d": achieved / HBM_PEAK,
                          "b_pair_s8d": bpair, "b_pair_detail": bdetail,
-                         "bytes_per_launch": bpair * pairs_launch if bpair else None,
-                         # the same B_pair over the whole step (every kernel + the gather)
-                         "frac_step": (bpair * value / (HBM_PEAK * world)) if bpair else None,
+                         "bytes_per_launch_s8d": bpair * pairs_launch if bpair else None,
+                         "frac_step_s8d": (bpair * value / (HBM_PEAK * world)) if bpair else None,
+                         # what the schedule requests (L2 serves part): not an HBM fraction
+                         "frac_request": frac_request,
+                         "request_bytes_per_launch": request_launch,
+                         "query_bytes_per_query": qbytes,
                          "operand_bytes_per_launch": prof["score_bytes"] / launches,
-                         "frac_operand_bytes": sched / HBM_PEAK,
+                         "frac_operand_request": sched / HBM_PEAK,
                          "limiter": "valu" if valu else None, "valu": valu},
             "pcie_inclusive": pcie,
             # per-rank pairs scored of the last step (tile balance; N>1)

@@ -21,11 +21,15 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
-KERNELS = {  # bench.py workload -> the k_score variant its launches use
-    "dedup": "_ZN2dk7k_scoreILi40ELb1ELb0E",  # GR = false: no gram-set code
-    "linkage": "_ZN2dk12k_score_nodpILb0E",
-    "allpairs": "_ZN2dk7k_scoreILi16ELb0ELb0E",
-    "longtext": "_ZN2dk12k_score_longILi16ELi16E",
+KERNELS = {  # bench.py roofline pmc_key -> (the kernel its launches use, loop region priced)
+    # "inner": the innermost loop bodies (the DP kernels' cell loops); "outer": the largest
+    # loop body (k_score_gq's per-group loop, whose inner loops are rare tails)
+    "dedup": ("_ZN2dk7k_scoreILi40ELb1ELb0E", "inner"),  # GR = false: no gram-set code
+    "dedup_utf16": ("_ZN2dk7k_scoreILi40ELb1ELb0E", "inner"),
+    "linkage": ("_ZN2dk10k_score_gqILi2ELi2E", "outer"),
+    "allpairs_lev": ("_ZN2dk7k_scoreILi16ELb0ELb0E", "inner"),
+    "allpairs_jw": ("_ZN2dk7k_scoreILi16ELb0ELb0E", "inner"),
+    "longtext": ("_ZN2dk12k_score_longILi16ELi16E", "inner"),
 }
 # cycles per wave64 instruction per SIMD (profiles/r01/valu_rate_gfx950.txt), by class
 TWO = ("v_add_u32_e32", "v_sub_u32_e32", "v_subrev_u32_e32", "v_and_b32_e32", "v_or_b32_e32",
@@ -74,8 +78,22 @@ def innermost_loops(body):
     return ins, inner
 
 
-def mix(dis, sym):
+def all_loops(ins):
+    base = ins[0][0]
+    loops = []
+    for addr, op, l in ins:
+        if op.startswith("s_cbranch") or op == "s_branch":
+            t = re.search(r"<[^>]*\+0x([0-9a-f]+)>", l)
+            if t and base + int(t.group(1), 16) <= addr:
+                loops.append((base + int(t.group(1), 16), addr))
+    return loops
+
+
+def mix(dis, sym, region="inner"):
     ins, inner = innermost_loops(function_body(dis, sym))
+    if region == "outer":  # the single largest loop (backward branch spanning the most code)
+        spans = all_loops(ins)
+        inner = [max(spans, key=lambda a: a[1] - a[0])] if spans else []
     counts = {}
     for lo, hi in inner:
         for addr, op, _ in ins:
@@ -83,7 +101,7 @@ def mix(dis, sym):
                 counts[op] = counts.get(op, 0) + 1
     n = sum(counts.values())
     cyc = sum(cycles(op) * c for op, c in counts.items())
-    return {"kernel": sym, "innermost_loops": len(inner), "valu_static": n,
+    return {"kernel": sym, "region": region, "loops": len(inner), "valu_static": n,
             "avg_cycles_per_valu": cyc / n if n else None,
             "two_cycle_frac": sum(c for op, c in counts.items() if cycles(op) < 3) / n if n else None,
             "top": sorted(counts.items(), key=lambda kv: -kv[1])[:12]}
@@ -98,14 +116,18 @@ def main():
             b.write(a.read())
         subprocess.run([f"{LLVM}/llvm-objdump", "--offloading", local], cwd=d, check=True,
                        capture_output=True)
-        co = [f for f in os.listdir(d) if "gfx950" in f][0]
-        dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", os.path.join(d, co)],
-                             check=True, capture_output=True, text=True).stdout
-    out = {"source": "static mix of the innermost loops; cycle table profiles/r01/valu_rate_gfx950.txt"}
-    for w, k in KERNELS.items():
+        # one code object per translation unit (dk_kernels, dk_score_grouped, dk_grams)
+        dis = "".join(subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", os.path.join(d, co)],
+                                     check=True, capture_output=True, text=True).stdout
+                      for co in sorted(os.listdir(d)) if "gfx950" in co)
+    out = {"source": "static mix of each kernel's priced loop region; cycle table "
+                     "profiles/r01/valu_rate_gfx950.txt"}
+    commit = os.environ.get("DK_COMMIT") or subprocess.run(
+        ["git", "rev-parse", "--short", "HEAD"], cwd=ROOT, capture_output=True, text=True).stdout.strip()
+    for w, (k, region) in KERNELS.items():
         sym = re.search(rf"<({re.escape(k)}[^>]*)>:", dis)
         if sym:
-            out[w] = mix(dis, sym.group(1))
+            out[w] = dict(mix(dis, sym.group(1), region), commit=commit)
     print(json.dumps(out, indent=1))
 
 

@@ -544,7 +544,7 @@ struct dk_ctx {
   uint64_t rstride = 0;               // replica positions
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
   // k_score_grouped's execution order: task sort keys / values (double-buffered), chunk starts
-  DevBuf task_key, task_val, task_cb, gprops;
+  DevBuf task_key, task_val, task_cb, gprops, gqargs;
   DevBuf gram_tmp, gram_scratch;  // dk_upsert's device q-gram sets (dk_grams.hip)
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
@@ -2221,6 +2221,73 @@ static std::vector<GroupedProp> grouped_props(const ScoreParams& P) {
   return gp;
 }
 
+// k_score_gq (round 5) serves the grouped schemas without DK_CMP_NONE properties, of 1-2
+// bigram QGram and at most kGQMaxNum Numeric properties, whose key-word rows fit the head
+// and tail buffer resources; DK_GQ=0 keeps k_score_grouped (A/B).  Fills the roles: QGram
+// roles by key-word rows (fewest first: role 0 holds fewer rows in registers), Numeric roles
+// in property order, and each order class's visiting order as roles.
+static bool gq_args(const ScoreParams& P, GQArgs* A, int* nq, int* nn) {
+  const char* e = getenv("DK_GQ");
+  if (e && e[0] == '0') return false;
+  memset(A, 0, sizeof *A);
+  int qp[kMaxProps], np[kMaxProps], a = 0, b = 0;
+  for (int p = 0; p < P.nprops; ++p) {
+    const int op = P.props[p].op;
+    if (op == DK_CMP_QGRAM) qp[a++] = p;
+    else if (op == DK_CMP_NUMERIC) np[b++] = p;
+    else return false;
+  }
+  if (a < 1 || a > kGroupedTabs || b > kGQMaxNum) return false;
+  if (a == 2 && P.props[qp[1]].rgrows < P.props[qp[0]].rgrows) std::swap(qp[0], qp[1]);
+  const uint64_t n = P.rstride;
+  if (n * 2 >= (1ull << 32) || n * 8 >= (1ull << 32)) return false;
+  A->nq = a;
+  A->nn = b;
+  A->len_bytes = (uint32_t)(n * 2);
+  A->pos_n = (uint32_t)n;
+  uint32_t role[kMaxProps];
+  for (int i = 0; i < a; ++i) {
+    const DevProp& D = P.props[qp[i]];
+    GQRoleQ& R = A->q[i];
+    R.rlen = D.rlen;
+    R.rgcnt = D.rgcnt;
+    R.rows = static_cast<const uint64_t*>(D.rgrams);
+    R.tail = R.rows + (uint64_t)kGroupedHeadRows * n;
+    R.nrows = (uint32_t)D.rgrows;
+    R.rowb = (uint32_t)(n * 8);
+    const uint64_t head = (uint64_t)std::min(D.rgrows, kGroupedHeadRows) * n * 8;
+    const uint64_t tail = D.rgrows > kGroupedHeadRows ? (uint64_t)(D.rgrows - kGroupedHeadRows) * n * 8 : 0;
+    if (head >= (1ull << 32) || tail >= (1ull << 32)) return false;
+    R.head_bytes = (uint32_t)head;
+    R.tail_bytes = (uint32_t)tail;
+    R.prop = qp[i];
+    R.formula = D.formula;
+    R.low = D.low;
+    R.high = D.high;
+    role[qp[i]] = (uint32_t)i;
+  }
+  for (int i = 0; i < b; ++i) {
+    const DevProp& D = P.props[np[i]];
+    GQRoleN& R = A->n[i];
+    R.rlen = D.rlen;
+    R.rnumok = D.rnumok;
+    R.rnum = D.rnum;
+    R.prop = np[i];
+    R.low = D.low;
+    R.high = D.high;
+    R.min_ratio = D.min_ratio;
+    role[np[i]] = 8u + (uint32_t)i;
+  }
+  for (int c = 0; c < kMaxOrders; ++c) {
+    uint64_t w = 0;
+    for (int k = 0; k < P.nprops; ++k) w |= (uint64_t)role[(P.order[c] >> (4 * k)) & 15u] << (4 * k);
+    A->rorder[c] = w;
+  }
+  *nq = a;
+  *nn = b;
+  return true;
+}
+
 // Lucene source, per dk_match: every query's hits (k_lucene_topk) become its candidate
 // range -- positions qi * max_hits + j of a per-call candidate replica, in hit order -- and
 // the slot layout (counts, offsets, wave map) of the direct schedule.  d_queries holds the
@@ -2544,7 +2611,26 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   // position (bucket by bucket), DK_TASK_SORT=0: slot order (A/B)
   const uint32_t* perm = nullptr;
   int gmode = 0;  // k_score_grouped<MODE>: how the key-word rows are addressed
-  if (grouped) {
+  GQArgs gqa;
+  int gq_nq = 0, gq_nn = 0;
+  const bool gq = grouped && gq_args(P, &gqa, &gq_nq, &gq_nn);
+  if (gq) {
+    // one copy per staging set (the launch's output buffers are part of it)
+    GQArgs two[2] = {gqa, gqa};
+    for (int b = 0; b < 2; ++b) {
+      two[b].rident = src.rident;
+      two[b].rkey0 = nk > 1 ? src.rkeys[0] : src.rident;
+      two[b].rowof = P.rowof;
+      two[b].oprob = st[b].prob;
+      two[b].ocand = st[b].cand;
+      two[b].oqidx = st[b].qidx;
+      two[b].threshold = P.threshold;
+      two[b].maybe = P.maybe;
+    }
+    HIPCHK(c->gqargs.reserve(sizeof two, 0, s));
+    HIPCHK(hipMemcpyAsync(c->gqargs.p, two, sizeof two, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));  // two is a temporary
+  } else if (grouped) {
     std::vector<GroupedProp> gp = grouped_props(P);
     // one resource per property while its rows (and the tail rows read past them) stay
     // below 2^32 bytes of offset
@@ -2678,7 +2764,9 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging b drained
       {
         Timer t_score(c, &c->prof.ms_score, s);
-        if (grouped)
+        if (gq)
+          HIPCHK(launch_score_gq(P, src, s0, s1 - s0, perm, c->gqargs.as<GQArgs>() + b, gq_nq, gq_nn, st[b], s));
+        else if (grouped)
           HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), gmode, st[b], s));
         else HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
         t_score.stop();

@@ -208,6 +208,55 @@ struct GroupedProp {
 static_assert(sizeof(GroupedProp) == 64, "two s_load_dwordx8");
 constexpr int kGroupedHeadRows = 4;  // k_score_grouped reads rows [0, 2 DK_GROUPED_ROWS) per pair
 
+// k_score_gq<NQ, NN> (dk_score_grouped.hip, round 5): the same schemas as k_score_grouped
+// without DK_CMP_NONE properties, NQ <= kGroupedTabs bigram QGram properties and NN <=
+// kGQMaxNum Numeric ones, each in a ROLE of its kind (QGram roles ordered by key-word rows,
+// fewest first).  Per role the host gives the candidate operands' bases and sizes and the
+// comparator constants, so every per-role value the kernel reads sits at a fixed offset
+// (scalar loads, no per-group property indexing).  Key-word row j of a QGram role is read
+// through the head buffer resource (rows < kGroupedHeadRows, based at row 0) or the tail
+// one (based at row kGroupedHeadRows); both must stay below 2^32 bytes (the host checks).
+constexpr int kGQMaxNum = 3;
+struct GQRoleQ {
+  const uint16_t* rlen;
+  const uint16_t* rgcnt;
+  const uint64_t* rows;   // key-word rows [j * rstride + g]
+  const uint64_t* tail;   // rows + kGroupedHeadRows * rstride
+  uint32_t nrows;         // rgrows
+  uint32_t head_bytes;    // min(nrows, kGroupedHeadRows) rows
+  uint32_t tail_bytes;    // the rows past kGroupedHeadRows
+  uint32_t rowb;          // bytes per row (replica positions x 8)
+  int32_t prop, formula;
+  double low, high;
+};
+struct GQRoleN {
+  const uint16_t* rlen;
+  const uint8_t* rnumok;
+  const double* rnum;
+  int32_t prop;
+  uint32_t pad;
+  double low, high, min_ratio;
+};
+struct alignas(16) GQArgs {
+  int32_t nq, nn;
+  uint32_t len_bytes;     // replica positions x 2 (rlen / rgcnt resources)
+  uint32_t pos_n;         // replica positions
+  // the group loop's other operands (the kernel copies GQArgs to LDS and re-reads it per
+  // group, so none of this is held in scalar registers across the loop)
+  const uint64_t* rident;
+  const uint64_t* rkey0;  // rkeys[0] (nkeys > 1)
+  const uint32_t* rowof;
+  double* oprob;          // the launch's staging set (StageOut)
+  uint32_t* ocand;
+  uint32_t* oqidx;
+  double threshold, maybe;
+  // Processor.compare's visiting order per order class as ROLES, 4 bits per position: a
+  // QGram role a is a, a Numeric role b is 8 + b
+  uint64_t rorder[kMaxOrders];
+  GQRoleQ q[kGroupedTabs];
+  GQRoleN n[kGQMaxNum];
+};
+
 // The emission pass of the symmetric schedule: slots of the full candidate order (qoff /
 // wq / ranges as in PairSource) read their probability from the owner results.
 struct EmitSource {
@@ -408,6 +457,10 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                                 uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
                                 int mode, const StageOut& out, hipStream_t s);
+// k_score_gq<nq, nn> (A: device copy of the host's GQArgs, whose nq / nn are passed too)
+hipError_t launch_score_gq(const ScoreParams& P, const PairSource& src, uint64_t slot0, uint64_t nslots,
+                           const uint32_t* perm, const GQArgs* A, int nq, int nn, const StageOut& out,
+                           hipStream_t s);
 // key[t] = chunk << 32 | first candidate's replica position of task t, val[t] = t;
 // cb[0..nchunks] = first task of each chunk
 hipError_t launch_task_keys(const PairSource& src, uint64_t ntask, const uint64_t* cb, int nchunks,

@@ -23,6 +23,8 @@
 #include "dk_internal.h"
 #include "dk_device.h"
 
+#include <type_traits>
+
 #ifndef DK_WAVES_GROUPED
 #define DK_WAVES_GROUPED 8  // k_score_grouped waves per SIMD
 #endif
@@ -451,6 +453,401 @@ hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uin
   else if (mode == 1) k_score_grouped<1><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
   else k_score_grouped<0><<<(unsigned)grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, gp, out);
   return hipGetLastError();
+}
+
+// =======================================================================================
+// k_score_gq<NQ, NN> (round 5): k_score_grouped's schemas on a schedule with ONE memory
+// round trip per group of 64 candidates instead of one per property plus one or two for the
+// key-word rows past the first two.  k_score_grouped<1> at configs[2] 10M x 10M spent 0.53
+// of its wave cycles waiting (rows 2-3 of each QGram property were loaded when the
+// property began, rows 4+ one batch later behind the next property's prefetch, and a
+// Numeric property's compute was too short to cover the next one's loads), and issued
+// nearly as many scalar instructions as vector ones (the per-property operand sources
+// rebuilt per group from a runtime property index).  Here:
+//  * Properties are ROLES of a fixed kind (NQ bigram QGram, NN Numeric; GQArgs), unrolled
+//    at compile time: every per-role constant sits at a fixed offset, and the HashMap
+//    visiting order only selects which role's probability enters computeBayes next (a
+//    uniform branch), after all roles are computed.
+//  * The FRONT of group g+1 (candidate positions and gram counts: what the row loads need)
+//    is loaded while group g computes; at group g's start its BACK operands -- every
+//    key-word row each lane needs (per-lane offsets past the lane's own rows are out of
+//    range: no data moved), lengths, filters, Numeric values -- are issued in one batch.
+//  * The waves of a SIMD (DK_WAVES_GQ) cover that one round trip.
+// =======================================================================================
+#ifndef DK_WAVES_GQ
+#define DK_WAVES_GQ 5  // k_score_gq waves per SIMD
+#endif
+#ifndef DK_GQ_ABL
+#define DK_GQ_ABL 0  // timing ablations only (wrong results): 1 probes, 2 f64 math, 4 row traffic
+#endif
+#ifndef DK_GQ_GUARD
+#define DK_GQ_GUARD 0  // 1: probe a register row only when some lane has it (uniform branches: the
+                       // ballot masks then cost SGPRs and every probe its own LDS wait)
+#endif
+#ifndef DK_GQ_ROWS0
+#define DK_GQ_ROWS0 5  // key-word rows held in registers: QGram role 0 (24 grams)
+#endif
+#ifndef DK_GQ_ROWS1
+#define DK_GQ_ROWS1 8  // role 1 (36 grams); longer sets read the rest in batches of 4
+#endif
+
+template <int A>
+struct GQRows {
+  static constexpr int v = A == 0 ? DK_GQ_ROWS0 : DK_GQ_ROWS1;
+};
+
+// element i of a global array whose pointer was read from memory (GQArgs): a generic
+// pointer would make it a FLAT load, which the wait-count pass cannot order against the
+// buffer loads in flight (every later wait becomes vmcnt(0))
+template <typename T>
+__device__ __forceinline__ T gq_ld(const T* p, uint32_t i) {
+  return ((const __attribute__((address_space(1))) T*)(p))[i];
+}
+template <typename T>
+__device__ __forceinline__ void gq_st(T* p, uint64_t i, T v) {
+  ((__attribute__((address_space(1))) T*)(p))[i] = v;
+}
+
+using GQLds = const __attribute__((address_space(3))) GQArgs;
+
+// The launch's GQArgs as this wave's LDS copy, through an address the compiler cannot prove
+// loop-invariant: per-group reads are LDS reads (no vector-memory wait, no scalar registers
+// held -- and spilled -- across the group loop); uniform values are made scalar at their use
+__device__ __forceinline__ GQLds* gq_hdr(GQLds* h) {
+  uint32_t v = (uint32_t)(uintptr_t)h;
+  asm volatile("" : "+v"(v));
+  return (GQLds*)(uintptr_t)v;
+}
+template <typename T>
+__device__ __forceinline__ T* gq_uptr(T* p) {  // a uniform pointer (VGPR copy) -> scalar
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t gq_u(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ rsrc_t gq_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, kRsrcWord3);
+}
+
+// [Duke 1.2] PropertyImpl.compare (a comparator is set: QGram / Numeric) + Math.max(0.0, .)
+__device__ __forceinline__ double gq_prob(double low, double high, double sim) {
+  return java_max(0.0, sim < 0.5 ? low : ((high - 0.5) * (sim * sim)) + 0.5);
+}
+
+// the query's values of one role (wave-uniform), staged in LDS once per task
+struct GQQuery {
+  uint16_t len, m1, seed;  // QGram: grams, perfect-hash seed
+  uint8_t ok, pad;         // Numeric: parsed
+  double num;              // Numeric: value
+};
+static_assert(sizeof(GQQuery) == 16, "one ds_read_b128");
+static_assert(sizeof(GQArgs) % 16 == 0, "GQArgs copied to LDS in 16-B pieces");
+
+template <int NQ, int NN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_GQ, 8)))
+void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots,
+                const uint32_t* __restrict__ perm, const GQArgs* __restrict__ A, StageOut out) {
+  constexpr int NR = NQ + NN;
+  constexpr int NQ1 = NQ > 0 ? NQ : 1, NN1 = NN > 0 ? NN : 1;
+  __shared__ uint32_t lds[kScoreBlock / 64][kGroupedTabs * kTabWords];
+  __shared__ GQQuery qlds[kScoreBlock / 64][kGroupedTabs + kGQMaxNum];
+  __shared__ uint2 slds[kScoreBlock / 64][kMaxSegs];  // per segment: {first position, length}
+  __shared__ GQArgs hlds[kScoreBlock / 64];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = lane_id();
+  const uint64_t task = grouped_task(perm, slot0 / kScoreBlock, nslots / kScoreBlock, wave);
+  if (task == ~0ull) return;  // the whole wave: no workgroup barrier follows
+  uint32_t* tabs = lds[wave];
+  GQQuery* qv = qlds[wave];
+  uint2* seg = slds[wave];
+  for (int e = (int)lane; e < (int)(sizeof(GQArgs) / 16); e += 64)
+    reinterpret_cast<uint4*>(&hlds[wave])[e] = reinterpret_cast<const uint4*>(A)[e];
+  GQLds* const hdr0 = (GQLds*)&hlds[wave];
+
+  // ---- the task's query: its segment ranges in LDS (the group loop then reads no uniform
+  //      value from global memory: a vector load there would wait for every row in flight) ----
+  const uint64_t sb = slot0 + task * kScoreBlock;
+  const uint32_t qi = __builtin_amdgcn_readfirstlane(S.wq[sb >> 6]);
+  const uint32_t q = __builtin_amdgcn_readfirstlane(S.queries[qi]);
+  const uint64_t tbase = sb - S.qoff[qi];
+  const int nseg = S.nseg;
+  uint32_t slen = 0;
+  if ((int)lane < nseg) {
+    const uint2 r = S.ranges[(uint64_t)lane * S.nq + qi];
+    slen = r.y - r.x;
+    uint64_t so = 0;
+    for (int k = 0; k < nseg; ++k)
+      if (k == (int)lane) so = S.segoff[k];
+    seg[lane] = make_uint2((uint32_t)(so + r.x), slen);
+  }
+  const uint64_t total = wave_sum_u32(slen);
+  const uint64_t rest = (total - tbase + 63) >> 6;
+  const int ngroups = rest < (uint64_t)kTaskGroups ? (int)rest : kTaskGroups;
+  const uint64_t qident = P.ident[q];
+  const uint64_t qk0 = S.nkeys > 1 ? S.qkeys[0][q] : 0ull;
+  const int seg_shift = S.seg_shift;
+  const int nkeys = S.nkeys;
+
+  // candidate t of the query -> (segment, position), as k_score_grouped; the FRONT of a
+  // group: its positions (kf << 1 | pair in fk) and the QGram roles' gram counts
+  auto load_front = [&](GQLds* H, int grp, uint32_t& g, uint32_t& fk, uint32_t (&cq)[NQ1]) {
+    uint32_t t = (uint32_t)(tbase + (uint64_t)grp * 64) + lane;  // a task's t < 2^32
+    bool v = false;
+    g = 0u;
+    fk = 0u;
+    for (int k = 0; k < nseg; ++k) {
+      const uint2 r = seg[k];
+      if (!v && t < r.y) {
+        g = r.x + t;
+        fk = (uint32_t)(k >> seg_shift) << 1 | 1u;
+        v = true;
+      }
+      t -= v ? 0u : r.y;
+    }
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) cq[a] = gq_ld(gq_uptr(H->q[a].rgcnt), g) & 0xFFu;
+  };
+
+  // lane r < NR stages role r's query values in LDS (one batch of loads, one wait)
+  if ((int)lane < NR) {
+    const int r = (int)lane;
+    const DevProp& D = P.props[r < NQ ? A->q[r].prop : A->n[r - NQ].prop];
+    GQQuery v{};
+    v.len = D.len[q];
+    if (r < NQ) {
+      v.m1 = D.gcnt[q];
+      v.seed = D.gseed[q];
+      v.pad = (uint8_t)D.formula;
+    } else {
+      v.ok = D.numok[q];
+      v.num = D.num[q];
+    }
+    qv[r] = v;
+  }
+  // Processor.compare's visiting order for this query, as roles (this wave's header copy:
+  // re-read per group, like the rest of it)
+  {
+    const uint64_t ro = A->rorder[P.norders > 1 ? (int)__builtin_amdgcn_readfirstlane((uint32_t)P.oclass[q]) : 0];
+    if (lane == 0) hlds[wave].rorder[0] = ro;
+  }
+  for (int e = (int)lane * 4; e < NQ * kTabWords; e += 256)
+    *reinterpret_cast<uint4*>(tabs + e) = make_uint4(0u, 0u, 0u, 0u);
+  wave_lds_sync();
+  uint32_t gn, fkn, cqn[NQ1];
+  load_front(hdr0, 0, gn, fkn, cqn);
+  // the query's bigram sets in its perfect-hash tables (table a = QGram role a)
+#pragma unroll
+  for (int a = 0; a < NQ; ++a) {
+    const GQQuery v = qv[a];
+    const uint32_t sd = __builtin_amdgcn_readfirstlane((uint32_t)v.seed);
+    const uint32_t m1 = __builtin_amdgcn_readfirstlane((uint32_t)v.m1);
+    if (__builtin_amdgcn_readfirstlane((uint32_t)v.len) != kMissing && m1 > 0 && sd != kGramSeedNone) {
+      uint32_t* tab = tabs + a * kTabWords;
+      const DevProp& D = P.props[A->q[a].prop];
+      if (lane == 0) tab[0] = ~0u;  // a real key landing in slot 0 overwrites the sentinel
+      if (lane < m1) {
+        const uint32_t key = gram_key(D.grams[D.goff[q] + lane]);
+        tab[(uint32_t)__umul24(key, gram_mult(sd & 0xFFu)) >> (24 - (int)(sd >> 8))] = key;
+      }
+    }
+  }
+  wave_lds_sync();
+
+  uint32_t cnt = 0, scored = 0, bytes = 0;
+  const uint64_t blk = task;  // staging block of the task (k_compact: block order = slot order)
+  for (int grp = 0; grp < ngroups; ++grp) {
+    GQLds* const H = gq_hdr(hdr0);
+    const uint32_t g = gn, fk = fkn;
+    uint32_t cq[NQ1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) cq[a] = cqn[a];
+    const bool pair = (fk & 1u) != 0u;
+    // the roles' query values (LDS, uniform)
+    uint32_t qlen[NR > 0 ? NR : 1];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) qlen[r] = gq_u((uint32_t)qv[r].len);
+    bool perfect[NQ1];
+    uint32_t m1[NQ1], sd[NQ1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) {
+      m1[a] = gq_u((uint32_t)qv[a].m1);
+      sd[a] = gq_u((uint32_t)qv[a].seed);
+      perfect[a] = qlen[a] != kMissing && m1[a] > 0 && sd[a] != kGramSeedNone;
+    }
+
+    // ---- back operands, one batch: key-word rows (past the lane's rows: no access),
+    //      lengths, filters, Numeric values ----
+    uint32_t nw[NQ1];  // key-word rows the lane reads (a pair, the query has a table)
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) nw[a] = pair && perfect[a] ? (cq[a] + 3u) >> 2 : 0u;
+    uint64_t w0[GQRows<0>::v];
+    uint64_t w1[GQRows<1>::v];
+    const uint32_t g8 = g * 8u;
+    auto issue_rows = [&](auto ic, uint64_t* w) {
+      constexpr int a = decltype(ic)::value;
+      const rsrc_t rh = gq_rsrc(gq_uptr(H->q[a].rows), gq_u(H->q[a].head_bytes));
+      const rsrc_t rt = gq_rsrc(gq_uptr(H->q[a].tail), gq_u(H->q[a].tail_bytes));
+      const uint32_t rowb = gq_u(H->q[a].rowb);
+#pragma unroll
+      for (int j = 0; j < GQRows<a>::v; ++j) {
+        const uint32_t off = g8 + (uint32_t)(j < kGroupedHeadRows ? j : j - kGroupedHeadRows) * rowb;
+        const uint32_t o = (DK_GQ_ABL & 4) ? 0xFFFFFFFFu : (uint32_t)j < nw[a] ? off : 0xFFFFFFFFu;
+        w[j] = __builtin_bit_cast(uint64_t,
+                                  __builtin_amdgcn_raw_buffer_load_b64(j < kGroupedHeadRows ? rh : rt, o, 0, 0));
+      }
+    };
+    if constexpr (NQ > 0) issue_rows(std::integral_constant<int, 0>{}, w0);
+    if constexpr (NQ > 1) issue_rows(std::integral_constant<int, 1>{}, w1);
+    const uint64_t rid = gq_ld(gq_uptr(H->rident), g);
+    const uint64_t rk = nkeys > 1 && fk > 1u ? gq_ld(gq_uptr(H->rkey0), g) : 0ull;
+    const uint32_t crow = gq_ld(gq_uptr(H->rowof), g);
+    uint32_t lq[NQ1], ln[NN1], cok[NN1];
+    double cn[NN1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) lq[a] = gq_ld(gq_uptr(H->q[a].rlen), g);
+#pragma unroll
+    for (int b = 0; b < NN; ++b) {
+      ln[b] = gq_ld(gq_uptr(H->n[b].rlen), g);
+      cn[b] = gq_ld(gq_uptr(H->n[b].rnum), g);
+      cok[b] = gq_ld(gq_uptr(H->n[b].rnumok), g);
+    }
+    // the next group's front (past the last group: position 0, no pair)
+    load_front(H, grp + 1, gn, fkn, cqn);
+
+    // ---- filters: Processor.isSameAs, a superseded base position, a candidate already
+    //      returned under an earlier key function (Duke's candidate set) ----
+    const int kf = (int)(fk >> 1);
+    bool valid = pair && rid != qident && rid != kDeadIdent;
+    if (kf > 0) valid = valid && rk != qk0;
+    for (int j = 1; j < nkeys - 1; ++j)  // more than two key functions
+      if (j < kf) valid = valid && S.rkeys[j][g] != S.qkeys[j][q];
+
+    // ---- every role's probability, then computeBayes in the visiting order ----
+    double pp[NR > 0 ? NR : 1];
+    bool ap[NR > 0 ? NR : 1];
+    uint32_t by = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
+    auto score_role = [&](auto ic, const uint64_t* w) {
+      constexpr int a = decltype(ic)::value;
+      const bool present = valid && lq[a] != kMissing;
+      const bool cmp = present && lq[a] > 0 && qlen[a] > 0;
+      double sim = 0.0;
+      if (qlen[a] != kMissing) {
+        if (present) by += 2u;
+        if (cmp) by += 6u + 2u * cq[a];
+        if (perfect[a]) {
+          const uint32_t* tab = tabs + a * kTabWords;
+          const uint32_t mult = gram_mult(sd[a] & 0xFFu);
+          const int sh = 24 - (int)(sd[a] >> 8);  // 32 - lt
+          int common = 0;
+#pragma unroll
+          for (int j = 0; j < GQRows<a>::v; ++j)
+            if (!DK_GQ_GUARD || __builtin_amdgcn_ballot_w64((uint32_t)j < nw[a]))  // uniform: a lane has row j
+              if (!(DK_GQ_ABL & 1)) common += probe_word(tab, w[j], mult, sh);
+          // sets past the rows held in registers: the rest DK_GROUPED_TAIL rows at a time
+          if (__builtin_amdgcn_ballot_w64(nw[a] > (uint32_t)GQRows<a>::v)) {
+            const rsrc_t rt = gq_rsrc(gq_uptr(H->q[a].tail), gq_u(H->q[a].tail_bytes));
+            const uint32_t rowb = gq_u(H->q[a].rowb);
+            const int nrows = (int)gq_u(H->q[a].nrows);
+            for (int j = GQRows<a>::v; j < nrows; j += kTailRows) {
+              uint64_t wt[kTailRows];
+#pragma unroll
+              for (int i = 0; i < kTailRows; ++i) {
+                const uint32_t off = g8 + (uint32_t)(j + i - kGroupedHeadRows) * rowb;
+                wt[i] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
+                                                         rt, (uint32_t)(j + i) < nw[a] ? off : 0xFFFFFFFFu, 0, 0));
+              }
+#pragma unroll
+              for (int i = 0; i < kTailRows; ++i) common += probe_word(tab, wt[i], mult, sh);
+              if (!__builtin_amdgcn_ballot_w64(nw[a] > (uint32_t)(j + kTailRows))) break;
+            }
+          }
+          const int m2 = cmp ? (int)cq[a] : 0;
+          if (m2 > 0) sim = (DK_GQ_ABL & 2) ? (double)common * 0.015625 : qgram_formula(common, (int)m1[a], m2, (int)gq_u(qv[a].pad));
+        } else {  // no perfect hash for the query: the sorted lists (rare), as k_score_grouped
+          const DevProp& D = P.props[gq_u((uint32_t)H->q[a].prop)];
+          sim = qgram_generic<uint8_t>(D, P.rstride, q, g, crow, (int)m1[a], (int)qlen[a], (int)lq[a], cmp);
+        }
+      }
+      pp[a] = cmp ? gq_prob(H->q[a].low, H->q[a].high, sim) : 0.0;
+      ap[a] = present;
+    };
+    if constexpr (NQ > 0) score_role(std::integral_constant<int, 0>{}, w0);
+    if constexpr (NQ > 1) score_role(std::integral_constant<int, 1>{}, w1);
+#pragma unroll
+    for (int b = 0; b < NN; ++b) {
+      const bool present = valid && ln[b] != kMissing;
+      const bool cmp = present && ln[b] > 0 && qlen[NQ + b] > 0;
+      double sim = 0.0;
+      if (qlen[NQ + b] != kMissing) {
+        if (present) by += 2u;
+        if (cmp) {
+          const GQQuery v = qv[NQ + b];
+          sim = (DK_GQ_ABL & 2) ? cn[b] * v.num : numeric(v.num, v.ok != 0, cn[b], cok[b] != 0u, H->n[b].min_ratio);
+          by += 9u;  // rnum + rnumok
+        }
+      }
+      pp[NQ + b] = cmp ? gq_prob(H->n[b].low, H->n[b].high, sim) : 0.0;
+      ap[NQ + b] = present;
+    }
+    // [Duke 1.2] Processor.compare: per property of r1 in its HashMap order, skipping those
+    // r1 or r2 has no value of, prob = computeBayes(prob, max(0.0, PropertyImpl.compare))
+    double prob = 0.5;
+    const uint64_t ro = ((uint64_t)gq_u((uint32_t)(H->rorder[0] >> 32)) << 32) | gq_u((uint32_t)H->rorder[0]);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const uint32_t r = (uint32_t)(ro >> (4 * k)) & 15u;
+      const int ri = r >= 8u ? NQ + (int)(r - 8u) : (int)r;  // wave-uniform
+      double x = 0.5;
+      bool use = false;
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+        if (ri == i) {
+          x = pp[i];
+          use = qlen[i] != kMissing && ap[i];
+        }
+      const double nb = (DK_GQ_ABL & 2) ? prob * x : compute_bayes(prob, x);
+      prob = use ? nb : prob;
+    }
+
+    // [Duke 1.2] Processor.compareCandidatesSimple; block-ordered compaction within the task
+    const uint32_t kind = valid ? decide(prob, H->threshold, H->maybe) : 0u;
+    const uint64_t em = __ballot(kind != 0u);
+    if (kind != 0u) {
+      const uint64_t e = blk * kScoreBlock + cnt + mask_rank(em);
+      gq_st(gq_uptr(H->oprob), e, prob);
+      gq_st(gq_uptr(H->ocand), e, crow | (kind << kKindShift));
+      gq_st(gq_uptr(H->oqidx), e, qi);
+    }
+    cnt += (uint32_t)__popcll(em);
+    scored += valid ? 1u : 0u;
+    bytes += by;
+  }
+  const uint32_t ss = wave_sum_u32(scored), sbytes = wave_sum_u32(bytes);
+  if (lane == 0) {
+    out.bcnt[blk] = cnt;
+    out.bscored[blk] = ss;
+    out.bbytes[blk] = sbytes;
+  }
+}
+
+hipError_t launch_score_gq(const ScoreParams& P, const PairSource& src, uint64_t slot0, uint64_t nslots,
+                           const uint32_t* perm, const GQArgs* A, int nq, int nn, const StageOut& out,
+                           hipStream_t s) {
+  if (nslots == 0) return hipSuccess;
+  if (nslots % kScoreBlock || slot0 % kScoreBlock) return hipErrorInvalidValue;
+  const uint64_t ntask = nslots / kScoreBlock;
+  const unsigned grid = (unsigned)((ntask + kScoreBlock / 64 - 1) / (kScoreBlock / 64));
+#define DK_GQ_CASE(NQ_, NN_)                                                                  \
+  if (nq == NQ_ && nn == NN_) {                                                               \
+    k_score_gq<NQ_, NN_><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, A, out);   \
+    return hipGetLastError();                                                                 \
+  }
+  DK_GQ_CASE(1, 0) DK_GQ_CASE(1, 1) DK_GQ_CASE(1, 2) DK_GQ_CASE(1, 3)
+  DK_GQ_CASE(2, 0) DK_GQ_CASE(2, 1) DK_GQ_CASE(2, 2) DK_GQ_CASE(2, 3)
+#undef DK_GQ_CASE
+  return hipErrorInvalidValue;
 }
 
 // Sort keys of the tasks (kScoreBlock slots of one query each): chunk << 32 | the replica

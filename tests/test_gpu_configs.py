@@ -102,18 +102,22 @@ def test_reference_schema_dedup_gpu():
 # configs[2] (QGram DICE/JACCARD + Numeric min-ratio 0.9, cross-group key blocking) and
 # configs[4] (WeightedLevenshtein + QGram q=3 JACCARD, key = first two tokens) in linkage
 # ---------------------------------------------------------------------------------------
-@pytest.mark.parametrize("variant", ["default", "tail_resource", "row_resources", "no_grouped", "host_grams"])
+@pytest.mark.parametrize("variant", ["default", "legacy_grouped", "tail_resource", "row_resources",
+                                     "no_grouped", "host_grams"])
 def test_config2_linkage_qgram_numeric(variant, monkeypatch):
     """configs[2]'s schema through each of its device paths, bit-exact against the oracle:
-    k_score_grouped with one buffer resource per property (default at this size), with head
-    and tail resources (DK_GROUPED_ROW=1: what a 10M x 10M replica takes) or a resource per
-    tail row (DK_GROUPED_ROW=2: larger replicas), k_score_nodp
-    (DK_GROUPED=0), and q-gram sets built on the host instead of the device (DK_DEV_GRAMS=0)."""
-    env = {"tail_resource": ("DK_GROUPED_ROW", "1"), "row_resources": ("DK_GROUPED_ROW", "2"),
-           "no_grouped": ("DK_GROUPED", "0"),
-           "host_grams": ("DK_DEV_GRAMS", "0")}.get(variant)
-    if env:
-        monkeypatch.setenv(*env)
+    k_score_gq (default; its head / tail row resources are the layout a 10M x 10M replica
+    takes, at any size), k_score_grouped (DK_GQ=0) with one buffer resource per property,
+    with head and tail resources (DK_GROUPED_ROW=1) or a resource per tail row
+    (DK_GROUPED_ROW=2: replicas past k_score_gq's resources), k_score_nodp (DK_GROUPED=0),
+    and q-gram sets built on the host instead of the device (DK_DEV_GRAMS=0)."""
+    env = {"legacy_grouped": [("DK_GQ", "0")],
+           "tail_resource": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "1")],
+           "row_resources": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "2")],
+           "no_grouped": [("DK_GROUPED", "0")],
+           "host_grams": [("DK_DEV_GRAMS", "0")]}.get(variant, [])
+    for kv in env:
+        monkeypatch.setenv(*kv)
     p, group = synth.linkage_persons(2500)
     props = [{"comparator": QG, "low": 0.1, "high": 0.95, "q": 2, "formula": A.QGRAM_DICE},
              {"comparator": QG, "low": 0.2, "high": 0.8, "q": 2, "formula": A.QGRAM_JACCARD},
