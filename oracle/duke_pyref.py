@@ -310,6 +310,84 @@ def geoposition(s1, s2, max_distance) -> float:
     return ((1.0 - (dist / max_distance)) * 0.5) + 0.5
 
 
+# --- RecordImpl's HashMap iteration order (SURVEY a-7; Processor.compare visits r1's map) ---
+# Simulated as java.util.HashMap runs it (an independent restatement of the bucket-sort in
+# dukehip/config.py): a table of per-bucket lists, puts appended at the bucket's tail, resize
+# doubling and splitting each bucket into lo/hi lists that keep their order.  WHICH
+# construction Duke's RecordImpl uses is unpinned (its source is absent): "incremental"
+# (`new HashMap()` + one put per key) or "copy_jdk8" (`new HashMap(m)` of such a map on JDK
+# 8..18: table sized tableSizeFor((int)(s / 0.75f + 1)), entries in m's iteration order).
+
+def java_string_hashcode(s):
+    h = 0
+    for u in units(s):
+        h = (31 * h + u) & 0xFFFFFFFF
+    return h
+
+
+class JavaHashMapOrder:
+    def __init__(self, initial_threshold=0):
+        self.table = None
+        self.size = 0
+        self.threshold = initial_threshold    # HashMap(int)/HashMap(Map): next table size
+
+    def _resize(self):
+        if self.table is None:
+            cap = self.threshold if self.threshold > 0 else 16
+            self.table = [[] for _ in range(cap)]
+        else:
+            old = self.table
+            cap = 2 * len(old)
+            self.table = [[] for _ in range(cap)]
+            for j, b in enumerate(old):
+                for k in b:                    # lo stays at j, hi moves to j + old cap
+                    self.table[self._spread(k) & (cap - 1)].append(k)
+        self.threshold = int(len(self.table) * 0.75)
+
+    @staticmethod
+    def _spread(k):
+        h = java_string_hashcode(k)
+        return h ^ (h >> 16)
+
+    def put(self, k):
+        if self.table is None:
+            self._resize()
+        b = self.table[self._spread(k) & (len(self.table) - 1)]
+        if k in b:
+            return
+        b.append(k)
+        self.size += 1
+        if self.size > self.threshold:
+            self._resize()
+
+    def keys(self):
+        return [k for b in (self.table or []) for k in b]
+
+
+def _float32(x):
+    import struct
+    return struct.unpack("f", struct.pack("f", x))[0]
+
+
+def record_map_order(keys, construction="incremental"):
+    """Iteration order of a record map whose keys were put in `keys` order."""
+    m = JavaHashMapOrder()
+    for k in keys:
+        m.put(k)
+    if construction == "incremental":
+        return m.keys()
+    if construction == "copy_jdk8":
+        t = int(_float32(_float32(float(len(keys))) / _float32(0.75)) + 1.0)
+        cap = 1
+        while cap < t:
+            cap *= 2
+        c = JavaHashMapOrder(cap if keys else 0)
+        for k in m.keys():
+            c.put(k)
+        return c.keys()
+    raise ValueError(construction)
+
+
 def java_max(a, b):
     if a != a:
         return a

@@ -545,6 +545,16 @@ struct dk_ctx {
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
   // k_score_grouped's execution order: task sort keys / values (double-buffered), chunk starts
   DevBuf task_key, task_val, task_cb, gprops, gqargs;
+  // k_tile (dk_tile.hip): per QGram role the bigram dictionary (keys marked from the gram
+  // arena up to tile_marked codes, their ids), and the per-call bucket / entry buffers
+  DevBuf tile_present[kGroupedTabs], tile_scan[kGroupedTabs], tile_lut[kGroupedTabs];
+  uint64_t tile_marked[kGroupedTabs] = {0, 0};
+  uint32_t tile_dict[kGroupedTabs] = {0, 0};
+  bool tile_key0[kGroupedTabs] = {false, false};
+  DevBuf tile_qids, tile_qrec, tile_bkey, tile_bval, tile_head, tile_bid, tile_bfirst, tile_bpos, tile_bseg,
+      tile_blen, tile_bnq, tile_nitems, tile_bitem, tile_ibucket, tile_ekey, tile_eval, tile_eprob, tile_ecand,
+      tile_small;
+  uint64_t tile_ecap = 1ull << 22;
   DevBuf gram_tmp, gram_scratch;  // dk_upsert's device q-gram sets (dk_grams.hip)
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
@@ -2264,6 +2274,11 @@ static bool gq_args(const ScoreParams& P, GQArgs* A, int* nq, int* nn) {
     R.formula = D.formula;
     R.low = D.low;
     R.high = D.high;
+    R.flow = (float)D.low;
+    R.fhigh = (float)D.high;
+    R.flow0 = (float)std::max(0.0, D.low);
+    const double g5 = (D.high - 0.5) * 0.25 + 0.5;
+    R.fub = (float)std::max(std::max(0.0, D.low), std::max(g5, D.high));
     role[qp[i]] = (uint32_t)i;
   }
   for (int i = 0; i < b; ++i) {
@@ -2283,6 +2298,16 @@ static bool gq_args(const ScoreParams& P, GQArgs* A, int* nq, int* nn) {
     for (int k = 0; k < P.nprops; ++k) w |= (uint64_t)role[(P.order[c] >> (4 * k)) & 15u] << (4 * k);
     A->rorder[c] = w;
   }
+  // the screen (k_score_gq): kind != 0 iff prob > tm; the bound's odds must reach
+  // tm / (1 - tm), less a 2e-3 margin for the single-precision bound
+  const double tm = P.maybe != 0.0 ? std::min(P.threshold, P.maybe) : P.threshold;
+  A->screen = tm >= kScreenLo && tm <= kScreenHi ? (float)(tm / (1.0 - tm) * (1.0 - 2e-3)) : 0.0f;
+  const char* es = getenv("DK_GQ_SCREEN");  // 0: every valid pair to the exact pass (A/B)
+  if (es && es[0] == '0') A->screen = 0.0f;
+  // the deferred QGram role: DK_GQ_DEFER = -1 / 0 / 1 (default 0 with two QGram roles)
+  A->defer = a == 2 ? 0 : -1;
+  const char* ed = getenv("DK_GQ_DEFER");
+  if (ed && a == 2) A->defer = atoi(ed) < 0 ? -1 : std::min(atoi(ed), 1);
   *nq = a;
   *nn = b;
   return true;
@@ -2358,6 +2383,281 @@ static int lucene_candidates(dk_ctx* c, uint64_t nq, uint64_t* total, uint64_t* 
   return DK_OK;
 }
 
+// ---------------------------------------------------------------------------------------
+// The bucket-tiled schedule (k_tile, dk_tile.hip) for GQArgs schemas on the direct schedule:
+// the same list as k_score_gq (tests/test_gpu_configs.py compares both with the oracle).
+// DK_TILE=1 selects it (k_score_gq is the default).  Eligible: key functions <= 2 (the duplicate filter reads
+// rkeys[0]), per QGram role a dictionary of <= kTileMaxDict keys without the key-0 bigram.
+// ---------------------------------------------------------------------------------------
+static bool tile_enabled() {  // DK_TILE=1: measured slower than k_score_gq, opt-in
+  const char* e = getenv("DK_TILE");
+  return e && e[0] == '1';
+}
+
+// the dictionary of QGram role a (property p): mark the gram arena's codes not marked yet,
+// ids = exclusive prefix of the marks; returns DK_OK and fills tile_dict / tile_key0
+static int tile_dictionary(dk_ctx* c, int a, int p) {
+  hipStream_t s = c->stream;
+  PropState& S = c->P[p];
+  HIPCHK(c->tile_present[a].reserve(65536 * 4, 0, s));
+  HIPCHK(c->tile_scan[a].reserve(65536 * 4 + 4, 0, s));
+  HIPCHK(c->tile_lut[a].reserve(65536 * 2, 0, s));
+  if (S.grams_used < c->tile_marked[a]) c->tile_marked[a] = 0;  // the arena was rebuilt
+  if (c->tile_marked[a] == 0) HIPCHK(hipMemsetAsync(c->tile_present[a].p, 0, 65536 * 4, s));
+  if (S.grams_used > c->tile_marked[a])
+    HIPCHK(launch_tile_mark(S.grams.as<uint64_t>(), c->tile_marked[a], S.grams_used - c->tile_marked[a],
+                            c->tile_present[a].as<uint32_t>(), s));
+  c->tile_marked[a] = S.grams_used;
+  HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+    return exclusive_scan_u32(t, b, c->tile_present[a].as<uint32_t>(), c->tile_scan[a].as<uint32_t>(), 65536, s);
+  }));
+  HIPCHK(launch_tile_lut(c->tile_scan[a].as<uint32_t>(), c->tile_lut[a].as<uint16_t>(), s));
+  uint32_t h[3];
+  HIPCHK(hipMemcpyAsync(&h[0], c->tile_scan[a].as<uint32_t>() + 65535, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&h[1], c->tile_present[a].as<uint32_t>() + 65535, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&h[2], c->tile_present[a].as<uint32_t>(), 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  c->tile_dict[a] = h[0] + h[1];
+  c->tile_key0[a] = h[2] != 0;
+  return DK_OK;
+}
+
+// the tiled dk_match after the index is in place (T, P); returns 1 when the schema or the
+// index does not fit the tiled path (the caller goes on with the slot schedule)
+static int tile_match(dk_ctx* c, const ScoreParams& P, const BlockTables& T, uint64_t nq, int flags,
+                      ResultHolder* R, std::chrono::steady_clock::time_point t0) {
+  hipStream_t s = c->stream;
+  GQArgs gqa;
+  int nqr = 0, nnr = 0;
+  if (!tile_enabled() || c->schema.nkeys > 2 || !grouped_schema_ok(P) || !gq_args(P, &gqa, &nqr, &nnr)) return 1;
+  int planes = 6;
+  for (int a = 0; a < nqr; ++a) {
+    if (c->P[gqa.q[a].prop].maxgrams > kTileIdsPerRole) return 1;
+    if (c->P[gqa.q[a].prop].maxgrams >= 64) planes = 7;
+  }
+  Timer t_gen(c, &c->prof.ms_generate, s);
+  for (int a = 0; a < nqr; ++a) {
+    int rc = tile_dictionary(c, a, gqa.q[a].prop);
+    if (rc) return rc;
+    if (c->tile_dict[a] > kTileMaxDict || c->tile_key0[a]) return 1;
+  }
+  // candidate ranges per (segment, query)
+  HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
+  HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
+  HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
+  HIPCHK(launch_count(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(), c->counts.as<uint64_t>(),
+                      c->counters.as<uint64_t>() + 2, 64, s));
+  PairSource src{};
+  src.queries = c->d_queries.as<uint32_t>();
+  src.ranges = c->ranges.as<uint2>();
+  src.nq = nq;
+  src.nkeys = c->schema.nkeys;
+  src.nseg = T.nseg;
+  src.seg_shift = T.seg_shift;
+  for (int k = 0; k < T.nseg; ++k) src.segoff[k] = T.seg_off[k];
+  src.rident = c->rident.as<uint64_t>();
+  for (int k = 0; k < c->schema.nkeys; ++k) {
+    src.qkeys[k] = c->keys[k].as<uint64_t>();
+    src.rkeys[k] = c->rkeys[k].as<uint64_t>();
+  }
+  // the roles' device copy, and each query's key ids
+  HIPCHK(c->gqargs.reserve(sizeof(GQArgs), 0, s));
+  HIPCHK(hipMemcpyAsync(c->gqargs.p, &gqa, sizeof(GQArgs), hipMemcpyHostToDevice, s));
+  HIPCHK(c->tile_qids.reserve(nq * nqr * kTileIdsPerRole * 2 + 16, 0, s));
+  HIPCHK(launch_tile_qids(P, c->d_queries.as<uint32_t>(), nq, c->gqargs.as<GQArgs>(), nqr,
+                          c->tile_lut[0].as<uint16_t>(), nqr > 1 ? c->tile_lut[1].as<uint16_t>() : nullptr,
+                          c->tile_qids.as<uint16_t>(), s));
+  HIPCHK(c->tile_qrec.reserve(nq * sizeof(TileQRec) + 64, 0, s));
+  HIPCHK(launch_tile_qrec(P, src, c->gqargs.as<GQArgs>(), c->tile_qrec.as<TileQRec>(), s));
+  // buckets: (range start << 32 | query index) of every (segment, query) with candidates, sorted
+  const uint64_t n = (uint64_t)T.nseg * nq;
+  HIPCHK(c->tile_bkey.reserve(2 * n * 8 + 16, 0, s));
+  HIPCHK(c->tile_bval.reserve(2 * n * 4 + 16, 0, s));
+  HIPCHK(c->tile_head.reserve(n * 4 + 4, 0, s));
+  HIPCHK(c->tile_bid.reserve(n * 4 + 4, 0, s));
+  uint64_t* k0 = c->tile_bkey.as<uint64_t>();
+  uint64_t* k1 = k0 + n;
+  uint32_t* v0 = c->tile_bval.as<uint32_t>();
+  HIPCHK(c->tile_small.reserve(64, 0, s));
+  HIPCHK(hipMemsetAsync(c->tile_small.p, 0, 16, s));
+  HIPCHK(launch_tile_bkeys(src, k0, c->tile_small.as<uint64_t>() + 1, s));
+  HIPCHK(with_tmp(c, [&](void* t, size_t& b) { return sort_pairs_u64_u32(t, b, k0, k1, v0, v0 + n, n, s); }));
+  HIPCHK(launch_tile_heads(k1, n, c->tile_head.as<uint32_t>(), s));
+  HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+    return exclusive_scan_u32(t, b, c->tile_head.as<uint32_t>(), c->tile_bid.as<uint32_t>(), n, s);
+  }));
+  uint64_t* hs = c->h_small.as<uint64_t>();
+  uint32_t h4[2];
+  HIPCHK(hipMemcpyAsync(&h4[0], c->tile_bid.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&h4[1], c->tile_head.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&hs[2], c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&hs[5], c->tile_small.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint64_t generated = hs[2];
+  const uint64_t nb = n ? (uint64_t)h4[0] + h4[1] : 0;
+  // the keys with candidates (k_tile_bkeys counted them): a prefix of the sorted keys
+  // (empty ranges sort last as ~0)
+  const uint64_t nvalid = hs[5];
+  HIPCHK(c->tile_bfirst.reserve(nb * 4 + 4, 0, s));
+  HIPCHK(c->tile_bpos.reserve(nb * 4 + 4, 0, s));
+  HIPCHK(c->tile_bseg.reserve(nb * 4 + 4, 0, s));
+  HIPCHK(c->tile_blen.reserve(nb * 4 + 4, 0, s));
+  HIPCHK(c->tile_bnq.reserve(nb * 4 + 4, 0, s));
+  HIPCHK(c->tile_nitems.reserve(nb * 8 + 8, 0, s));
+  HIPCHK(c->tile_bitem.reserve(nb * 8 + 16, 0, s));
+  HIPCHK(launch_tile_buckets(src, k1, n, nvalid, c->tile_head.as<uint32_t>(), c->tile_bid.as<uint32_t>(), nb,
+                             c->tile_bfirst.as<uint32_t>(), c->tile_bpos.as<uint32_t>(), c->tile_bseg.as<uint32_t>(),
+                             c->tile_blen.as<uint32_t>(), c->tile_bnq.as<uint32_t>(), c->tile_nitems.as<uint64_t>(), s));
+  uint64_t nitems = 0;
+  if (nb) {
+    HIPCHK(hipMemsetAsync(c->tile_nitems.as<uint64_t>() + nb, 0, 8, s));
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+      return exclusive_scan_u64(t, b, c->tile_nitems.as<uint64_t>(), c->tile_bitem.as<uint64_t>(), nb + 1, s);
+    }));
+    HIPCHK(hipMemcpyAsync(&hs[3], c->tile_bitem.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    nitems = hs[3];
+  }
+  if (nitems >= (1ull << 31)) return 1;
+  HIPCHK(c->tile_ibucket.reserve(nitems * 4 + 4, 0, s));
+  HIPCHK(launch_tile_itemmap(c->tile_bitem.as<uint64_t>(), nb, nitems, c->tile_ibucket.as<uint32_t>(), s));
+  t_gen.stop();
+
+  TileArgs TA{};
+  TA.bkey = k1;
+  TA.bfirst = c->tile_bfirst.as<uint32_t>();
+  TA.bnq = c->tile_bnq.as<uint32_t>();
+  TA.bpos = c->tile_bpos.as<uint32_t>();
+  TA.bseg = c->tile_bseg.as<uint32_t>();
+  TA.blen = c->tile_blen.as<uint32_t>();
+  TA.bitem = c->tile_bitem.as<uint64_t>();
+  TA.ibucket = c->tile_ibucket.as<uint32_t>();
+  TA.nbuckets = nb;
+  TA.nitems = nitems;
+  uint32_t rows = 0;
+  for (int a = 0; a < nqr; ++a) {
+    TA.lut[a] = c->tile_lut[a].as<uint16_t>();
+    TA.dict[a] = c->tile_dict[a];
+    TA.toff[a] = rows;
+    rows += c->tile_dict[a] + 1;  // + the zero row
+  }
+  if (rows > kTileMaxRows) return 1;
+  TA.tsize = rows;
+  TA.qids = c->tile_qids.as<uint16_t>();
+  TA.qrec = c->tile_qrec.as<TileQRec>();
+  TA.counters = c->counters.as<uint64_t>();
+  TA.nq = nq;
+  TA.nvalid = nvalid;
+  TA.npos = P.rstride;
+  const bool tdebug = getenv("DK_TILE_DEBUG") != nullptr;
+  HIPCHK(c->tile_small.reserve(64, 0, s));
+  TA.dbg = reinterpret_cast<uint32_t*>(c->tile_small.as<uint64_t>() + 2);
+  if (tdebug) HIPCHK(hipMemsetAsync(TA.dbg, 0, 4, s));
+  uint64_t nm = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    const uint64_t cap = c->tile_ecap;
+    HIPCHK(c->tile_ekey.reserve(2 * cap * 8 + 16, 0, s));
+    HIPCHK(c->tile_eval.reserve(2 * cap * 4 + 16, 0, s));
+    HIPCHK(c->tile_eprob.reserve(cap * 8 + 16, 0, s));
+    HIPCHK(c->tile_ecand.reserve(cap * 4 + 16, 0, s));
+    TA.ecount = c->tile_small.as<uint64_t>();
+    TA.ecap = cap;
+    TA.ekey = c->tile_ekey.as<uint64_t>();
+    TA.eval = c->tile_eval.as<uint32_t>();
+    TA.eprob = c->tile_eprob.as<double>();
+    TA.ecand = c->tile_ecand.as<uint32_t>();
+    HIPCHK(hipMemsetAsync(c->tile_small.p, 0, 8, s));
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * sizeof(uint64_t), s));
+    {
+      Timer t_score(c, &c->prof.ms_score, s);
+      HIPCHK(launch_tile(P, src, c->gqargs.as<GQArgs>(), nqr, nnr, planes, TA, s));
+      t_score.stop();
+    }
+    c->prof.score_launches += 1;
+    HIPCHK(hipMemcpyAsync(&hs[4], c->tile_small.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    nm = hs[4];
+    if (tdebug) {
+      uint32_t f = 0;
+      HIPCHK(hipMemcpy(&f, TA.dbg, 4, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[dk_tile] items %llu buckets %llu nvalid %llu entries %llu dict %u/%u check flags 0x%x\n",
+              (unsigned long long)nitems, (unsigned long long)nb, (unsigned long long)nvalid,
+              (unsigned long long)nm, TA.dict[0], TA.dict[1], f);
+    }
+    if (nm <= cap) break;
+    c->tile_ecap = nm + nm / 4 + 1024;  // the list outgrew the entries: once more, sized
+    if (attempt == 1) return fail(DK_E_STATE, "tiled match: entry count changed between runs");
+  }
+
+  // ---- the list in Duke's order: entries sorted by (query index, slot) ----
+  Timer t_gather(c, &c->prof.ms_gather, s);
+  ResultBufs& B = *R->bufs;
+  uint64_t* ek = c->tile_ekey.as<uint64_t>();
+  uint32_t* ev = c->tile_eval.as<uint32_t>();
+  const uint64_t cap = c->tile_ecap;
+  if (nm) {
+    HIPCHK(with_tmp(c, [&](void* t, size_t& b) { return sort_pairs_u64_u32(t, b, ek, ek + cap, ev, ev + cap, nm, s); }));
+  }
+  HIPCHK(B.d_cand.reserve(nm * 4 + 4, 0, s));
+  HIPCHK(B.d_kind.reserve(nm + 1, 0, s));
+  HIPCHK(B.d_prob.reserve(nm * 8 + 8, 0, s));
+  HIPCHK(B.d_qidx.reserve(nm * 4 + 4, 0, s));
+  MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(), B.d_qidx.as<uint32_t>()};
+  HIPCHK(launch_tile_emit(ek + cap, ev + cap, nm, c->tile_eprob.as<double>(), c->tile_ecand.as<uint32_t>(), ml, s));
+  HIPCHK(hipMemcpyAsync(c->h_small.p, c->counters.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint64_t scored = c->h_small.as<uint64_t>()[0];
+  const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
+  R->r.pairs_scored = scored;
+  R->r.pairs_generated = generated;
+  c->prof.pairs_scored += scored;
+  c->prof.pairs_generated += generated;
+  c->prof.score_bytes += sbytes;
+  HIPCHK(B.d_first.reserve((nq + 1) * 8, 0, s));
+  HIPCHK(launch_first(B.d_qidx.as<uint32_t>(), nm, nq, B.d_first.as<uint64_t>(), s));
+  R->r.nqueries = nq;
+  R->r.n = nm;
+  if (!(flags & DK_MATCH_DEVICE)) {
+    uint32_t* hc;
+    double* hp;
+    uint8_t* hk;
+    uint64_t* hf;
+    if (c->region.base) {
+      if (nm > c->region.cap)
+        return fail(DK_E_NOMEM, "match list needs more than %llu entries; the result region holds %llu",
+                    (unsigned long long)nm, (unsigned long long)c->region.cap);
+      hc = c->region.cand;
+      hp = c->region.prob;
+      hk = c->region.kind;
+      hf = c->region.first;
+    } else {
+      HIPCHK(B.h_first.reserve((nq + 1) * 8));
+      HIPCHK(B.h_cand.reserve(nm * 4 + 4, 0));
+      HIPCHK(B.h_prob.reserve(nm * 8 + 8, 0));
+      HIPCHK(B.h_kind.reserve(nm + 1, 0));
+      hc = B.h_cand.as<uint32_t>();
+      hp = B.h_prob.as<double>();
+      hk = B.h_kind.as<uint8_t>();
+      hf = B.h_first.as<uint64_t>();
+    }
+    Timer t_copy(c, &c->prof.ms_copy, s);
+    HIPCHK(hipMemcpyAsync(hc, B.d_cand.p, nm * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hp, B.d_prob.p, nm * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hk, B.d_kind.p, nm, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hf, B.d_first.p, (nq + 1) * 8, hipMemcpyDeviceToHost, s));
+    t_copy.stop();
+    R->r.first = hf;
+    R->r.candidate = hc;
+    R->r.prob = hp;
+    R->r.kind = hk;
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  t_gather.stop();
+  resolve_spans(c);
+  c->prof.ms_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return DK_OK;
+}
+
 static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
                      ResultHolder* R, bool contiguous) {
   hipStream_t s = c->stream;
@@ -2390,6 +2690,11 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   }
   const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
   bool sym = !lucene && contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
+  if (!sym && !lucene && !allpairs && nq > 0) {
+    t_gen.stop();
+    const int trc = tile_match(c, P, T, nq, flags, R, t0);
+    if (trc != 1) return trc;   // 1: not this schema / index -- the slot schedule below
+  }
   bool grouped = false;  // k_score_grouped: query slots padded to kScoreBlock
   const uint32_t r0 = nq ? query_rows[0] : 0;
   uint64_t* hs = c->h_small.as<uint64_t>();
@@ -2765,7 +3070,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       {
         Timer t_score(c, &c->prof.ms_score, s);
         if (gq)
-          HIPCHK(launch_score_gq(P, src, s0, s1 - s0, perm, c->gqargs.as<GQArgs>() + b, gq_nq, gq_nn, st[b], s));
+          HIPCHK(launch_score_gq(P, src, s0, s1 - s0, perm, c->gqargs.as<GQArgs>() + b, gq_nq, gq_nn, gqa.defer, st[b], s));
         else if (grouped)
           HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), gmode, st[b], s));
         else HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));

@@ -288,4 +288,10 @@ __device__ __forceinline__ double property_prob(const DevProp& D, double sim) {
   return java_max(0.0, v);
 }
 
+// [Duke 1.2] PropertyImpl.compare for a property with a comparator (QGram / Numeric roles
+// of k_score_gq / k_tile) + the start of Processor.compare's Math.max(0.0, .)
+__device__ __forceinline__ double gq_prob(double low, double high, double sim) {
+  return java_max(0.0, sim < 0.5 ? low : ((high - 0.5) * (sim * sim)) + 0.5);
+}
+
 }  // namespace dk

@@ -228,6 +228,9 @@ struct GQRoleQ {
   uint32_t rowb;          // bytes per row (replica positions x 8)
   int32_t prop, formula;
   double low, high;
+  // the screen's single-precision constants: low, high, max(0, low) (a candidate without
+  // grams), and the most PropertyImpl.compare can give over sim in [0, 1] (a deferred role)
+  float flow, fhigh, flow0, fub;
 };
 struct GQRoleN {
   const uint16_t* rlen;
@@ -255,7 +258,17 @@ struct alignas(16) GQArgs {
   uint64_t rorder[kMaxOrders];
   GQRoleQ q[kGroupedTabs];
   GQRoleN n[kGQMaxNum];
+  // k_score_gq's screen: a pair goes to the exact pass when its probability bound's odds
+  // reach `screen` (0: every valid pair); `defer`: the QGram role left to the exact pass
+  // (-1: none)
+  float screen;
+  int32_t defer;
+  uint32_t pad_[2];
 };
+// queue of screened pairs per wave (k_score_gq), and the bounds inside which a role's
+// single-precision probability keeps Bayes monotone and the odds accurate
+constexpr int kGQQueue = 128;
+constexpr float kScreenLo = 0.011f, kScreenHi = 0.989f;
 
 // The emission pass of the symmetric schedule: slots of the full candidate order (qoff /
 // wq / ranges as in PairSource) read their probability from the owner results.
@@ -457,9 +470,78 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                                 uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
                                 int mode, const StageOut& out, hipStream_t s);
+// k_tile (dk_tile.hip): the bucket-tiled schedule of GQArgs schemas.  Buckets are runs of
+// equal range starts in the sorted (range start << 32 | query index) keys of every (segment,
+// query) with candidates; an item is (bucket, chunk of 64 candidates, group of 256 queries).
+constexpr int kTileIdsPerRole = 64;  // per query and QGram role: its keys' dictionary ids
+constexpr uint32_t kTileMaxDict = 4095;  // dictionary ids per role (mask table rows + 1 <= 4096)
+constexpr uint32_t kTileMaxRows = 6144;  // mask-table rows of all roles (48 KB of LDS)
+constexpr uint32_t kTileQueryGroup = 512;  // queries of one item (its chunk's mask table reused)
+// per query (index qi): what k_tile reads of it, in one 64-B record (k_tile_qrec)
+struct TileQRec {
+  uint64_t ident;       // Processor.isSameAs
+  uint64_t key0;        // keys[0] (the duplicate filter)
+  uint16_t len[kGroupedTabs + kGQMaxNum];  // per role (QGram roles, then Numeric): len
+  uint8_t m1[kGroupedTabs];                // QGram roles: grams
+  uint8_t c0[kGroupedTabs];                // QGram roles: first unit
+  uint8_t ok[kGQMaxNum];                   // Numeric roles: parsed
+  uint8_t oc;                              // HashMap order class
+  uint8_t pad[6];
+  double num[kGQMaxNum];
+};
+static_assert(sizeof(TileQRec) == 64, "four 16-B loads");
+struct TileArgs {
+  const uint64_t* bkey;     // sorted keys (the bucket's queries: low 32 bits)
+  const uint32_t* bfirst;   // per bucket: its first key
+  const uint32_t* bnq;      // per bucket: queries
+  const uint32_t* bpos;     // per bucket: first replica position of the range
+  const uint32_t* bseg;     // per bucket: segment
+  const uint32_t* blen;     // per bucket: candidates
+  const uint64_t* bitem;    // per bucket: first item (exclusive prefix), nbuckets + 1
+  const uint32_t* ibucket;  // per item: its bucket
+  uint64_t nbuckets, nitems;
+  const uint16_t* lut[kGroupedTabs];  // per QGram role: bigram key -> dictionary id
+  uint32_t dict[kGroupedTabs];        // ids per role (row dict[a] of its mask table is zero)
+  uint32_t toff[kGroupedTabs];        // first mask-table row of role a
+  uint32_t tsize;                     // mask-table rows (dynamic LDS: 8 B each)
+  const uint16_t* qids;     // [qi][role][kTileIdsPerRole]
+  const TileQRec* qrec;     // [qi]
+  uint64_t* ecount;         // entries appended
+  uint64_t ecap;            // entry capacity (the host re-runs with more past it)
+  uint64_t* ekey;           // query index << 32 | slot t
+  uint32_t* eval;           // entry index (the sort's payload)
+  double* eprob;
+  uint32_t* ecand;          // candidate row | kind << kKindShift
+  uint64_t* counters;       // [0] pairs scored, [1] operand bytes
+  // DK_TILE_CHECK builds (bounds checks that flag instead of faulting): the bounds and the
+  // flag word the host prints under DK_TILE_DEBUG
+  uint64_t nq, nvalid, npos;
+  uint32_t* dbg;
+};
+// planes: 6 (every QGram set of at most 63 grams) or 7
+hipError_t launch_tile(const ScoreParams& P, const PairSource& src, const GQArgs* A, int nq, int nn,
+                       int planes, const TileArgs& T, hipStream_t s);
+hipError_t launch_tile_mark(const uint64_t* grams, uint64_t g0, uint64_t n, uint32_t* present, hipStream_t s);
+hipError_t launch_tile_lut(const uint32_t* scan, uint16_t* lut, hipStream_t s);
+hipError_t launch_tile_qids(const ScoreParams& P, const uint32_t* queries, uint64_t nq, const GQArgs* A,
+                            int nqr, const uint16_t* lut0, const uint16_t* lut1, uint16_t* qids,
+                            hipStream_t s);
+hipError_t launch_tile_qrec(const ScoreParams& P, const PairSource& src, const GQArgs* A, TileQRec* qrec,
+                            hipStream_t s);
+hipError_t launch_tile_bkeys(const PairSource& S, uint64_t* key, uint64_t* nvalid, hipStream_t s);
+hipError_t launch_tile_heads(const uint64_t* key, uint64_t n, uint32_t* head, hipStream_t s);
+hipError_t launch_tile_buckets(const PairSource& S, const uint64_t* key, uint64_t n, uint64_t nvalid,
+                               const uint32_t* head, const uint32_t* bid, uint64_t nb, uint32_t* bfirst,
+                               uint32_t* bpos, uint32_t* bseg, uint32_t* blen, uint32_t* bnq,
+                               uint64_t* nitems, hipStream_t s);
+hipError_t launch_tile_itemmap(const uint64_t* bitem, uint64_t nb, uint64_t nitems, uint32_t* ibucket,
+                               hipStream_t s);
+hipError_t launch_tile_emit(const uint64_t* skey, const uint32_t* sval, uint64_t n, const double* eprob,
+                            const uint32_t* ecand, const MatchList& out, hipStream_t s);
+
 // k_score_gq<nq, nn> (A: device copy of the host's GQArgs, whose nq / nn are passed too)
 hipError_t launch_score_gq(const ScoreParams& P, const PairSource& src, uint64_t slot0, uint64_t nslots,
-                           const uint32_t* perm, const GQArgs* A, int nq, int nn, const StageOut& out,
+                           const uint32_t* perm, const GQArgs* A, int nq, int nn, int defer, const StageOut& out,
                            hipStream_t s);
 // key[t] = chunk << 32 | first candidate's replica position of task t, val[t] = t;
 // cb[0..nchunks] = first task of each chunk

@@ -531,10 +531,6 @@ __device__ __forceinline__ rsrc_t gq_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, kRsrcWord3);
 }
 
-// [Duke 1.2] PropertyImpl.compare (a comparator is set: QGram / Numeric) + Math.max(0.0, .)
-__device__ __forceinline__ double gq_prob(double low, double high, double sim) {
-  return java_max(0.0, sim < 0.5 ? low : ((high - 0.5) * (sim * sim)) + 0.5);
-}
 
 // the query's values of one role (wave-uniform), staged in LDS once per task
 struct GQQuery {
@@ -545,13 +541,15 @@ struct GQQuery {
 static_assert(sizeof(GQQuery) == 16, "one ds_read_b128");
 static_assert(sizeof(GQArgs) % 16 == 0, "GQArgs copied to LDS in 16-B pieces");
 
-template <int NQ, int NN>
+template <int NQ, int NN, int DEF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_GQ, 8)))
 void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots,
                 const uint32_t* __restrict__ perm, const GQArgs* __restrict__ A, StageOut out) {
   constexpr int NR = NQ + NN;
-  constexpr int NQ1 = NQ > 0 ? NQ : 1, NN1 = NN > 0 ? NN : 1;
+  constexpr int NQ1 = NQ > 0 ? NQ : 1, NN1 = NN > 0 ? NN : 1, NR1 = NR > 0 ? NR : 1;
+  static_assert(DEF < NQ, "the deferred role is a QGram role");
   __shared__ uint32_t lds[kScoreBlock / 64][kGroupedTabs * kTabWords];
+  __shared__ uint64_t queue_lds[kScoreBlock / 64][kGQQueue];
   __shared__ GQQuery qlds[kScoreBlock / 64][kGroupedTabs + kGQMaxNum];
   __shared__ uint2 slds[kScoreBlock / 64][kMaxSegs];  // per segment: {first position, length}
   __shared__ GQArgs hlds[kScoreBlock / 64];
@@ -562,6 +560,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
   uint32_t* tabs = lds[wave];
   GQQuery* qv = qlds[wave];
   uint2* seg = slds[wave];
+  uint64_t* queue = queue_lds[wave];
   for (int e = (int)lane; e < (int)(sizeof(GQArgs) / 16); e += 64)
     reinterpret_cast<uint4*>(&hlds[wave])[e] = reinterpret_cast<const uint4*>(A)[e];
   GQLds* const hdr0 = (GQLds*)&hlds[wave];
@@ -657,51 +656,86 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
 
   uint32_t cnt = 0, scored = 0, bytes = 0;
   const uint64_t blk = task;  // staging block of the task (k_compact: block order = slot order)
-  for (int grp = 0; grp < ngroups; ++grp) {
-    GQLds* const H = gq_hdr(hdr0);
-    const uint32_t g = gn, fk = fkn;
-    uint32_t cq[NQ1];
-#pragma unroll
-    for (int a = 0; a < NQ; ++a) cq[a] = cqn[a];
-    const bool pair = (fk & 1u) != 0u;
-    // the roles' query values (LDS, uniform)
-    uint32_t qlen[NR > 0 ? NR : 1];
+
+  // the query's role constants (LDS, uniform)
+  auto query_roles = [&](uint32_t (&qlen)[NR1], bool (&perfect)[NQ1], uint32_t (&m1)[NQ1], uint32_t (&sd)[NQ1]) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) qlen[r] = gq_u((uint32_t)qv[r].len);
-    bool perfect[NQ1];
-    uint32_t m1[NQ1], sd[NQ1];
 #pragma unroll
     for (int a = 0; a < NQ; ++a) {
       m1[a] = gq_u((uint32_t)qv[a].m1);
       sd[a] = gq_u((uint32_t)qv[a].seed);
       perfect[a] = qlen[a] != kMissing && m1[a] > 0 && sd[a] != kGramSeedNone;
     }
-
-    // ---- back operands, one batch: key-word rows (past the lane's rows: no access),
-    //      lengths, filters, Numeric values ----
-    uint32_t nw[NQ1];  // key-word rows the lane reads (a pair, the query has a table)
-#pragma unroll
-    for (int a = 0; a < NQ; ++a) nw[a] = pair && perfect[a] ? (cq[a] + 3u) >> 2 : 0u;
-    uint64_t w0[GQRows<0>::v];
-    uint64_t w1[GQRows<1>::v];
+  };
+  // key-word rows [0, GQRows<a>) of role a at position g, nw of them in range (one batch)
+  auto issue_rows = [&](GQLds* H, auto ic, uint32_t g, uint32_t nw, uint64_t* w) {
+    constexpr int a = decltype(ic)::value;
+    const rsrc_t rh = gq_rsrc(gq_uptr(H->q[a].rows), gq_u(H->q[a].head_bytes));
+    const rsrc_t rt = gq_rsrc(gq_uptr(H->q[a].tail), gq_u(H->q[a].tail_bytes));
+    const uint32_t rowb = gq_u(H->q[a].rowb);
     const uint32_t g8 = g * 8u;
-    auto issue_rows = [&](auto ic, uint64_t* w) {
-      constexpr int a = decltype(ic)::value;
-      const rsrc_t rh = gq_rsrc(gq_uptr(H->q[a].rows), gq_u(H->q[a].head_bytes));
+#pragma unroll
+    for (int j = 0; j < GQRows<a>::v; ++j) {
+      const uint32_t off = g8 + (uint32_t)(j < kGroupedHeadRows ? j : j - kGroupedHeadRows) * rowb;
+      const uint32_t o = (DK_GQ_ABL & 4) ? 0xFFFFFFFFu : (uint32_t)j < nw ? off : 0xFFFFFFFFu;
+      w[j] = __builtin_bit_cast(uint64_t,
+                                __builtin_amdgcn_raw_buffer_load_b64(j < kGroupedHeadRows ? rh : rt, o, 0, 0));
+    }
+  };
+  // |Q ∩ C| of role a: the rows held in registers, then the rest kTailRows at a time
+  auto role_common = [&](GQLds* H, auto ic, uint32_t g, uint32_t nw, uint32_t sdv, const uint64_t* w) -> int {
+    constexpr int a = decltype(ic)::value;
+    const uint32_t* tab = tabs + a * kTabWords;
+    const uint32_t mult = gram_mult(sdv & 0xFFu);
+    const int sh = 24 - (int)(sdv >> 8);  // 32 - lt
+    int common = 0;
+#pragma unroll
+    for (int j = 0; j < GQRows<a>::v; ++j)
+      if (!DK_GQ_GUARD || __builtin_amdgcn_ballot_w64((uint32_t)j < nw))  // uniform: a lane has row j
+        if (!(DK_GQ_ABL & 1)) common += probe_word(tab, w[j], mult, sh);
+    if (__builtin_amdgcn_ballot_w64(nw > (uint32_t)GQRows<a>::v)) {
       const rsrc_t rt = gq_rsrc(gq_uptr(H->q[a].tail), gq_u(H->q[a].tail_bytes));
       const uint32_t rowb = gq_u(H->q[a].rowb);
+      const int nrows = (int)gq_u(H->q[a].nrows);
+      const uint32_t g8 = g * 8u;
+      for (int j = GQRows<a>::v; j < nrows; j += kTailRows) {
+        uint64_t wt[kTailRows];
 #pragma unroll
-      for (int j = 0; j < GQRows<a>::v; ++j) {
-        const uint32_t off = g8 + (uint32_t)(j < kGroupedHeadRows ? j : j - kGroupedHeadRows) * rowb;
-        const uint32_t o = (DK_GQ_ABL & 4) ? 0xFFFFFFFFu : (uint32_t)j < nw[a] ? off : 0xFFFFFFFFu;
-        w[j] = __builtin_bit_cast(uint64_t,
-                                  __builtin_amdgcn_raw_buffer_load_b64(j < kGroupedHeadRows ? rh : rt, o, 0, 0));
+        for (int i = 0; i < kTailRows; ++i) {
+          const uint32_t off = g8 + (uint32_t)(j + i - kGroupedHeadRows) * rowb;
+          wt[i] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
+                                                   rt, (uint32_t)(j + i) < nw ? off : 0xFFFFFFFFu, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < kTailRows; ++i) common += probe_word(tab, wt[i], mult, sh);
+        if (!__builtin_amdgcn_ballot_w64(nw > (uint32_t)(j + kTailRows))) break;
       }
-    };
-    if constexpr (NQ > 0) issue_rows(std::integral_constant<int, 0>{}, w0);
-    if constexpr (NQ > 1) issue_rows(std::integral_constant<int, 1>{}, w1);
-    const uint64_t rid = gq_ld(gq_uptr(H->rident), g);
-    const uint64_t rk = nkeys > 1 && fk > 1u ? gq_ld(gq_uptr(H->rkey0), g) : 0ull;
+    }
+    return common;
+  };
+
+  // ---- EXACT pass over queued pairs (lanes < n hold queue entries head..head+n-1, in
+  //      candidate order): the deferred role's rows and probes, every role's probability
+  //      in double precision, computeBayes in the visiting order, the decision, emission ----
+  auto exact = [&](uint32_t head, uint32_t n) {
+    GQLds* const H = gq_hdr(hdr0);
+    const bool act = lane < n;
+    const uint64_t ent = act ? queue[(head + lane) & (kGQQueue - 1)] : 0ull;
+    const uint32_t g = (uint32_t)ent;
+    uint32_t qlen[NR1], m1[NQ1], sd[NQ1];
+    bool perfect[NQ1];
+    query_roles(qlen, perfect, m1, sd);
+    int common[NQ1];
+    uint32_t cq[NQ1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) {
+      common[a] = (int)((ent >> (32 + 8 * a)) & 0xFFu);
+      cq[a] = (uint32_t)((ent >> (48 + 8 * a)) & 0xFFu);
+    }
+    uint64_t wd[DEF >= 0 ? GQRows<DEF < 0 ? 0 : DEF>::v : 1];
+    const uint32_t nwd = DEF >= 0 && act && perfect[DEF < 0 ? 0 : DEF] ? (cq[DEF < 0 ? 0 : DEF] + 3u) >> 2 : 0u;
+    if constexpr (DEF >= 0) issue_rows(H, std::integral_constant<int, DEF < 0 ? 0 : DEF>{}, g, nwd, wd);
     const uint32_t crow = gq_ld(gq_uptr(H->rowof), g);
     uint32_t lq[NQ1], ln[NN1], cok[NN1];
     double cn[NN1];
@@ -713,58 +747,19 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
       cn[b] = gq_ld(gq_uptr(H->n[b].rnum), g);
       cok[b] = gq_ld(gq_uptr(H->n[b].rnumok), g);
     }
-    // the next group's front (past the last group: position 0, no pair)
-    load_front(H, grp + 1, gn, fkn, cqn);
-
-    // ---- filters: Processor.isSameAs, a superseded base position, a candidate already
-    //      returned under an earlier key function (Duke's candidate set) ----
-    const int kf = (int)(fk >> 1);
-    bool valid = pair && rid != qident && rid != kDeadIdent;
-    if (kf > 0) valid = valid && rk != qk0;
-    for (int j = 1; j < nkeys - 1; ++j)  // more than two key functions
-      if (j < kf) valid = valid && S.rkeys[j][g] != S.qkeys[j][q];
-
-    // ---- every role's probability, then computeBayes in the visiting order ----
-    double pp[NR > 0 ? NR : 1];
-    bool ap[NR > 0 ? NR : 1];
-    uint32_t by = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
-    auto score_role = [&](auto ic, const uint64_t* w) {
-      constexpr int a = decltype(ic)::value;
-      const bool present = valid && lq[a] != kMissing;
+    if constexpr (DEF >= 0)
+      if (perfect[DEF < 0 ? 0 : DEF]) common[DEF < 0 ? 0 : DEF] = role_common(H, std::integral_constant<int, DEF < 0 ? 0 : DEF>{}, g, nwd, sd[DEF < 0 ? 0 : DEF], wd);
+    double pp[NR1];
+    bool ap[NR1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) {
+      const bool present = act && lq[a] != kMissing;
       const bool cmp = present && lq[a] > 0 && qlen[a] > 0;
       double sim = 0.0;
       if (qlen[a] != kMissing) {
-        if (present) by += 2u;
-        if (cmp) by += 6u + 2u * cq[a];
         if (perfect[a]) {
-          const uint32_t* tab = tabs + a * kTabWords;
-          const uint32_t mult = gram_mult(sd[a] & 0xFFu);
-          const int sh = 24 - (int)(sd[a] >> 8);  // 32 - lt
-          int common = 0;
-#pragma unroll
-          for (int j = 0; j < GQRows<a>::v; ++j)
-            if (!DK_GQ_GUARD || __builtin_amdgcn_ballot_w64((uint32_t)j < nw[a]))  // uniform: a lane has row j
-              if (!(DK_GQ_ABL & 1)) common += probe_word(tab, w[j], mult, sh);
-          // sets past the rows held in registers: the rest DK_GROUPED_TAIL rows at a time
-          if (__builtin_amdgcn_ballot_w64(nw[a] > (uint32_t)GQRows<a>::v)) {
-            const rsrc_t rt = gq_rsrc(gq_uptr(H->q[a].tail), gq_u(H->q[a].tail_bytes));
-            const uint32_t rowb = gq_u(H->q[a].rowb);
-            const int nrows = (int)gq_u(H->q[a].nrows);
-            for (int j = GQRows<a>::v; j < nrows; j += kTailRows) {
-              uint64_t wt[kTailRows];
-#pragma unroll
-              for (int i = 0; i < kTailRows; ++i) {
-                const uint32_t off = g8 + (uint32_t)(j + i - kGroupedHeadRows) * rowb;
-                wt[i] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
-                                                         rt, (uint32_t)(j + i) < nw[a] ? off : 0xFFFFFFFFu, 0, 0));
-              }
-#pragma unroll
-              for (int i = 0; i < kTailRows; ++i) common += probe_word(tab, wt[i], mult, sh);
-              if (!__builtin_amdgcn_ballot_w64(nw[a] > (uint32_t)(j + kTailRows))) break;
-            }
-          }
           const int m2 = cmp ? (int)cq[a] : 0;
-          if (m2 > 0) sim = (DK_GQ_ABL & 2) ? (double)common * 0.015625 : qgram_formula(common, (int)m1[a], m2, (int)gq_u(qv[a].pad));
+          if (m2 > 0) sim = (DK_GQ_ABL & 2) ? (double)common[a] * 0.015625 : qgram_formula(common[a], (int)m1[a], m2, (int)gq_u(qv[a].pad));
         } else {  // no perfect hash for the query: the sorted lists (rare), as k_score_grouped
           const DevProp& D = P.props[gq_u((uint32_t)H->q[a].prop)];
           sim = qgram_generic<uint8_t>(D, P.rstride, q, g, crow, (int)m1[a], (int)qlen[a], (int)lq[a], cmp);
@@ -772,21 +767,15 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
       }
       pp[a] = cmp ? gq_prob(H->q[a].low, H->q[a].high, sim) : 0.0;
       ap[a] = present;
-    };
-    if constexpr (NQ > 0) score_role(std::integral_constant<int, 0>{}, w0);
-    if constexpr (NQ > 1) score_role(std::integral_constant<int, 1>{}, w1);
+    }
 #pragma unroll
     for (int b = 0; b < NN; ++b) {
-      const bool present = valid && ln[b] != kMissing;
+      const bool present = act && ln[b] != kMissing;
       const bool cmp = present && ln[b] > 0 && qlen[NQ + b] > 0;
       double sim = 0.0;
-      if (qlen[NQ + b] != kMissing) {
-        if (present) by += 2u;
-        if (cmp) {
-          const GQQuery v = qv[NQ + b];
-          sim = (DK_GQ_ABL & 2) ? cn[b] * v.num : numeric(v.num, v.ok != 0, cn[b], cok[b] != 0u, H->n[b].min_ratio);
-          by += 9u;  // rnum + rnumok
-        }
+      if (qlen[NQ + b] != kMissing && cmp) {
+        const GQQuery v = qv[NQ + b];
+        sim = (DK_GQ_ABL & 2) ? cn[b] * v.num : numeric(v.num, v.ok != 0, cn[b], cok[b] != 0u, H->n[b].min_ratio);
       }
       pp[NQ + b] = cmp ? gq_prob(H->n[b].low, H->n[b].high, sim) : 0.0;
       ap[NQ + b] = present;
@@ -810,9 +799,8 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
       const double nb = (DK_GQ_ABL & 2) ? prob * x : compute_bayes(prob, x);
       prob = use ? nb : prob;
     }
-
     // [Duke 1.2] Processor.compareCandidatesSimple; block-ordered compaction within the task
-    const uint32_t kind = valid ? decide(prob, H->threshold, H->maybe) : 0u;
+    const uint32_t kind = act ? decide(prob, H->threshold, H->maybe) : 0u;
     const uint64_t em = __ballot(kind != 0u);
     if (kind != 0u) {
       const uint64_t e = blk * kScoreBlock + cnt + mask_rank(em);
@@ -821,8 +809,139 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
       gq_st(gq_uptr(H->oqidx), e, qi);
     }
     cnt += (uint32_t)__popcll(em);
+  };
+
+  // ---- SCREEN pass, per group of 64 candidates: the non-deferred QGram roles' counts and
+  //      the Numeric roles, then a single-precision upper bound of the pair's probability
+  //      (the deferred role at its maximum); the pairs whose bound can reach the list go to
+  //      the queue, the exact pass takes 64 of them at a time ----
+  uint32_t qn = 0, qh = 0;  // queue: pushed, taken
+  for (int grp = 0; grp < ngroups; ++grp) {
+    GQLds* const H = gq_hdr(hdr0);
+    const uint32_t g = gn, fk = fkn;
+    uint32_t cq[NQ1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) cq[a] = cqn[a];
+    const bool pair = (fk & 1u) != 0u;
+    uint32_t qlen[NR1], m1[NQ1], sd[NQ1];
+    bool perfect[NQ1];
+    query_roles(qlen, perfect, m1, sd);
+
+    // ---- back operands, one batch: key-word rows of the screened roles, lengths, filters,
+    //      Numeric values ----
+    uint32_t nw[NQ1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) nw[a] = a != DEF && pair && perfect[a] ? (cq[a] + 3u) >> 2 : 0u;
+    uint64_t w0[DEF == 0 ? 1 : GQRows<0>::v];
+    uint64_t w1[DEF == 1 ? 1 : GQRows<1>::v];
+    if constexpr (NQ > 0 && DEF != 0) issue_rows(H, std::integral_constant<int, 0>{}, g, nw[0], w0);
+    if constexpr (NQ > 1 && DEF != 1) issue_rows(H, std::integral_constant<int, 1>{}, g, nw[1], w1);
+    const uint64_t rid = gq_ld(gq_uptr(H->rident), g);
+    const uint64_t rk = nkeys > 1 && fk > 1u ? gq_ld(gq_uptr(H->rkey0), g) : 0ull;
+    uint32_t lq[NQ1], ln[NN1], cok[NN1];
+    double cn[NN1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) lq[a] = gq_ld(gq_uptr(H->q[a].rlen), g);
+#pragma unroll
+    for (int b = 0; b < NN; ++b) {
+      ln[b] = gq_ld(gq_uptr(H->n[b].rlen), g);
+      cn[b] = gq_ld(gq_uptr(H->n[b].rnum), g);
+      cok[b] = gq_ld(gq_uptr(H->n[b].rnumok), g);
+    }
+    // the next group's front (past the last group: position 0, no pair)
+    load_front(H, grp + 1, gn, fkn, cqn);
+
+    // ---- filters: Processor.isSameAs, a superseded base position, a candidate already
+    //      returned under an earlier key function (Duke's candidate set) ----
+    const int kf = (int)(fk >> 1);
+    bool valid = pair && rid != qident && rid != kDeadIdent;
+    if (kf > 0) valid = valid && rk != qk0;
+    for (int j = 1; j < nkeys - 1; ++j)  // more than two key functions
+      if (j < kf) valid = valid && S.rkeys[j][g] != S.qkeys[j][q];
+
+    // ---- the bound: odds = prod x / (1 - x) over the roles applied (the HashMap order does
+    //      not change the product); a role whose bound is outside [kScreenLo, kScreenHi]
+    //      (where single precision is not enough, or Bayes is not monotone) sends the pair on ----
+    uint32_t by = valid ? 9u : 0u;  // two row ids + decision (SURVEY §8d B_pair)
+    float odds = 1.0f;
+    bool wide = false;
+    int common[NQ1];
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) common[a] = 0;
+    auto screen_x = [&](float x) {
+      if (!(x >= kScreenLo && x <= kScreenHi)) wide = true;
+      else odds *= x * __builtin_amdgcn_rcpf(1.0f - x);
+    };
+    auto screen_role = [&](auto ic, const uint64_t* w) {
+      constexpr int a = decltype(ic)::value;
+      if (qlen[a] == kMissing) return;
+      const bool present = valid && lq[a] != kMissing;
+      const bool cmp = present && lq[a] > 0 && qlen[a] > 0;
+      if (present) by += 2u;
+      if (cmp) by += 6u + 2u * cq[a];
+      if constexpr (a != DEF)
+        if (perfect[a]) common[a] = role_common(H, ic, g, nw[a], sd[a], w);
+      if (!present) return;
+      float x;
+      if (!cmp) {
+        x = 0.0f;
+      } else if (a == DEF || !perfect[a] || cq[a] == 0u) {
+        x = cq[a] == 0u && perfect[a] ? H->q[a].flow0 : H->q[a].fub;
+      } else {  // sim in [s (1 - 1e-5), s (1 + 1e-5)]: the f32 quotient is within 2 ulp
+        const int f = (int)gq_u(qv[a].pad);
+        const float c = (float)common[a], fm1 = (float)m1[a], fm2 = (float)cq[a];
+        const float num = f == DK_QGRAM_DICE ? 2.0f * c : c;
+        const float den = f == DK_QGRAM_JACCARD ? fm1 + fm2 - c : f == DK_QGRAM_DICE ? fm1 + fm2 : fminf(fm1, fm2);
+        const float sm = num * __builtin_amdgcn_rcpf(den);
+        const float slo = sm * (1.0f - 1e-5f), shi = sm * (1.0f + 1e-5f);
+        const float hi5 = H->q[a].fhigh - 0.5f;
+        float xb = slo < 0.5f ? H->q[a].flow : -1.0f;
+        if (shi >= 0.5f) {
+          const float s0 = fmaxf(slo, 0.5f);
+          xb = fmaxf(xb, fmaxf(hi5 * (s0 * s0) + 0.5f, hi5 * (shi * shi) + 0.5f));
+        }
+        x = fmaxf(xb, 0.0f);
+      }
+      screen_x(x);
+    };
+    if constexpr (NQ > 0) screen_role(std::integral_constant<int, 0>{}, w0);
+    if constexpr (NQ > 1) screen_role(std::integral_constant<int, 1>{}, w1);
+#pragma unroll
+    for (int b = 0; b < NN; ++b) {
+      if (qlen[NQ + b] == kMissing) continue;
+      const bool present = valid && ln[b] != kMissing;
+      const bool cmp = present && ln[b] > 0 && qlen[NQ + b] > 0;
+      if (present) by += 2u;
+      if (!present) continue;
+      double x = 0.0;
+      if (cmp) {
+        const GQQuery v = qv[NQ + b];
+        x = gq_prob(H->n[b].low, H->n[b].high,
+                    numeric(v.num, v.ok != 0, cn[b], cok[b] != 0u, H->n[b].min_ratio));
+        by += 9u;  // rnum + rnumok
+      }
+      screen_x((float)x);
+    }
+    const bool pass = valid && (wide || odds >= H->screen);
+    const uint64_t pm = __ballot(pass);
+    if (pass) {
+      uint64_t ent = (uint64_t)g;
+#pragma unroll
+      for (int a = 0; a < NQ; ++a) ent |= (uint64_t)((uint32_t)common[a] & 0xFFu) << (32 + 8 * a) | (uint64_t)cq[a] << (48 + 8 * a);
+      queue[(qn + mask_rank(pm)) & (kGQQueue - 1)] = ent;
+    }
+    qn += (uint32_t)__popcll(pm);
     scored += valid ? 1u : 0u;
     bytes += by;
+    if (qn - qh >= 64u) {
+      wave_lds_sync();
+      exact(qh, 64u);
+      qh += 64u;
+    }
+  }
+  if (qn > qh) {
+    wave_lds_sync();
+    exact(qh, qn - qh);
   }
   const uint32_t ss = wave_sum_u32(scored), sbytes = wave_sum_u32(bytes);
   if (lane == 0) {
@@ -833,19 +952,21 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
 }
 
 hipError_t launch_score_gq(const ScoreParams& P, const PairSource& src, uint64_t slot0, uint64_t nslots,
-                           const uint32_t* perm, const GQArgs* A, int nq, int nn, const StageOut& out,
-                           hipStream_t s) {
+                           const uint32_t* perm, const GQArgs* A, int nq, int nn, int defer,
+                           const StageOut& out, hipStream_t s) {
   if (nslots == 0) return hipSuccess;
   if (nslots % kScoreBlock || slot0 % kScoreBlock) return hipErrorInvalidValue;
   const uint64_t ntask = nslots / kScoreBlock;
   const unsigned grid = (unsigned)((ntask + kScoreBlock / 64 - 1) / (kScoreBlock / 64));
-#define DK_GQ_CASE(NQ_, NN_)                                                                  \
-  if (nq == NQ_ && nn == NN_) {                                                               \
-    k_score_gq<NQ_, NN_><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, A, out);   \
-    return hipGetLastError();                                                                 \
+#define DK_GQ_CASE(NQ_, NN_, DEF_)                                                                 \
+  if (nq == NQ_ && nn == NN_ && defer == DEF_) {                                                   \
+    k_score_gq<NQ_, NN_, DEF_><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, A, out);  \
+    return hipGetLastError();                                                                      \
   }
-  DK_GQ_CASE(1, 0) DK_GQ_CASE(1, 1) DK_GQ_CASE(1, 2) DK_GQ_CASE(1, 3)
-  DK_GQ_CASE(2, 0) DK_GQ_CASE(2, 1) DK_GQ_CASE(2, 2) DK_GQ_CASE(2, 3)
+  DK_GQ_CASE(1, 0, -1) DK_GQ_CASE(1, 1, -1) DK_GQ_CASE(1, 2, -1) DK_GQ_CASE(1, 3, -1)
+  DK_GQ_CASE(2, 0, -1) DK_GQ_CASE(2, 1, -1) DK_GQ_CASE(2, 2, -1) DK_GQ_CASE(2, 3, -1)
+  DK_GQ_CASE(2, 0, 0) DK_GQ_CASE(2, 1, 0) DK_GQ_CASE(2, 2, 0) DK_GQ_CASE(2, 3, 0)
+  DK_GQ_CASE(2, 0, 1) DK_GQ_CASE(2, 1, 1) DK_GQ_CASE(2, 2, 1) DK_GQ_CASE(2, 3, 1)
 #undef DK_GQ_CASE
   return hipErrorInvalidValue;
 }

@@ -9,6 +9,8 @@ Processor.compare visits them: the iteration order of the record's HashMap.
 """
 from __future__ import annotations
 
+import os
+import struct
 import xml.etree.ElementTree as ET
 from dataclasses import dataclass, field
 
@@ -190,19 +192,19 @@ class DukeConfig:
             raise UnsupportedComparator(
                 f"up to {hi} record properties: past 48 a record's HashMap grows past "
                 "capacity 64 (not GPU-eligible)")
-        caps = sorted({hashmap_capacity(k) for k in range(lo, hi + 1)})
+        caps = sorted({class_key(k) for k in range(lo, hi + 1)})
         keys = names + synth + [DELETED_PROPERTY_NAME]
         scored = {p.name: p for p in self.scored_properties()}
         orders = []
         for cap in caps:
-            order = java_hashmap_order(keys, cap)
+            order = class_order(keys, cap)
             orders.append([scored[n] for n in order if n in scored])
         # every data source must give its records the same visiting orders (a different
         # column order only matters for keys sharing a HashMap bucket)
         for ds in self.data_sources[1:]:
             alt, _, _ = self._record_keys(ds)
             for cap, want in zip(caps, orders):
-                got = [n for n in java_hashmap_order(alt + synth + [DELETED_PROPERTY_NAME], cap)
+                got = [n for n in class_order(alt + synth + [DELETED_PROPERTY_NAME], cap)
                        if n in scored]
                 if got != [p.name for p in want]:
                     raise UnsupportedComparator(
@@ -220,7 +222,7 @@ class DukeConfig:
     def record_class(self, record, caps):
         """The order class of a record (index into order_classes()[0]): its HashMap's
         capacity from the number of properties it holds values for."""
-        return caps.index(hashmap_capacity(len(record.get_properties())))
+        return caps.index(class_key(len(record.get_properties())))
 
     def to_schema(self, mode, nkeys):
         """(dk_schema, props in its order); with several order classes the schema carries
@@ -251,13 +253,63 @@ def java_string_hash(s: str) -> int:
     return h
 
 
-def hashmap_capacity(nkeys):
-    """java.util.HashMap's table size after `nkeys` puts (default 16, doubled when the size
-    passes 0.75 of it)."""
-    cap = 16
-    while nkeys > cap * 0.75:
+# How a record's RecordImpl HashMap gets its capacity (SURVEY a-7).  Duke's source is absent,
+# so which construction the reference's records go through is NOT pinned:
+#   "incremental" -- `new HashMap<>()` then one put per key (IncrementalDataSource.java:67-98
+#                    builds the property map key by key): 16, doubled when size > 0.75 * cap.
+#                    A JDK 19+ copy constructor (`new HashMap<>(m)`, ceil(s / 0.75)) sizes
+#                    every s the same way.
+#   "copy_jdk8"   -- `new HashMap<>(m)` on JDK 8..18: putMapEntries sizes the table to
+#                    tableSizeFor((int)(s / 0.75f + 1)), one doubling earlier at s = 12, 24, 48.
+HASHMAP_CONSTRUCTIONS = ("incremental", "copy_jdk8")
+HASHMAP_CONSTRUCTION = os.environ.get("DUKEHIP_HASHMAP_CONSTRUCTION", "incremental")
+
+
+def _f32(x):
+    return struct.unpack("f", struct.pack("f", x))[0]
+
+
+def _table_size_for(n):
+    cap = 1
+    while cap < n:
         cap *= 2
     return cap
+
+
+def hashmap_capacity(nkeys, construction=None):
+    """java.util.HashMap's table size for a map of `nkeys` keys built by `construction`
+    (default HASHMAP_CONSTRUCTION; see above)."""
+    construction = construction or HASHMAP_CONSTRUCTION
+    if construction == "incremental":
+        cap = 16
+        while nkeys > cap * 0.75:
+            cap *= 2
+        return cap
+    if construction == "copy_jdk8":
+        # float arithmetic as putMapEntries: ft = s / 0.75f + 1.0f, t = (int) ft
+        t = int(_f32(_f32(float(nkeys)) / _f32(0.75)) + 1.0)
+        return _table_size_for(max(t, 1)) if nkeys else 16
+    raise ValueError(f"unknown HashMap construction {construction!r} "
+                     f"(one of {HASHMAP_CONSTRUCTIONS})")
+
+
+def class_key(nkeys, construction=None):
+    """What fixes the iteration order of a record map of `nkeys` keys: its capacity
+    ("incremental"), or (capacity of the source map, capacity of the copy) ("copy_jdk8": a
+    copy inserts the source's entries in the source's iteration order)."""
+    construction = construction or HASHMAP_CONSTRUCTION
+    if construction == "incremental":
+        return hashmap_capacity(nkeys, "incremental")
+    return (hashmap_capacity(nkeys, "incremental"), hashmap_capacity(nkeys, construction))
+
+
+def class_order(keys, key):
+    """Iteration order of the record map of order class `key` (class_key) holding `keys`
+    (a record holding fewer keeps their relative order)."""
+    if isinstance(key, tuple):
+        src, cap = key
+        return java_hashmap_order(java_hashmap_order(keys, src), cap)
+    return java_hashmap_order(keys, key)
 
 
 def java_hashmap_order(keys, cap=None):

@@ -102,16 +102,23 @@ def test_reference_schema_dedup_gpu():
 # configs[2] (QGram DICE/JACCARD + Numeric min-ratio 0.9, cross-group key blocking) and
 # configs[4] (WeightedLevenshtein + QGram q=3 JACCARD, key = first two tokens) in linkage
 # ---------------------------------------------------------------------------------------
-@pytest.mark.parametrize("variant", ["default", "legacy_grouped", "tail_resource", "row_resources",
+@pytest.mark.parametrize("variant", ["default", "gq_defer1", "gq_nodefer", "gq_noscreen", "tile",
+                                     "legacy_grouped", "tail_resource", "row_resources",
                                      "no_grouped", "host_grams"])
 def test_config2_linkage_qgram_numeric(variant, monkeypatch):
     """configs[2]'s schema through each of its device paths, bit-exact against the oracle:
-    k_score_gq (default; its head / tail row resources are the layout a 10M x 10M replica
-    takes, at any size), k_score_grouped (DK_GQ=0) with one buffer resource per property,
-    with head and tail resources (DK_GROUPED_ROW=1) or a resource per tail row
+    k_score_gq (default: the screen with QGram role 0 deferred to the exact pass; role 1
+    deferred; no role deferred; no screen -- every valid pair takes the exact pass; its head /
+    tail row resources are the layout a 10M x 10M replica takes, at any size), the
+    bucket-tiled k_tile (DK_TILE=1), k_score_grouped (DK_GQ=0) with one buffer resource per
+    property, with head and tail resources (DK_GROUPED_ROW=1) or a resource per tail row
     (DK_GROUPED_ROW=2: replicas past k_score_gq's resources), k_score_nodp (DK_GROUPED=0),
     and q-gram sets built on the host instead of the device (DK_DEV_GRAMS=0)."""
-    env = {"legacy_grouped": [("DK_GQ", "0")],
+    env = {"gq_defer1": [("DK_GQ_DEFER", "1")],
+           "gq_nodefer": [("DK_GQ_DEFER", "-1")],
+           "gq_noscreen": [("DK_GQ_SCREEN", "0")],
+           "tile": [("DK_TILE", "1")],
+           "legacy_grouped": [("DK_GQ", "0")],
            "tail_resource": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "1")],
            "row_resources": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "2")],
            "no_grouped": [("DK_GROUPED", "0")],
@@ -127,6 +134,37 @@ def test_config2_linkage_qgram_numeric(variant, monkeypatch):
     res, ref = run_both(props, vals, synth.keys_config2(p), mode="linkage", group=group,
                         threshold=0.9, maybe=0.7, queries=np.arange(2500, len(group)))
     assert res.n > 100
+    assert_same(res, ref)
+
+
+@pytest.mark.parametrize("case", ["bench", "low_maybe", "match_only", "zero_low", "overlap", "wide_high"])
+def test_config2_screen_edges(case, monkeypatch):
+    """k_score_gq's single-precision screen only drops pairs whose exact probability cannot
+    reach the list: bit-exact lists against the oracle where the bound is tight (the bench's
+    configuration, thresholds that put many pairs near the bound), where it must give up
+    (low = 0: the zero factor; high = 0.995: a role bound past kScreenHi), and for the
+    OVERLAP formula; with the role deferred or not."""
+    monkeypatch.setenv("DK_GQ_DEFER", "1" if case in ("zero_low", "overlap") else "0")
+    p, group = synth.linkage_persons(2000)
+    qlow, qhigh, formula, th, mb = 0.1, 0.9, A.QGRAM_DICE, 0.9, 0.7
+    if case == "low_maybe":
+        th, mb = 0.8, 0.35
+    elif case == "match_only":
+        th, mb = 0.6, 0.0
+    elif case == "zero_low":
+        qlow = 0.0
+    elif case == "overlap":
+        formula = A.QGRAM_OVERLAP
+    elif case == "wide_high":
+        qhigh = 0.995
+    props = [{"comparator": QG, "low": qlow, "high": qhigh, "q": 2, "formula": formula},
+             {"comparator": QG, "low": 0.1, "high": 0.8, "q": 2, "formula": A.QGRAM_JACCARD},
+             {"comparator": NUM, "low": 0.2, "high": 0.6, "min_ratio": 0.9996},
+             {"comparator": NUM, "low": 0.4, "high": 0.75, "min_ratio": 0.9}]
+    vals = [p["name"], p["address"], p["birthyear"], p["zip"]]
+    res, ref = run_both(props, vals, synth.keys_config2(p), mode="linkage", group=group,
+                        threshold=th, maybe=mb, queries=np.arange(2000, len(group)))
+    assert res.n > 50
     assert_same(res, ref)
 
 
