@@ -133,13 +133,17 @@ def build_workload(args):
         p, group = synth.linkage_persons(n)
         # BIRTHYEAR's min-ratio rejects every non-equal year of 1930..2010 (2009 / 2010 =
         # 0.99950 < 0.9996): with 0.9 every same-bucket pair had a near-constant 0.69 factor and
-        # the list held ~10 % of the scored pairs; the low / high values
-        # (SURVEY §8d names the comparators, not them) put the list near one entry per query
+        # the list held ~10 % of the scored pairs.  ADDRESS low = 0.05: a
+        # pair whose addresses share under half their bigrams cannot reach the list however
+        # alike the names are (with 0.1, same-name / same-year / near-zip strangers did, and
+        # their number grew with the bucket size: 1.6 entries per query at 1M, 13 at 10M).
+        # The list is then the perturbed copies (30 % of group 2): ~0.28 entries per query
+        # at every size.  SURVEY §8d names the comparators, not these values.
         w.update(desc=f"BASELINE configs[2]: person record linkage {n} x {len(group) - n}, QGram "
                       "q=2 DICE/JACCARD + Numeric BIRTHYEAR (min-ratio 0.9996: equal years) / ZIP "
                       "(min-ratio 0.9), cross-group key blocking",
                  props=[prop("NAME", A.CMP_QGRAM, 0.1, 0.9, q=2, formula=A.QGRAM_DICE),
-                        prop("ADDRESS", A.CMP_QGRAM, 0.1, 0.8, q=2, formula=A.QGRAM_JACCARD),
+                        prop("ADDRESS", A.CMP_QGRAM, 0.05, 0.8, q=2, formula=A.QGRAM_JACCARD),
                         prop("BIRTHYEAR", A.CMP_NUMERIC, 0.2, 0.6, min_ratio=0.9996),
                         prop("ZIP", A.CMP_NUMERIC, 0.4, 0.75, min_ratio=0.9)],
                  values={"NAME": p["name"], "ADDRESS": p["address"], "BIRTHYEAR": p["birthyear"],

@@ -475,7 +475,7 @@ hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uin
 //  * The waves of a SIMD (DK_WAVES_GQ) cover that one round trip.
 // =======================================================================================
 #ifndef DK_WAVES_GQ
-#define DK_WAVES_GQ 5  // k_score_gq waves per SIMD
+#define DK_WAVES_GQ 6  // k_score_gq waves per SIMD (<= 80 VGPRs; 23 KB LDS per 4 waves: 6 fit)
 #endif
 #ifndef DK_GQ_ABL
 #define DK_GQ_ABL 0  // timing ablations only (wrong results): 1 probes, 2 f64 math, 4 row traffic
@@ -542,7 +542,7 @@ static_assert(sizeof(GQQuery) == 16, "one ds_read_b128");
 static_assert(sizeof(GQArgs) % 16 == 0, "GQArgs copied to LDS in 16-B pieces");
 
 template <int NQ, int NN, int DEF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_GQ, 8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEF < 0 && NQ == 2 ? DK_WAVES_GQ - 1 : DK_WAVES_GQ, 8)))
 void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots,
                 const uint32_t* __restrict__ perm, const GQArgs* __restrict__ A, StageOut out) {
   constexpr int NR = NQ + NN;
@@ -963,10 +963,14 @@ hipError_t launch_score_gq(const ScoreParams& P, const PairSource& src, uint64_t
     k_score_gq<NQ_, NN_, DEF_><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, perm, A, out);  \
     return hipGetLastError();                                                                      \
   }
+#ifdef DK_GQ_MIN  // timing variants (csrc/Makefile gvariant): configs[2]'s case only
+  DK_GQ_CASE(2, 2, 0)
+#else
   DK_GQ_CASE(1, 0, -1) DK_GQ_CASE(1, 1, -1) DK_GQ_CASE(1, 2, -1) DK_GQ_CASE(1, 3, -1)
   DK_GQ_CASE(2, 0, -1) DK_GQ_CASE(2, 1, -1) DK_GQ_CASE(2, 2, -1) DK_GQ_CASE(2, 3, -1)
   DK_GQ_CASE(2, 0, 0) DK_GQ_CASE(2, 1, 0) DK_GQ_CASE(2, 2, 0) DK_GQ_CASE(2, 3, 0)
   DK_GQ_CASE(2, 0, 1) DK_GQ_CASE(2, 1, 1) DK_GQ_CASE(2, 2, 1) DK_GQ_CASE(2, 3, 1)
+#endif
 #undef DK_GQ_CASE
   return hipErrorInvalidValue;
 }
