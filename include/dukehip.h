@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DK_ABI_VERSION 7
+#define DK_ABI_VERSION 8
 
 /* status codes */
 #define DK_OK 0
@@ -193,6 +193,10 @@ typedef struct dk_profile {
   uint64_t full_builds;   /* blocking-table builds that sorted every usable row */
   uint64_t delta_builds;  /* builds that re-sorted only the rows added since the last full
                              one (sorted base + sorted delta) */
+  uint64_t replica_positions; /* the last dk_match's candidate replica: positions (rstride) */
+  uint64_t gram_row_bytes;    /* and the bytes of its largest QGram property's key-word rows
+                                 (rows x positions x 8; past 4 GiB the grouped kernels address
+                                 them through head / tail buffer resources) */
 } dk_profile;
 
 typedef struct dk_ctx dk_ctx;

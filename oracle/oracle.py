@@ -243,6 +243,43 @@ class OracleTable:
                            arr(alive, np.uint8), self.off, self.chars, self.present,
                            self.key_off, self.key_chars, arr(oclass, np.uint8))
 
+    @classmethod
+    def from_packed(cls, props, columns, keys, ident, group=None, threshold=0.9, maybe=0.0,
+                    mode="dedup"):
+        """A table from already-packed columns (full-size tests): columns[p] / keys[k] =
+        (offsets uint32 [n+1], UTF-16 units uint16), every value present."""
+        self = cls.__new__(cls)
+        n = len(ident)
+        self.n = n
+        self._keep = []
+        self.props = (Prop * max(1, len(props)))()
+        for i, pr in enumerate(props):
+            self.props[i] = Prop(pr["comparator"], pr["low"], pr["high"], pr.get("q", 2),
+                                 pr.get("formula", 0), pr.get("tokenizer", 0),
+                                 pr.get("min_ratio", 0.0))
+        self.schema = Schema(len(props), self.props, threshold, maybe, MODE[mode], len(keys))
+
+        def keep(a, dt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            self._keep.append(a)
+            return a.ctypes.data
+
+        pres = np.ones(n, np.uint8)
+        self.off = (C.c_void_p * max(1, len(columns)))()
+        self.chars = (C.c_void_p * max(1, len(columns)))()
+        self.present = (C.c_void_p * max(1, len(columns)))()
+        for p, (o, u) in enumerate(columns):
+            self.off[p], self.chars[p] = keep(o, np.uint32), keep(u, np.uint16)
+            self.present[p] = keep(pres, np.uint8)
+        self.key_off = (C.c_void_p * max(1, len(keys)))()
+        self.key_chars = (C.c_void_p * max(1, len(keys)))()
+        for k, (o, u) in enumerate(keys):
+            self.key_off[k], self.key_chars[k] = keep(o, np.uint32), keep(u, np.uint16)
+        self.table = Table(n, keep(ident, np.uint64), None if group is None else keep(group, np.uint8),
+                           None, None, self.off, self.chars, self.present, self.key_off,
+                           self.key_chars, None)
+        return self
+
     def compare_rows(self, a, b):
         return lib().dko_compare_rows(C.byref(self.schema), C.byref(self.table), a, b)
 

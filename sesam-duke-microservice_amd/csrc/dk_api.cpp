@@ -854,6 +854,8 @@ int dk_get_profile(const dk_ctx* c, dk_profile* out) {
       t.sym_matches += p.sym_matches;
       t.full_builds += p.full_builds;
       t.delta_builds += p.delta_builds;
+      t.replica_positions = std::max(t.replica_positions, p.replica_positions);
+      t.gram_row_bytes = std::max(t.gram_row_bytes, p.gram_row_bytes);
     }
     t.ms_total = c->prof.ms_total;  // the multi-device dk_match's own wall time
     *out = t;
@@ -2689,6 +2691,11 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     if (rc) return rc;
   }
   const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
+  c->prof.replica_positions = P.rstride;
+  c->prof.gram_row_bytes = 0;
+  for (int p = 0; p < P.nprops; ++p)
+    if (P.props[p].op == DK_CMP_QGRAM)
+      c->prof.gram_row_bytes = std::max(c->prof.gram_row_bytes, (uint64_t)P.props[p].rgrows * P.rstride * 8);
   bool sym = !lucene && contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
   if (!sym && !lucene && !allpairs && nq > 0) {
     t_gen.stop();

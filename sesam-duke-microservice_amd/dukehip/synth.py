@@ -159,6 +159,159 @@ def linkage_persons(n_group1, dup_frac=0.3, seed=SEED + 2):
     return out, group
 
 
+def _word_matrix(words):
+    """(uint8 [len(words), W] zero padded, lengths) of Latin-1 words."""
+    enc = [w.encode("latin-1") for w in words]
+    L = np.fromiter(map(len, enc), dtype=np.int64, count=len(enc))
+    M = np.zeros((len(enc), int(L.max())), np.uint8)
+    for i, b in enumerate(enc):
+        M[i, :len(b)] = np.frombuffer(b, np.uint8)
+    return M, L
+
+
+def _digits(v, width):
+    """[n, width] ASCII digits of v (zero padded on the left)."""
+    out = np.empty((len(v), width), np.uint8)
+    for j in range(width):
+        out[:, width - 1 - j] = 48 + (v // 10 ** j) % 10
+    return out
+
+
+def _pack(parts, n):
+    """Column of the concatenation, per record, of `parts`: each (uint8 [n, W], lengths[n])
+    or a bytes literal.  The parts side by side, then one row-major compress of the bytes
+    inside each part's length."""
+    Ms, Vs = [], []
+    lens = np.zeros(n, np.int64)
+    for p in parts:
+        if isinstance(p, bytes):
+            Ms.append(np.broadcast_to(np.frombuffer(p, np.uint8), (n, len(p))))
+            Vs.append(np.ones((n, len(p)), bool))
+            lens += len(p)
+        else:
+            M, L = p
+            Ms.append(M)
+            Vs.append(np.arange(M.shape[1])[None, :] < L[:, None])
+            lens += L
+    units = np.concatenate(Ms, axis=1)[np.concatenate(Vs, axis=1)]
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    return Column(offs, units)
+
+
+def linkage_columns(n_group1, dup_frac=0.3, seed=SEED + 5, copies=1, long_every=0):
+    """configs[2]-shaped linkage data at full size, built column-wise with numpy (no
+    per-record Python): group 1 = n_group1 persons, group 2 = n_group1 persons of which
+    dup_frac copy a group-1 record with, per field, p=0.3 of one a-z substitution (dob: p=0.1
+    of a day<->month swap).  NAME = "given surname", ADDRESS = "num street suffix district
+    city", BIRTHYEAR = dob's year, ZIP = 4 digits fixed per city; key columns K1 =
+    surname[0:3] + year, K2 = given[0:2] + dob[5:10] (keys_config2) and their integer codes
+    (k1 / k2: equal codes <=> equal key strings).
+    copies > 1: n_group1 / copies persons per group, the whole set repeated `copies` times
+    with the year moved by 100 per copy (K1 and BIRTHYEAR differ between copies, K2 does not:
+    cross-copy candidates) -- full-size replicas at memcpy speed.  long_every > 0: every such
+    record's ADDRESS gets two more words, cut at 65 units (sets of up to 64 bigrams: the
+    longest key-word rows a replica holds).  Records: copy 0's group 1, its group 2, copy 1's
+    group 1, ...  Returns (columns dict, key columns, group, k1, k2)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    given_v, sur_v = _word_matrix(_vocab(rng, 5000, 1, 3)), _word_matrix(_vocab(rng, 20000, 2, 3))
+    street_v, city_v = _word_matrix(_vocab(rng, 3000, 2, 3)), _word_matrix(_vocab(rng, 1000, 2, 3))
+    dist_v = _word_matrix(_vocab(rng, 2000, 2, 3))
+    suf_v = _word_matrix(_SUFFIX)
+    n1 = n_group1 // copies
+    n_dup = int(n1 * dup_frac)
+    n_src = 2 * n1 - n_dup                      # distinct persons drawn
+    n = 2 * n1
+    # group 1 rows, then the copies, then the new group-2 persons
+    src = np.concatenate([np.arange(n1), rng.integers(0, n1, n_dup), np.arange(n1, n_src)])
+    gi = _zipf_choice(rng, len(given_v[1]), 1.1, n_src)[src]
+    si = _zipf_choice(rng, len(sur_v[1]), 1.07, n_src)[src]
+    num = rng.integers(1, 1000, n_src)[src]
+    sti = rng.integers(0, len(street_v[1]), n_src)[src]
+    sfi = rng.integers(0, len(_SUFFIX), n_src)[src]
+    di = rng.integers(0, len(dist_v[1]), n_src)[src]
+    ci = rng.integers(0, len(city_v[1]), n_src)[src]
+    day = (np.datetime64("1930-01-01") + rng.integers(0, 29584, n_src).astype("timedelta64[D]"))[src]
+    year = day.astype("datetime64[Y]").astype(np.int64) + 1970
+    month = (day.astype("datetime64[M]") - day.astype("datetime64[Y]")).astype(np.int64) + 1
+    dom = (day - day.astype("datetime64[M]")).astype(np.int64) + 1
+    dup = np.zeros(n, bool)
+    dup[n1:n1 + n_dup] = True
+
+    def field(V, idx):
+        M, L = V[0][idx], V[1][idx].copy()
+        hit = np.nonzero(dup & (rng.random(n) < 0.3))[0]   # one substitution, a-z
+        at = (rng.random(len(hit)) * L[hit]).astype(np.int64)
+        M[hit, at] = rng.integers(ord("a"), ord("z") + 1, len(hit), dtype=np.uint8)
+        return M, L
+
+    given, sur = field(given_v, gi), field(sur_v, si)
+    street = field(street_v, sti)
+    swap = dup & (rng.random(n) < 0.1) & (dom <= 12)
+    mm = np.where(swap, dom, month)
+    dd = np.where(swap, month, dom)
+    nd = 1 + (num >= 10) + (num >= 100)
+    numd = _digits(num, 3)
+    numd = np.where((np.arange(3)[None, :] < nd[:, None]), np.take_along_axis(
+        numd, (np.arange(3)[None, :] + (3 - nd)[:, None]) % 3, axis=1), 0).astype(np.uint8)
+    dist = (dist_v[0][di], dist_v[1][di].copy())
+    if long_every:
+        lr = np.arange(0, n, long_every)
+        extra = _pack([b" ", (dist_v[0][(di[lr] + 7) % len(dist_v[1])], dist_v[1][(di[lr] + 7) % len(dist_v[1])]),
+                       b" ", (city_v[0][(ci[lr] + 3) % len(city_v[1])], city_v[1][(ci[lr] + 3) % len(city_v[1])]),
+                       b" ", (street_v[0][(sti[lr] + 5) % len(street_v[1])], street_v[1][(sti[lr] + 5) % len(street_v[1])])],
+                      len(lr))
+        w = int(np.diff(extra.offsets.astype(np.int64)).max())
+        X = np.zeros((len(lr), w), np.uint8)
+        eo = extra.offsets.astype(np.int64)
+        el = np.diff(eo)
+        for j in range(w):
+            sel = np.nonzero(j < el)[0]
+            X[sel, j] = extra.units[eo[sel] + j]
+        D = np.zeros((n, dist[0].shape[1] + w), np.uint8)
+        D[:, :dist[0].shape[1]] = dist[0]
+        for r, i in enumerate(lr):
+            D[i, dist[1][i]:dist[1][i] + el[r]] = X[r, :el[r]]
+        DL = dist[1].copy()
+        DL[lr] += el
+        dist = (D, DL)
+    addr = _pack([(numd, nd), b" ", street, b" ", (suf_v[0][sfi], suf_v[1][sfi]), b" ", dist, b" ",
+                  (city_v[0][ci], city_v[1][ci])], n)
+    if long_every:  # cut at 65 units
+        ao = addr.offsets.astype(np.int64)
+        al = np.minimum(np.diff(ao), 65)
+        keep = np.repeat(np.arange(n), al) if n else np.zeros(0, np.int64)
+        pos = np.arange(int(al.sum())) - np.repeat(np.cumsum(al) - al, al)
+        units = addr.units[ao[keep] + pos]
+        no = np.zeros(n + 1, np.int64)
+        np.cumsum(al, out=no[1:])
+        addr = Column(no, units)
+    cols = {"NAME": _pack([given, b" ", sur], n), "ADDRESS": addr,
+            "ZIP": _pack([(_digits(1000 + (ci * 2654435761) % 9000, 4), np.full(n, 4))], n)}
+    dob5 = np.concatenate([_digits(mm, 2), np.full((n, 1), ord("-"), np.uint8), _digits(dd, 2)], axis=1)
+    s3 = sur[0][:, :3]
+    g2 = given[0][:, :2]
+
+    def tile(c):  # the column `copies` times
+        o = c.offsets.astype(np.int64)
+        return Column(np.concatenate([o[:-1] + k * o[-1] for k in range(copies)] + [[copies * o[-1]]]),
+                      np.tile(c.units, copies))
+
+    ys = [year + 100 * k for k in range(copies)]
+    yd = np.concatenate([_digits(y, 4) for y in ys])
+    N = n * copies
+    out = {k: tile(c) for k, c in cols.items()}
+    out["BIRTHYEAR"] = _pack([(yd, np.full(N, 4))], N)
+    kcols = [_pack([(np.tile(s3, (copies, 1)), np.full(N, 3)), (yd, np.full(N, 4))], N),
+             tile(_pack([(g2, np.full(n, 2)), (dob5, np.full(n, 5))], n))]
+    s3i = s3.astype(np.int64)
+    g2i = g2.astype(np.int64)
+    k1 = np.concatenate([((s3i[:, 0] << 16 | s3i[:, 1] << 8 | s3i[:, 2]) << 16) | y for y in ys])
+    k2 = np.tile(((g2i[:, 0] << 8 | g2i[:, 1]) << 16) | (mm * 100 + dd), copies)
+    group = np.tile(np.concatenate([np.ones(n1, np.uint8), np.full(n - n1, 2, np.uint8)]), copies)
+    return out, kcols, group, k1, k2
+
+
 def hash_str(s):
     """Deterministic string hash (FNV-1a 32), stable across processes."""
     h = 0x811C9DC5
