@@ -317,7 +317,9 @@ int dk_reset_profile(dk_ctx* ctx);
 
 typedef struct dk_source_column {
   const char* name;   /* JSON attribute (<column name>), UTF-8 */
-  int32_t prop;       /* schema property it fills (<column property>); -1 = not scored */
+  int32_t prop;       /* schema property it fills (<column property>); -1 = not scored;
+                         nprops + j (j < 16): a property only key functions read (its value
+                         is kept for dk_key_part.prop = nprops + j, not packed) */
   int32_t cleaner;    /* DK_CLEAN_* (<column cleaner>) */
 } dk_source_column;
 

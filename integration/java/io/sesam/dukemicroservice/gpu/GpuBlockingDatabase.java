@@ -180,6 +180,16 @@ public class GpuBlockingDatabase implements Database {
             throw new IllegalArgumentException("too many HashMap order classes");
         List<List<Property>> byClass = new ArrayList<>();
         for (int cap : capList) {
+            // a bucket of 8 or more keys: a real record map would treeify it, or resize below
+            // capacity 64 (HashMap.treeifyBin) -- an order this model does not give (the
+            // Python wiring, config.java_hashmap_order, refuses the same pipelines)
+            int[] occ = new int[cap];
+            for (String k : recordKeys) {
+                int h = k.hashCode();
+                if (++occ[(h ^ (h >>> 16)) & (cap - 1)] >= 8)
+                    throw new IllegalArgumentException("8 record keys in one HashMap bucket at capacity "
+                                                       + cap + ": order not modelled");
+            }
             // a table of exactly `cap` buckets that never resizes (load factor 100), holding
             // every key a record can have: a record's own keys iterate in this relative order
             Map<String, Boolean> m = new HashMap<>(cap, 100f);
@@ -202,8 +212,16 @@ public class GpuBlockingDatabase implements Database {
         return new OrderClasses(props, caps, orders);
     }
 
-    /** Pipelines whose records hold at most 12 properties: the one order. */
+    /**
+     * Pipelines whose records hold at most 12 properties: the one order (a HashMap of
+     * capacity 16).  A pipeline whose records can hold more has a second order class at least
+     * (a record holding 12 or fewer keys still iterates at capacity 16): refused here -- use
+     * orderClasses and the OrderClasses constructor, which give every record its class.
+     */
     public static List<Property> comparisonOrder(Configuration config, List<String> recordKeys) {
+        if (recordKeys.size() > 12)
+            throw new IllegalArgumentException(recordKeys.size() + " record keys: several HashMap order "
+                                               + "classes, use orderClasses(config, keys, minKeys, maxKeys)");
         return orderClasses(config, recordKeys, recordKeys.size(), recordKeys.size()).props;
     }
 

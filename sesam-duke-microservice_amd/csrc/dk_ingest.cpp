@@ -37,6 +37,10 @@
 #include "dk_interner.h"
 #include "dukehip.h"
 
+// columns a key function reads but no property scores (dk_source_column.prop >= nprops)
+constexpr int kMaxKeyOnly = 16;
+
+
 extern "C" int dk_fail_ingest(int code, const char* msg);  // dk_api.cpp: sets dk_last_error
 
 namespace {
@@ -955,8 +959,9 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
   out.hash.reserve(n);
   std::vector<Val> got(V.names.size()), side;
   std::vector<char> has(V.names.size());
-  std::vector<std::u16string> pv(np);
-  std::vector<char> pset(np);
+  // the scored properties, then the key-only ones (columns with prop >= nprops)
+  std::vector<std::u16string> pv(np + kMaxKeyOnly);
+  std::vector<char> pset(np + kMaxKeyOnly);
   std::u16string s, key, mname, eid, rid;
   KeyScratch ks;
   uint64_t r = out.e0;
@@ -1045,7 +1050,7 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
         const dk_key_function& kf = src->keys[k];
         for (int i = 0; i < kf.nparts; ++i) {
           const dk_key_part& kp = kf.parts[i];
-          if (kp.prop < 0 || kp.prop >= np) fail(DK_E_INVALID, "key part property out of range");
+          if (kp.prop < 0 || kp.prop >= np + kMaxKeyOnly) fail(DK_E_INVALID, "key part property out of range");
           key_part(pset[kp.prop] ? &pv[kp.prop] : nullptr, kp, key, ks);
         }
         out.cols[np + k].add(key);
@@ -1204,7 +1209,7 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
     return dk_fail_ingest(DK_E_INVALID, "bad dk_source");
   for (int c = 0; c < src->ncolumns; ++c) {
     const dk_source_column& sc = src->columns[c];
-    if (!sc.name || sc.prop < -1 || sc.prop >= src->nprops || sc.cleaner < DK_CLEAN_NONE ||
+    if (!sc.name || sc.prop < -1 || sc.prop >= src->nprops + kMaxKeyOnly || sc.cleaner < DK_CLEAN_NONE ||
         sc.cleaner > DK_CLEAN_CAPITAL)
       return dk_fail_ingest(DK_E_INVALID, "bad dk_source_column");
   }

@@ -433,8 +433,16 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+#ifndef DK_LONG_NOINLINE
+#define DK_LONG_NOINLINE 1  // 0: long_dp inlined into the kernel (no call frame)
+#endif
+#if DK_LONG_NOINLINE
+#define DK_LONG_ATTR __attribute__((noinline))
+#else
+#define DK_LONG_ATTR __attribute__((always_inline))
+#endif
 template <int G, int R, bool WL, typename CT>
-__device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1p, int n1, int nneed) {
+__device__ DK_LONG_ATTR void long_dp(uint64_t wstride, const CT* s1p, int n1, int nneed) {
   uint64_t* lds = g_wave_tables[threadIdx.x >> 6];
   using T = typename std::conditional<WL, double, int>::type;
   constexpr int UPW = 4 / (int)sizeof(CT);

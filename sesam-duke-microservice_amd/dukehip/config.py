@@ -316,15 +316,16 @@ def java_hashmap_order(keys, cap=None):
     """Iteration order of a java.util.HashMap<String,?> filled with `keys` in this order
     (capacity `cap`, default: the one those puts give; buckets by (h ^ h>>>16) & (cap-1),
     insertion order inside a bucket -- a resize splits a bucket keeping its order).  A
-    bucket of 8 or more keys at capacity >= 64 would be a tree bin: refused."""
+    bucket of 8 or more keys is refused: a real map would treeify it at capacity >= 64 and
+    resize below that (HashMap.treeifyBin), an order this model does not give."""
     cap = hashmap_capacity(len(keys)) if cap is None else cap
     buckets = {}
     for k in keys:
         h = java_string_hash(k)
         idx = (h ^ (h >> 16)) & (cap - 1)
         buckets.setdefault(idx, []).append(k)
-    if cap >= 64 and any(len(b) >= 8 for b in buckets.values()):
-        raise UnsupportedComparator("HashMap tree bin (8 keys in one bucket): order not modelled")
+    if any(len(b) >= 8 for b in buckets.values()):
+        raise UnsupportedComparator("8 keys in one HashMap bucket (tree bin or resize): order not modelled")
     return [k for i in sorted(buckets) for k in buckets[i]]
 
 

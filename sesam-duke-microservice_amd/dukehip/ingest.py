@@ -190,12 +190,23 @@ class NativeSource:
     def __init__(self, source: DataSource, props, key_functions=()):
         self.lib = _lib()
         names = list(props)
+        # properties only key functions read (a column's property no comparator scores):
+        # indices nprops + j, kept for the key parts, not packed
+        colprops = {c.property for c in source.columns}
+        keyonly = []
+        for kf in key_functions:
+            for prop, *_ in getattr(kf, "parts", ()):
+                if prop not in names and prop in colprops and prop not in keyonly:
+                    keyonly.append(prop)
+        if len(keyonly) > 16:
+            raise UnsupportedComparator("more than 16 key-only properties")
+        allnames = names + keyonly
         cols = []
         for c in source.columns:
             if c.cleaner not in DK_CLEAN:
                 raise UnsupportedComparator(f"cleaner {c.cleaner} has no native implementation")
             cols.append(dk_source_column(c.name.encode("utf-8"),
-                                         names.index(c.property) if c.property in names else -1,
+                                         allnames.index(c.property) if c.property in allnames else -1,
                                          DK_CLEAN[c.cleaner]))
         self._cols = (dk_source_column * max(1, len(cols)))(*cols)
         self._parts, kfs = [], []
@@ -204,10 +215,10 @@ class NativeSource:
                 raise UnsupportedComparator(f"key function {type(kf).__name__} has no native form")
             parts = []
             for prop, token, start, end in kf.parts:
-                if prop not in names:
-                    raise UnsupportedComparator(f"key part on {prop!r}: not a scored property")
+                if prop not in allnames:
+                    raise UnsupportedComparator(f"key part on {prop!r}: no column fills it")
                 conv = lambda v: NONE_I32 if v is None else int(v)
-                parts.append(dk_key_part(names.index(prop), conv(token), conv(start), conv(end)))
+                parts.append(dk_key_part(allnames.index(prop), conv(token), conv(start), conv(end)))
             arr = (dk_key_part * max(1, len(parts)))(*parts)
             self._parts.append(arr)
             kfs.append(dk_key_function(len(parts), arr))

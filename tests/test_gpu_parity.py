@@ -608,6 +608,70 @@ def test_order_classes_wide_schema(mode):
     assert not (np.array_equal(flat.candidate, res.candidate) and np.array_equal(flat.prob, res.prob))
 
 
+@pytest.mark.parametrize("variant", ["gq", "grouped", "grouped_row1", "grouped_row2", "tile"])
+def test_order_classes_grouped(variant, monkeypatch):
+    """the order classes through the grouped kernels -- two bigram QGram and three
+    Numeric properties (k_score_gq's roles; k_score_grouped with DK_GQ=0, its head / tail
+    and per-row resources with DK_GROUPED_ROW=1 / 2; k_tile with DK_TILE=1) in records of
+    more than 12 keys (the unscored columns count), each row in its HashMap capacity's class,
+    bit-exact against the oracle fed the same classes; the two classes' orders differ."""
+    from dukehip import config as cfgmod
+    env = {"grouped": [("DK_GQ", "0")], "grouped_row1": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "1")],
+           "grouped_row2": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "2")],
+           "tile": [("DK_TILE", "1")]}.get(variant, [])
+    for kv in env:
+        monkeypatch.setenv(*kv)
+    rng = random.Random(23)
+    n = 1200
+    props = [{"comparator": QG, "low": 0.15, "high": 0.92, "q": 2, "formula": A.QGRAM_DICE},
+             {"comparator": QG, "low": 0.1, "high": 0.85, "q": 2, "formula": A.QGRAM_JACCARD},
+             {"comparator": NUM, "low": 0.3, "high": 0.7, "min_ratio": 0.8},
+             {"comparator": NUM, "low": 0.35, "high": 0.65, "min_ratio": 0.5},
+             {"comparator": NUM, "low": 0.4, "high": 0.75, "min_ratio": 0.9}]
+    names = ["NAME", "ADDRESS", "AGE", "ZIP", "SCORE"]
+    unscored = [f"COL{i}" for i in range(8)]   # columns no property scores: record keys only
+    extra = [cfgmod.ID_PROPERTY, cfgmod.ORIGINAL_ENTITY_ID_PROPERTY_NAME, cfgmod.DATASET_ID_PROPERTY_NAME]
+    allkeys = names + unscored + extra + [cfgmod.DELETED_PROPERTY_NAME]
+    orders = []
+    for cap in (16, 32):
+        o = cfgmod.java_hashmap_order(allkeys, cap)
+        orders.append([names.index(k) for k in o if k in names])
+    assert orders[0] != orders[1]
+    pool = rand_strings(rng, 60, "abcdefgh", 3, 12)
+    vals = []
+    for p in props:
+        col = []
+        for _ in range(n):
+            if rng.random() < 0.2:
+                col.append(None)
+            elif p["comparator"] == NUM:
+                col.append(str(rng.randint(20, 40)))
+            else:
+                col.append(rng.choice(pool))
+        vals.append(col)
+    # a record's keys: its values, 0-8 unscored columns, the synthetic ones
+    nun = np.array([rng.randint(0, 8) for _ in range(n)])
+    nvals = np.array([sum(v[r] is not None for v in vals) for r in range(n)])
+    oclass = (nvals + nun + len(extra) > 12).astype(np.uint8)
+    assert 0 < oclass.sum() < n
+    keys = [[rng.choice("pqrs") for _ in range(n)]]
+    group = [1 + (r % 2) for r in range(n)]
+    ident = np.arange(n, dtype=np.uint64)
+    s = schema_of(props, 0.8, 0.5, "linkage", len(keys))
+    flat = (C.c_int * (2 * len(props)))(*[x for o in orders for x in o])
+    s.norders, s.orders, s._orders = 2, flat, flat
+    eng = dh.GpuEngine(s)
+    eng.upsert(n, ident, [dh.Column.from_strings(v) for v in vals], group=np.asarray(group, np.uint8),
+               key_columns=[dh.Column.from_strings(k) for k in keys], order_class=oclass)
+    res = eng.match(np.arange(n, dtype=np.uint32))
+    eng.close()
+    ot = O.OracleTable(props, vals, keys=keys, ident=ident, group=group, threshold=0.8, maybe=0.5,
+                       mode="linkage", orders=orders, oclass=oclass)
+    ref = ot.match(np.arange(n, dtype=np.uint32))
+    assert len(ref["query"]) > 50
+    assert_same(res, ref)
+
+
 def assert_close(res, ref, thresholds, rel=1e-12, edge=1e-9):
     """The north star's floating-point bar for comparators on sin / cos / atan2: candidate
     sets equal, probabilities within 1e-12 relative, decisions equal except for pairs within

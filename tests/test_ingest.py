@@ -103,6 +103,30 @@ def test_pack_json_matches_python_path(seed):
         assert c.width == ref_col.units.itemsize
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_pack_json_key_only_property(seed):
+    """A key function may read a column no property scores ("extra" -> UNSCORED): its value
+    is kept for the key parts (dk_source_column.prop = nprops + j) and not packed (the
+    configs[2] json leg's DOB)."""
+    rng = random.Random(100 + seed)
+    src = source()
+    kfs = KEYS + [dh.PartsKey(("UNSCORED", None, 0, 3), ("AREA", None, None, None)),
+                  dh.PartsKey(("NAME", 0, 0, 2), ("UNSCORED", None, 1, 4))]
+    ns = I.NativeSource(src, PROPS, kfs)
+    ents = rand_entities(rng, 300)
+    body = json.dumps(ents)
+    recs = dh.records_from_entities(dh.parse_entities(body)[0], src)
+    pk = ns.pack(body, I.Interner())
+    assert pk.n == len(recs) and ns.nprops == len(PROPS)
+    for p in range(len(PROPS)):
+        assert pk.values(p) == [r.get_value(PROPS[p]) for r in recs]
+    for k, kf in enumerate(kfs):
+        assert pk.keys(k) == [kf.make_key(r) for r in recs]
+    assert any(r.get_value("UNSCORED") for r in recs)
+    with pytest.raises(I.UnsupportedComparator):   # no column fills it
+        I.NativeSource(src, PROPS, [dh.PartsKey(("NOWHERE", None, 0, 2))])
+
+
 def C_u32(p):
     import ctypes as C
     return C.cast(p, C.POINTER(C.c_uint32))
