@@ -37,6 +37,7 @@ public class GpuProcessor extends Processor {
     private final List<MatchListener> listeners = new ArrayList<>();
     private final FallbackDatabase fallback;
     private GpuLinkDatabase links;
+    private GpuJdbcLinkDatabase jdbcLinks;   // the opt-in H2 bulk writer (DUKEHIP_H2_BULK)
     private Processor stock;   // non-null once the pipeline has fallen back
 
     public GpuProcessor(Configuration config, GpuBlockingDatabase db, FallbackDatabase fallback) {
@@ -50,6 +51,17 @@ public class GpuProcessor extends Processor {
      *  disabled: App.java:1131-1132 disables the link writes of httptransform batches). */
     public void setLinkDatabase(GpuLinkDatabase links) {
         this.links = links;
+    }
+
+    /** The H2 link database with bulk writes (opt-in, GpuJdbcLinkDatabase): the same
+     *  listener window, the batch's links written by one MERGE batch per deduplicate. */
+    public void setJdbcLinkDatabase(GpuJdbcLinkDatabase links) {
+        this.jdbcLinks = links;
+    }
+
+    private void window(boolean open) {
+        if (links != null) links.setListenerWindow(open);
+        if (jdbcLinks != null) jdbcLinks.setListenerWindow(open);
     }
 
     @Override
@@ -81,13 +93,13 @@ public class GpuProcessor extends Processor {
         }
         int[] rows = new int[batch.size()];
         System.arraycopy(allRows, pending.size(), rows, 0, rows.length);
-        if (links != null) links.setListenerWindow(true);
+        window(true);
         try {
             for (MatchListener l : listeners) l.batchReady(batch.size());
             matchAndReplay(rows, batch);
             for (MatchListener l : listeners) l.batchDone();
         } finally {
-            if (links != null) links.setListenerWindow(false);
+            window(false);
         }
         db.releaseDeferred();
         if (db.indexingIsDisabled()) db.dropTransient();   // the batch never entered the index
@@ -110,13 +122,13 @@ public class GpuProcessor extends Processor {
             if (e.code() != DukeHip.E_UNSUPPORTED) throw e;
             return false;
         }
-        if (links != null) links.setListenerWindow(true);
+        window(true);
         try {
             for (MatchListener l : listeners) l.batchReady(rows.length);
             matchAndReplay(rows, null);
             for (MatchListener l : listeners) l.batchDone();
         } finally {
-            if (links != null) links.setListenerWindow(false);
+            window(false);
         }
         db.releaseDeferred();
         if (db.indexingIsDisabled()) db.dropTransient();
@@ -152,6 +164,12 @@ public class GpuProcessor extends Processor {
                 for (int e = 0; e < cand.length; e++) cid[e] = db.identAtRow(cand[e]);
                 links.applyBatch(qid, first, cid, prob, kind, System.currentTimeMillis());
             }
+            if (jdbcLinks != null && !db.indexingIsDisabled()) {
+                String[] qs = new String[rows.length], cs = new String[cand.length];
+                for (int i = 0; i < rows.length; i++) qs[i] = DukeHip.internerString(db.ids(), db.identAtRow(rows[i]));
+                for (int e = 0; e < cand.length; e++) cs[e] = DukeHip.internerString(db.ids(), db.identAtRow(cand[e]));
+                jdbcLinks.applyBatch(qs, first, cs, prob, kind, System.currentTimeMillis());
+            }
         } finally {
             DukeHip.freeResult(res);
         }
@@ -166,6 +184,7 @@ public class GpuProcessor extends Processor {
         stockDb.commit();
         config.setDatabase(stockDb);
         if (links != null) links.handOver();   // the listener writes links per callback again
+        jdbcLinks = null;                      // (the H2 table: per callback, as in the reference)
         stock = new Processor(config, false);
         for (MatchListener l : listeners) stock.addMatchListener(l);
         return stock;

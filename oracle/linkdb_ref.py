@@ -4,6 +4,10 @@ dk_linkdb_apply / dukehip.links.LinkDatabase; never imported by the product).
 * ``SinceAwareLinkDB``   <- SinceAwareInMemoryLinkDatabase.java:12-41 (assertLink's identical-
   link skip within 1e-6, getChangesSince) over [Duke 1.2, recalled] InMemoryLinkDatabase (one
   link per ID pair, assertLink replaces it).
+* ``SqlLinkDB``          <- [Duke 1.2, recalled] JDBCLinkDatabase over a SQL table (the H2
+  link-database-type, App.java:567-570, 597-602): getAllLinksFor = one SELECT, assertLink =
+  one update-or-insert of the (id1, id2) row -- the per-callback stream the bulk writer
+  (dukehip.jdbc_links) is checked against; table layout recalled (unpinned).
 * ``LinkDBListener``     <- [Duke 1.2, recalled] LinkDatabaseMatchListener as
   BaseLinkDatabaseMatchListener.java:53-109 drives it: per record, its matches /
   matchesPerhaps collected; when the next record starts (or noMatchFor / batchDone) the
@@ -71,6 +75,34 @@ class SinceAwareLinkDB:
     def changes_since(self, since):                 # :32-40
         out = [l for l in self.links.values() if l.timestamp > since]
         return sorted(out, key=lambda l: (l.timestamp, self.order[l.key()]))
+
+
+class SqlLinkDB:
+    """One SQL statement per call, on a DB-API (qmark) connection; the table layout of
+    dukehip.jdbc_links (created if missing)."""
+
+    def __init__(self, conn, create, table="links"):
+        self.conn, self.table = conn, table
+        conn.execute(create)
+        self.statements = 0
+
+    def all_links_for(self, rid):
+        self.statements += 1
+        rows = self.conn.execute(f"select id1, id2, kind, status, perhaps, timestamp from {self.table} "
+                                 "where id1 = ? or id2 = ?", (rid, rid)).fetchall()
+        return [Link(a, b, s, k, p, t) for a, b, k, s, p, t in rows]
+
+    def assert_link(self, link):
+        self.statements += 1
+        self.conn.execute(f"insert into {self.table} (id1, id2, kind, status, perhaps, timestamp) "
+                          "values (?, ?, ?, ?, ?, ?) on conflict (id1, id2) do update set "
+                          "kind = excluded.kind, status = excluded.status, perhaps = excluded.perhaps, "
+                          "timestamp = excluded.timestamp",
+                          (link.id1, link.id2, link.kind, link.status, link.confidence, link.timestamp))
+        return True
+
+    def commit(self):   # JDBCLinkDatabase.commit at batchDone
+        self.conn.commit()
 
 
 class LinkDBListener:
