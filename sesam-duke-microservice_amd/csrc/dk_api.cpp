@@ -559,6 +559,8 @@ struct dk_ctx {
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
   DevBuf ocounts, oqoff, owq, obase, ores, mcounts, mqoff, mbase, mres, bidx, bval;
+  DevBuf lsim;             // the long-value DP pre-pass's similarities (k_long_pre)
+  DevBuf symkey, symval;   // symmetric owner launches: block sort keys / bucket-order permutation
   PinnedBuf h_bounds;
   DevBuf counters;
   struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx; };
@@ -1696,6 +1698,18 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
       P.order[o] |= (uint64_t)(c->orders.empty() ? k : c->orders[(size_t)o * P.nprops + k]) << (4 * k);
   }
   P.oclass = c->oclass.as<uint8_t>();
+  // the long-value DP's properties (k_long_pre): WeightedLevenshtein, and Levenshtein (its
+  // queries over 64 units); the buffer is set per launch (long_sim_buffer)
+  P.lsim = nullptr;
+  P.lstride = 0;
+  P.long_word = ~0ull;
+  for (int p = 0, j = 0; p < P.nprops; ++p) {
+    const int op = c->P[p].cfg.comparator;
+    if (op == DK_CMP_WEIGHTED_LEVENSHTEIN || op == DK_CMP_LEVENSHTEIN) {
+      P.long_word &= ~(15ull << (4 * p));
+      P.long_word |= (uint64_t)j++ << (4 * p);
+    }
+  }
   for (const auto& S : c->P) {
     const int op = S.cfg.comparator;
     if (op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER || op == DK_CMP_WEIGHTED_LEVENSHTEIN) P.has_dp = 1;
@@ -1743,6 +1757,20 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
     D.gseed = S.gseed.as<uint16_t>();
   }
   return P;
+}
+
+// The long-value DP pre-pass's similarity buffer for launches of up to `maxslots` slots
+// (k_long_pre -> k_score_long): 8 B per slot and property on that DP.  Returns false on an
+// allocation failure.
+static bool long_sim_buffer(dk_ctx* c, ScoreParams& P, uint64_t maxslots) {
+  if (P.long_rows <= 0 || P.has_geo || !long_dp_split()) return true;
+  int nlong = 0;
+  for (int p = 0; p < P.nprops; ++p) nlong += ((P.long_word >> (4 * p)) & 15u) != 15u;
+  const uint64_t stride = std::max<uint64_t>(kScoreBlock, (maxslots + kScoreBlock - 1) / kScoreBlock * kScoreBlock);
+  if (c->lsim.reserve((uint64_t)std::max(nlong, 1) * stride * 8, 0, c->stream) != hipSuccess) return false;
+  P.lsim = c->lsim.as<double>();
+  P.lstride = stride;
+  return true;
 }
 
 // Candidate replica: every property's candidate-side values in replica order, units
@@ -3046,6 +3074,12 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     return DK_OK;
   };
   const size_t nchunks = bounds.size() - 1;
+  ScoreParams PL = P;  // + the long-value DP's buffer (k_long_pre)
+  {
+    uint64_t maxc = 0;
+    for (size_t ci = 0; ci < nchunks; ++ci) maxc = std::max(maxc, bounds[ci + 1] - bounds[ci]);
+    if (!sym && !long_sim_buffer(c, PL, maxc)) return fail(DK_E_DEVICE, "long-value DP buffer");
+  }
   // SYM: chunk ci's owner scoring runs on the ctx stream and its emission pass, scan and
   // count read-back on the emission stream, so emission (latency bound) overlaps the next
   // chunk's scoring (VALU bound).  Emission of chunk ci reads owner / mirror results of
@@ -3059,9 +3093,26 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     if (sym) {
       // phase 1: the chunk's owner slots, both directions of every owned pair -> ores
       const uint64_t o0 = obounds[ci], o1 = obounds[ci + 1];
+      // DK_SYM_SORT=1: the launch's blocks in bucket order over the XCDs (measured: the same
+      // kernel time, 26.45 vs 26.50 ms per configs[1] step -- VALU-bound, not L2 -- plus the
+      // sort), else launch order
+      PairSource osrc = src;
+      static const bool sym_sort = getenv("DK_SYM_SORT") && getenv("DK_SYM_SORT")[0] == '1';
+      const uint64_t onb = (o1 - o0 + kScoreBlock - 1) / kScoreBlock;
+      if (sym_sort && onb > 1) {
+        HIPCHK(c->symkey.reserve(2 * onb * 8 + 16, 0, s));
+        HIPCHK(c->symval.reserve(2 * onb * 4 + 16, 0, s));
+        uint64_t* k0 = c->symkey.as<uint64_t>();
+        uint32_t* v0 = c->symval.as<uint32_t>();
+        HIPCHK(launch_sym_block_keys(src, o0, onb, k0, v0, s));
+        HIPCHK(with_tmp(c, [&](void* t, size_t& bytes) {
+          return sort_pairs_u64_u32(t, bytes, k0, k0 + onb, v0, v0 + onb, onb, s);
+        }));
+        osrc.bperm = v0 + onb;
+      }
       {
         Timer t_score(c, &c->prof.ms_score, s);
-        HIPCHK(launch_score(P, src, o0, o1 - o0, so, s));
+        HIPCHK(launch_score(P, osrc, o0, o1 - o0, so, s));
         t_score.stop();
       }
       HIPCHK(launch_reduce_blocks(so, (o1 - o0 + kScoreBlock - 1) / kScoreBlock, s));
@@ -3080,7 +3131,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
           HIPCHK(launch_score_gq(P, src, s0, s1 - s0, perm, c->gqargs.as<GQArgs>() + b, gq_nq, gq_nn, gqa.defer, st[b], s));
         else if (grouped)
           HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), gmode, st[b], s));
-        else HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
+        else HIPCHK(launch_score(PL, src, s0, s1 - s0, st[b], s));
         t_score.stop();
       }
       HIPCHK(launch_reduce_blocks(st[b], nblk, s));
@@ -3373,6 +3424,7 @@ static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double
   src.m = 1;
   src.mpad = 64;
   src.same_ok = 1;  // Processor.compare scores a record against itself too
+  if (!long_sim_buffer(c, P, 1)) return fail(DK_E_DEVICE, "long-value DP buffer");
   HIPCHK(launch_score(P, src, 0, 1, st, s));
   uint32_t n = 0;
   double p = NAN;

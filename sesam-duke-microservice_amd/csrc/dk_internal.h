@@ -133,6 +133,12 @@ struct ScoreParams {
   int32_t norders;
   uint64_t order[kMaxOrders];
   const uint8_t* oclass;  // per row: its order class (norders > 1)
+  // the long-value DP pre-pass (k_long_pre -> k_score_long): property p's similarity of the
+  // launch's slot i at lsim[j * lstride + i], j = bits [4p, 4p + 4) of long_word (15: p is
+  // not on the long-value DP)
+  double* lsim;
+  uint64_t lstride;
+  uint64_t long_word;
   DevProp props[kMaxProps];
 };
 
@@ -179,6 +185,10 @@ struct PairSource {
   double* mres;
   const uint64_t* mbase;
   uint32_t r0, r1;
+  // the launch's blocks in bucket order (null: launch order): launch block b runs block
+  // bperm[xcd_slot(b)] -- consecutive sorted blocks on one XCD, so a bucket's replica rows
+  // are re-read from that XCD's L2 (the symmetric schedule's owner launches)
+  const uint32_t* bperm;
 };
 
 constexpr uint32_t kNoPos = 0xFFFFFFFFu;
@@ -559,6 +569,9 @@ hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, c
 hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
                              hipStream_t s);
 hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s);
+bool long_dp_split();  // dk_kernels.hip built with DK_LONG_SPLIT (k_long_pre + P.lsim)
+hipError_t launch_sym_block_keys(const PairSource& src, uint64_t slot0, uint64_t nblocks, uint64_t* key,
+                                 uint32_t* val, hipStream_t s);
 hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nblocks,
                           uint64_t base, const MatchList& out, hipStream_t s);
 hipError_t launch_first(const uint32_t* qidx, uint64_t n, uint64_t nq, uint64_t* first,

@@ -29,10 +29,16 @@
 #define DK_WAVES_NODP 8   // k_score_nodp waves per SIMD (no DP comparator: latency bound)
 #endif
 #ifndef DK_WAVES_LONG8
-#define DK_WAVES_LONG8 5  // k_score_long waves per SIMD, <= 8 DP rows per lane
+#define DK_WAVES_LONG8 5  // k_score_long waves per SIMD (the long DP is in k_long_pre)
 #endif
 #ifndef DK_WAVES_LONG16
-#define DK_WAVES_LONG16 5  // k_score_long waves per SIMD, 16 DP rows per lane (A/B: 4/3 -> 5/5 is +13% on longtext despite more spills)
+#define DK_WAVES_LONG16 5  // k_score_long_geo waves per SIMD (the DP in the fused kernel)
+#endif
+#ifndef DK_WAVES_LONGPRE
+#define DK_WAVES_LONGPRE 4  // k_long_pre waves per SIMD, DP variants of <= 4 rows per lane
+#endif
+#ifndef DK_WAVES_LONGPRE_HI
+#define DK_WAVES_LONGPRE_HI 4  // the same, 5-8 rows per lane (f64 columns of 6-9 values)
 #endif
 
 namespace dk {
@@ -433,16 +439,10 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-#ifndef DK_LONG_NOINLINE
-#define DK_LONG_NOINLINE 1  // 0: long_dp inlined into the kernel (no call frame)
-#endif
-#if DK_LONG_NOINLINE
-#define DK_LONG_ATTR __attribute__((noinline))
-#else
-#define DK_LONG_ATTR __attribute__((always_inline))
-#endif
+// long_dp_body is inlined into the pre-pass kernel k_long_pre (its own registers, no call
+// frame); long_dp, its out-of-line form, serves the fused geo variant
 template <int G, int R, bool WL, typename CT>
-__device__ DK_LONG_ATTR void long_dp(uint64_t wstride, const CT* s1p, int n1, int nneed) {
+__device__ __forceinline__ void long_dp_body(uint64_t wstride, const CT* s1p, int n1, int nneed) {
   uint64_t* lds = g_wave_tables[threadIdx.x >> 6];
   using T = typename std::conditional<WL, double, int>::type;
   constexpr int UPW = 4 / (int)sizeof(CT);
@@ -611,9 +611,26 @@ __device__ DK_LONG_ATTR void long_dp(uint64_t wstride, const CT* s1p, int n1, in
     });
 }
 
-// Similarity of every lane with `need` set (the others keep `sim`) through long_dp.
-// Wave-uniform call: all 64 lanes enter.
-template <int LR, bool WL, typename CT>
+template <int G, int R, bool WL, typename CT>
+__device__ __attribute__((noinline)) void long_dp(uint64_t wstride, const CT* s1p, int n1, int nneed) {
+  long_dp_body<G, R, WL, CT>(wstride, s1p, n1, nneed);
+}
+
+// The DP variant of a query of n1 units in a kernel of up to LR rows per lane (0..11):
+// 16-lane groups (4 streams, DPP row_shr) up to 128 rows, 32-lane groups (2 streams,
+// wave_shr) beyond; LR caps the variants a kernel carries.
+template <int LR>
+__host__ __device__ constexpr int long_variant(int n1) {
+  return n1 <= 16 ? 0 : n1 <= 32 ? 1 : n1 <= 48 ? 2 : (n1 <= 64 || LR <= 4) ? 3 : n1 <= 80 ? 4
+       : n1 <= 96 ? 5 : n1 <= 112 ? 6 : (n1 <= 128 || LR <= 8) ? 7 : n1 <= 160 ? 8 : n1 <= 192 ? 9
+       : n1 <= 224 ? 10 : 11;
+}
+template <int LR>
+__host__ __device__ constexpr int long_nvariants() { return LR <= 4 ? 4 : LR <= 8 ? 8 : 12; }
+
+// Similarity of every lane with `need` set (the others keep `sim`) through long_dp (INL:
+// the inlined body; VI >= 0: only DP variant VI).  Wave-uniform call: all 64 lanes enter.
+template <int LR, bool WL, typename CT, bool INL = false, int VI = -1>
 __device__ __forceinline__ double long_sims(const DevProp& D, uint64_t rstride, uint64_t* lds, uint32_t q,
                                             int n1, uint32_t g, uint32_t crow, int lc, bool need,
                                             double sim) {
@@ -648,18 +665,28 @@ __device__ __forceinline__ double long_sims(const DevProp& D, uint64_t rstride, 
   // DPP row_shr) up to 128 rows, 32-lane groups (2 streams, wave_shr) beyond; R = rows /
   // lanes rounded up, so most of a group's lanes hold rows, and R <= 8 keeps the column,
   // weights and units in VGPRs.  LR caps the variants a kernel carries.
-  if (n1 <= 16) long_dp<16, 1, WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 32) long_dp<16, 2, WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 48) long_dp<16, 3, WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 64 || LR <= 4) long_dp<16, 4, WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 80) long_dp<16, 5, WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 96) long_dp<16, 6, WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 112) long_dp<16, 7, WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 128 || LR <= 8) long_dp<16, 8, WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 160) long_dp<32, (LR < 16 ? 4 : 5), WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 192) long_dp<32, (LR < 16 ? 4 : 6), WL, CT>(wstride, s1p, n1, nneed);
-  else if (n1 <= 224) long_dp<32, (LR < 16 ? 4 : 7), WL, CT>(wstride, s1p, n1, nneed);
-  else long_dp<32, (LR < 16 ? 4 : 8), WL, CT>(wstride, s1p, n1, nneed);
+  // VI >= 0 (the pre-pass kernels): only variant VI is compiled in
+  const int vi = long_variant<LR>(n1);
+#define DK_LDP(V_, G_, R_)                                                                  \
+  if constexpr (VI < 0 || VI == (V_)) {                                                     \
+    if (vi == (V_)) {                                                                       \
+      if constexpr (INL) long_dp_body<G_, R_, WL, CT>(wstride, s1p, n1, nneed);             \
+      else long_dp<G_, R_, WL, CT>(wstride, s1p, n1, nneed);                                \
+    }                                                                                       \
+  }
+  DK_LDP(0, 16, 1)
+  DK_LDP(1, 16, 2)
+  DK_LDP(2, 16, 3)
+  DK_LDP(3, 16, 4)
+  DK_LDP(4, 16, 5)
+  DK_LDP(5, 16, 6)
+  DK_LDP(6, 16, 7)
+  DK_LDP(7, 16, 8)
+  DK_LDP(8, 32, (LR < 16 ? 4 : 5))
+  DK_LDP(9, 32, (LR < 16 ? 4 : 6))
+  DK_LDP(10, 32, (LR < 16 ? 4 : 7))
+  DK_LDP(11, 32, (LR < 16 ? 4 : 8))
+#undef DK_LDP
   wave_lds_sync();
   if (need) {
     const uint64_t bits = lds[kLongRes + lane];
@@ -966,10 +993,13 @@ __device__ __forceinline__ int qgram_common_perfect(uint32_t* tab, const uint64_
 // ------------------------------------------------------------------------------------
 // SYM: `rev` receives Comparator.compare(candidate, query) where it can differ from
 // compare(query, candidate) (JaroWinkler on equal lengths); it is left alone otherwise.
-template <int RMAX, int LR, typename CT, bool SYM, bool DP, bool GR>
+// LB: the long-value DP's similarities computed here (0), inlined for the pre-pass (1), or
+// taken from it (2: lbuf)
+template <int RMAX, int LR, typename CT, bool SYM, bool DP, bool GR, int LB = 0, int VI = -1>
 __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
-                                             int lc, bool cmp, double& rev, uint32_t qch) {
+                                             int lc, bool cmp, double& rev, uint32_t qch,
+                                             double lbuf = 0.0) {
   const CT* base = reinterpret_cast<const CT*>(D.units);
   const Str<CT> s1{reinterpret_cast<const uint32_t*>(base + D.off[q]), 1, 1 << 30};
   const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + g, rstride,
@@ -979,14 +1009,22 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
   switch (D.op) {
     case DK_CMP_WEIGHTED_LEVENSHTEIN:
       if (DP && LR > 0) {  // the host only schedules WeightedLevenshtein on LR > 0 variants
+        if (LB == 2) {
+          sim = lbuf;
+          break;
+        }
         const bool same = cmp && str_equal(s1, lq, s2, lc);
         sim = same ? 1.0 : 0.0;
-        sim = long_sims<LR, true, CT>(D, rstride, peq, q, lq, g, crow, lc, cmp && !same, sim);
+        sim = long_sims<LR, true, CT, LB == 1, VI>(D, rstride, peq, q, lq, g, crow, lc, cmp && !same, sim);
       }
       break;
     case DK_CMP_LEVENSHTEIN:
       if (!DP) break;  // the DP-free variant is only launched without DP comparators
       if (LR > 0 && lq > kMaxUnits) {  // query over 64 units: long-value DP
+        if (LB == 2) {
+          sim = lbuf;
+          break;
+        }
         bool need = false;
         if (cmp) {
           const int len = min(lq, lc), maxlen = max(lq, lc);
@@ -994,7 +1032,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
           else if (len == maxlen && str_equal(s1, lq, s2, lc)) sim = 1.0;
           else need = true;
         }
-        sim = long_sims<LR, false, CT>(D, rstride, peq, q, lq, g, crow, lc, need, sim);
+        sim = long_sims<LR, false, CT, LB == 1, VI>(D, rstride, peq, q, lq, g, crow, lc, need, sim);
         break;
       }
       [[fallthrough]];
@@ -1140,13 +1178,22 @@ __device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, d
 // SYM: the owner slots of the symmetric dedup schedule (PairSource::sym): every owned pair
 // is scored in both directions in one pass and the two probabilities go to S.ores; the
 // emission pass (k_emit) turns them into the match list.
-template <int RMAX, int LR, bool SYM, bool DP, bool GR = true, bool GEO = false>
+// LB (long-value DP properties): 0 computed in place; 1 the pre-pass (k_long_pre: only those
+// properties, their similarities to P.lsim, no decisions); 2 read from P.lsim (k_score_long)
+template <int RMAX, int LR, bool SYM, bool DP, bool GR = true, bool GEO = false, int LB = 0, int VI = -1>
 __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
                                            uint64_t nslots, const StageOut& out) {
   uint64_t* peq = g_wave_tables[threadIdx.x >> 6];
   for (int e = (int)lane_id(); e < kPeqEntries; e += 64) peq[e] = 0;
 
-  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the block this launch block runs: bucket order over the XCDs (S.bperm), or its own
+  uint64_t bid = blockIdx.x;
+  if (S.bperm) {
+    const uint64_t nb = gridDim.x, m = nb / 8;
+    const uint64_t sb = bid < 8 * m ? (bid % 8) * m + bid / 8 : bid;
+    bid = __builtin_amdgcn_readfirstlane(S.bperm[sb]);
+  }
+  const uint64_t idx = bid * blockDim.x + threadIdx.x;
   const bool in_launch = idx < nslots;
   bool valid = in_launch;
   const uint64_t s = slot0 + min(idx, nslots - 1);
@@ -1164,7 +1211,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     // one query per wave by construction (padded slot layout): the wave's first slot,
     // computed wave-uniformly, so the map read is a scalar load at the head of the chain
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t sw = slot0 + min((uint64_t)blockIdx.x * blockDim.x + (uint64_t)wave * 64u, nslots - 1);
+    const uint64_t sw = slot0 + min(bid * blockDim.x + (uint64_t)wave * 64u, nslots - 1);
     qi = S.wq[sw >> 6];
   }
   qi = __builtin_amdgcn_readfirstlane(qi);
@@ -1271,6 +1318,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     const uint32_t qch = qch_n;
     if (p + 1 < P.nprops) prefetch(order_at(ow, p + 1), lq_n, qch_n, lc_n);
     if (lq == (int)kMissing) continue;  // r1 has no value: property skipped for the wave
+    if (LB == 1 && D.op != DK_CMP_WEIGHTED_LEVENSHTEIN && D.op != DK_CMP_LEVENSHTEIN) continue;
     const bool present = lc != (int)kMissing;
     const bool cmp = present && lq > 0 && lc > 0;
     double sim = 0.0, rev = 0.0;
@@ -1288,8 +1336,18 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       rev = sim;
     } else if (D.op != DK_CMP_NONE) {
       rev = __builtin_nan("");  // marks "same as sim" unless the comparator sets it
-      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM, DP, GR>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch)
-                         : string_sim<RMAX, LR, uint16_t, SYM, DP, GR>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch);
+      // a property on the long-value DP for this wave (wave-uniform): the pre-pass's slot
+      const bool on_long = LR > 0 && (D.op == DK_CMP_WEIGHTED_LEVENSHTEIN ||
+                                      (D.op == DK_CMP_LEVENSHTEIN && lq > kMaxUnits));
+      const uint64_t lat = ((P.long_word >> (4 * pp)) & 15u) * P.lstride + min(idx, nslots - 1);
+      if (LB == 1 && (!on_long || long_variant<LR>(lq) != VI)) continue;  // another pre-pass kernel's
+      const double lbuf = LB == 2 && on_long ? P.lsim[lat] : 0.0;
+      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM, DP, GR, LB, VI>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch, lbuf)
+                         : string_sim<RMAX, LR, uint16_t, SYM, DP, GR, LB, VI>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch, lbuf);
+      if (LB == 1) {
+        if (in_launch) P.lsim[lat] = sim;
+        continue;
+      }
       if (!SYM || rev != rev) rev = sim;
       if (cmp) {
         if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2,
@@ -1317,6 +1375,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     }
   }
 
+  if (LB == 1) return;  // the pre-pass: similarities only
   if (SYM) {
     // owner result for this query's list; the reverse direction into the candidate's mirror
     // segment (a scattered store while the VALU-bound wave keeps computing) when it will be
@@ -1324,10 +1383,10 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     if (in_launch) S.ores[s] = valid ? prob : __builtin_nan("");
     if (mirror && decide(prob2, P.threshold, P.maybe) != 0u)
       S.mres[S.mbase[(uint64_t)ksel * S.nq + (crow - S.r0)] + moff] = prob2;
-    block_emit(out, 0u, 0.0, 0u, qi, valid ? (mirror ? 2u : 1u) : 0u, bytes);  // operands read once
+    block_emit_at(out, bid, 0u, 0.0, 0u, qi, valid ? (mirror ? 2u : 1u) : 0u, bytes);  // operands read once
   } else {
     const uint32_t kind = valid ? decide(prob, P.threshold, P.maybe) : 0u;
-    block_emit(out, kind, prob, crow, qi, valid ? 1u : 0u, bytes);
+    block_emit_at(out, bid, kind, prob, crow, qi, valid ? 1u : 0u, bytes);
   }
 }
 
@@ -1351,11 +1410,40 @@ void k_score_nodp(const ScoreParams P, const PairSource S, uint64_t slot0, uint6
   score_body<16, 0, SYM, false>(P, S, slot0, nslots, out);
 }
 
+// Long values (WeightedLevenshtein, Levenshtein over 64 units): the systolic DP runs in its
+// own pass first -- k_long_pre, the DP inlined (its registers alone, no call frame) -- and
+// leaves each slot's similarity in P.lsim (8 B per slot and long property); k_score_long then
+// scores with every other comparator and reads those.  With the DP as an out-of-line call
+// inside the fused kernel, the call frame and the callee-saved registers of the DP cost a
+// 120-280 B/lane scratch frame.
+#ifndef DK_LONG_SPLIT
+#define DK_LONG_SPLIT 0  // 1: the DP in its own pass (k_long_pre, no scratch) -- measured 1.6x
+                         // slower on configs[4], so the fused call stays the build
+#endif
+#if DK_LONG_SPLIT
+// One pre-pass kernel per DP variant VI (rows per lane, long_variant): each carries that
+// variant alone, so its registers are that variant's; the waves of queries of other lengths
+// leave after the slot mapping.
+template <int LR, int VI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VI >= 4 ? DK_WAVES_LONGPRE_HI : DK_WAVES_LONGPRE, 8)))
+void k_long_pre(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
+  score_body<16, LR, false, true, true, false, 1, VI>(P, S, slot0, nslots, out);
+}
+
+template <int LR, int VI = 0>
+static void launch_long_pre(const ScoreParams& P, const PairSource& src, uint64_t slot0, uint64_t nslots,
+                            const StageOut& out, unsigned grid, hipStream_t s) {
+  k_long_pre<LR, VI><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+  if constexpr (VI + 1 < long_nvariants<LR>()) launch_long_pre<LR, VI + 1>(P, src, slot0, nslots, out, grid, s);
+}
+#endif
+
+
 template <int RMAX, int LR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LR <= 8 ? DK_WAVES_LONG8 : DK_WAVES_LONG16, 8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_LONG8, 8)))
 void k_score_long(const ScoreParams P, const PairSource S,
                                                     uint64_t slot0, uint64_t nslots, StageOut out) {
-  score_body<RMAX, LR, false, true>(P, S, slot0, nslots, out);
+  score_body<RMAX, LR, false, true, true, false, DK_LONG_SPLIT ? 2 : 0>(P, S, slot0, nslots, out);
 }
 
 // Schemas with a GeopositionComparator (P.has_geo; never the symmetric schedule): the direct
@@ -2252,7 +2340,17 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
       else k_score<RM, false, false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);        \
     }                                                                                         \
   } while (0)
+#if DK_LONG_SPLIT
+#define DK_LONG(RM, L)                                                                   \
+  do {                                                                                   \
+    if (!P.lsim || P.lstride < (nslots + kScoreBlock - 1) / kScoreBlock * kScoreBlock)   \
+      return hipErrorInvalidValue;                                                       \
+    launch_long_pre<L>(P, src, slot0, nslots, out, grid, s);                             \
+    k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);        \
+  } while (0)
+#else
 #define DK_LONG(RM, L) k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
+#endif
   if (src.sym && P.long_rows > 0) return hipErrorInvalidValue;  // the host never schedules it
   if (P.has_geo) {
     if (src.sym) return hipErrorInvalidValue;  // the host never schedules it (sym_schema_ok)
@@ -2276,6 +2374,28 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
 #undef DK_LONG
   return hipGetLastError();
 }
+
+// Sort keys of a symmetric owner launch's blocks (256 owner slots from `slot0`): the
+// position of the block's first query in its first key function's sorted table (its own
+// position, else its bucket's start) -- a bucket's queries are then adjacent.
+__global__ void k_sym_block_keys(const PairSource S, uint64_t slot0, uint64_t nblocks,
+                                 uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const uint32_t qi = S.wq[(slot0 + b * kScoreBlock) >> 6];
+  const uint4 r = S.sranges[qi];
+  key[b] = S.segoff[0] + (r.w != kNoPos ? r.w : r.x);
+  val[b] = (uint32_t)b;
+}
+
+hipError_t launch_sym_block_keys(const PairSource& src, uint64_t slot0, uint64_t nblocks, uint64_t* key,
+                                 uint32_t* val, hipStream_t s) {
+  if (nblocks == 0) return hipSuccess;
+  k_sym_block_keys<<<(unsigned)((nblocks + 255) / 256), 256, 0, s>>>(src, slot0, nblocks, key, val);
+  return hipGetLastError();
+}
+
+bool long_dp_split() { return DK_LONG_SPLIT != 0; }
 
 hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s) {
   DK_LAUNCH_GUARD(nblocks);
