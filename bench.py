@@ -729,7 +729,13 @@ def json_batch(w, n, queries, device, torch):
     cols = {k: w["values"][k] for k in names}
     cols.update(extra)
     total = len(next(iter(cols.values())))
-    groups = [(0, total, 0)] if w["group"] is None else [(0, n, 1), (n, total, 2)]
+    if w["group"] is None:
+        groups = [(0, total, 0)]
+    else:   # one body per group (its data source), in row order: group 1's rows come first
+        g = np.asarray(w["group"])
+        n1 = int((g == 1).sum())
+        assert (g[:n1] == 1).all() and (g[n1:] == 2).all()
+        groups = [(0, n1, 1), (n1, total, 2)]
     t_json = time.perf_counter()
     bodies = [json_body(range(a, b), {k: v[a:b] for k, v in cols.items()}) for a, b, _ in groups]
     t_json = time.perf_counter() - t_json
