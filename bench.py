@@ -683,6 +683,8 @@ def main():
             out["warm_batch"] = warm_batch(eng, w, n, queries, torch)
             if w.get("kparts") and not args.no_json_batch:
                 jb = json_batch(w, n, queries, local, torch)
+                # the POSTed records must give the step's pairs (same records, same keys)
+                jb["pairs_equal_to_step"] = jb["cold"]["pairs_scored"] == int(pairs_step)
                 out["json_ingest"] = jb
                 # records/sec deduped from the POSTed body: the end-to-end figure
                 out["records_per_s_end_to_end_lists"] = out["records_per_s_end_to_end"]
