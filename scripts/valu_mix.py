@@ -26,10 +26,11 @@ KERNELS = {  # bench.py roofline pmc_key -> (the kernel its launches use, loop r
     # loop body (k_score_gq's per-group loop, whose inner loops are rare tails)
     "dedup": ("_ZN2dk7k_scoreILi40ELb1ELb0E", "inner"),  # GR = false: no gram-set code
     "dedup_utf16": ("_ZN2dk7k_scoreILi40ELb1ELb0E", "inner"),
-    "linkage": ("_ZN2dk10k_score_gqILi2ELi2E", "outer"),
+    "linkage": ("_ZN2dk10k_score_gqILi2ELi2ELi0E", "outer"),   # role 0 deferred (the build's default)
     "allpairs_lev": ("_ZN2dk7k_scoreILi16ELb0ELb0E", "inner"),
     "allpairs_jw": ("_ZN2dk7k_scoreILi16ELb0ELb0E", "inner"),
     "longtext": ("_ZN2dk12k_score_longILi16ELi16E", "inner"),
+    "reference": ("_ZN2dk7k_scoreILi16ELb0ELb0E", "inner"),
 }
 # cycles per wave64 instruction per SIMD (profiles/r01/valu_rate_gfx950.txt), by class
 TWO = ("v_add_u32_e32", "v_sub_u32_e32", "v_subrev_u32_e32", "v_and_b32_e32", "v_or_b32_e32",
