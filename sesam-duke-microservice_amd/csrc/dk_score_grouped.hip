@@ -913,14 +913,14 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
       const bool cmp = present && ln[b] > 0 && qlen[NQ + b] > 0;
       if (present) by += 2u;
       if (!present) continue;
-      double x = 0.0;
+      float x = 0.0f;
       if (cmp) {
-        const GQQuery v = qv[NQ + b];
-        x = gq_prob(H->n[b].low, H->n[b].high,
-                    numeric(v.num, v.ok != 0, cn[b], cok[b] != 0u, H->n[b].min_ratio));
         by += 9u;  // rnum + rnumok
+const GQQuery v = qv[NQ + b];
+        x = (float)gq_prob(H->n[b].low, H->n[b].high,
+                           numeric(v.num, v.ok != 0, cn[b], cok[b] != 0u, H->n[b].min_ratio));
       }
-      screen_x((float)x);
+      screen_x(x);
     }
     const bool pass = valid && (wide || odds >= H->screen);
     const uint64_t pm = __ballot(pass);
