@@ -916,7 +916,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
       float x = 0.0f;
       if (cmp) {
         by += 9u;  // rnum + rnumok
-const GQQuery v = qv[NQ + b];
+        const GQQuery v = qv[NQ + b];
         x = (float)gq_prob(H->n[b].low, H->n[b].high,
                            numeric(v.num, v.ok != 0, cn[b], cok[b] != 0u, H->n[b].min_ratio));
       }
