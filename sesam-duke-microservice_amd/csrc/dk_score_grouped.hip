@@ -475,7 +475,7 @@ hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uin
 //  * The waves of a SIMD (DK_WAVES_GQ) cover that one round trip.
 // =======================================================================================
 #ifndef DK_WAVES_GQ
-#define DK_WAVES_GQ 6  // k_score_gq waves per SIMD (<= 80 VGPRs; 23 KB LDS per 4 waves: 6 fit)
+#define DK_WAVES_GQ 7  // k_score_gq waves per SIMD (<= 72 VGPRs; 15 KB LDS per 4 waves)
 #endif
 #ifndef DK_GQ_ABL
 #define DK_GQ_ABL 0  // timing ablations only (wrong results): 1 probes, 2 f64 math, 4 row traffic
@@ -532,6 +532,18 @@ __device__ __forceinline__ rsrc_t gq_rsrc(const void* p, uint32_t bytes) {
 }
 
 
+// |Q ∩ C| of one key word against a table of 16-bit entries (k_score_gq): the same slots
+// as probe_word, half the LDS
+__device__ __forceinline__ int probe_word16(const uint16_t* tab, uint64_t w, uint32_t mult, int sh) {
+  int c = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t key = (uint32_t)(w >> (16 * e)) & 0xFFFFu;
+    c += (uint32_t)tab[(uint32_t)__umul24(key, mult) >> sh] == key ? 1 : 0;
+  }
+  return c;
+}
+
 // the query's values of one role (wave-uniform), staged in LDS once per task
 struct GQQuery {
   uint16_t len, m1, seed;  // QGram: grams, perfect-hash seed
@@ -542,13 +554,16 @@ static_assert(sizeof(GQQuery) == 16, "one ds_read_b128");
 static_assert(sizeof(GQArgs) % 16 == 0, "GQArgs copied to LDS in 16-B pieces");
 
 template <int NQ, int NN, int DEF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEF < 0 && NQ == 2 ? DK_WAVES_GQ - 1 : DK_WAVES_GQ, 8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEF < 0 && NQ == 2 ? DK_WAVES_GQ - 2 : DK_WAVES_GQ, 8)))
 void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots,
                 const uint32_t* __restrict__ perm, const GQArgs* __restrict__ A, StageOut out) {
   constexpr int NR = NQ + NN;
   constexpr int NQ1 = NQ > 0 ? NQ : 1, NN1 = NN > 0 ? NN : 1, NR1 = NR > 0 ? NR : 1;
   static_assert(DEF < NQ, "the deferred role is a QGram role");
-  __shared__ uint32_t lds[kScoreBlock / 64][kGroupedTabs * kTabWords];
+  // per QGram role a table of 512 16-bit slots (a key, 0 = empty; slot 0 starts with a
+  // sentinel key that hashes elsewhere, so neither a padding key 0 nor any other key that
+  // lands on slot 0 finds it)
+  __shared__ uint16_t lds[kScoreBlock / 64][kGroupedTabs * kTabWords];
   __shared__ uint64_t queue_lds[kScoreBlock / 64][kGQQueue];
   __shared__ GQQuery qlds[kScoreBlock / 64][kGroupedTabs + kGQMaxNum];
   __shared__ uint2 slds[kScoreBlock / 64][kMaxSegs];  // per segment: {first position, length}
@@ -557,7 +572,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
   const uint32_t lane = lane_id();
   const uint64_t task = grouped_task(perm, slot0 / kScoreBlock, nslots / kScoreBlock, wave);
   if (task == ~0ull) return;  // the whole wave: no workgroup barrier follows
-  uint32_t* tabs = lds[wave];
+  uint16_t* tabs = lds[wave];
   GQQuery* qv = qlds[wave];
   uint2* seg = slds[wave];
   uint64_t* queue = queue_lds[wave];
@@ -631,7 +646,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
     const uint64_t ro = A->rorder[P.norders > 1 ? (int)__builtin_amdgcn_readfirstlane((uint32_t)P.oclass[q]) : 0];
     if (lane == 0) hlds[wave].rorder[0] = ro;
   }
-  for (int e = (int)lane * 4; e < NQ * kTabWords; e += 256)
+  for (int e = (int)lane * 8; e < NQ * kTabWords; e += 512)
     *reinterpret_cast<uint4*>(tabs + e) = make_uint4(0u, 0u, 0u, 0u);
   wave_lds_sync();
   uint32_t gn, fkn, cqn[NQ1];
@@ -643,12 +658,20 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
     const uint32_t sd = __builtin_amdgcn_readfirstlane((uint32_t)v.seed);
     const uint32_t m1 = __builtin_amdgcn_readfirstlane((uint32_t)v.m1);
     if (__builtin_amdgcn_readfirstlane((uint32_t)v.len) != kMissing && m1 > 0 && sd != kGramSeedNone) {
-      uint32_t* tab = tabs + a * kTabWords;
+      uint16_t* tab = tabs + a * kTabWords;
       const DevProp& D = P.props[A->q[a].prop];
-      if (lane == 0) tab[0] = ~0u;  // a real key landing in slot 0 overwrites the sentinel
-      if (lane < m1) {
-        const uint32_t key = gram_key(D.grams[D.goff[q] + lane]);
-        tab[(uint32_t)__umul24(key, gram_mult(sd & 0xFFu)) >> (24 - (int)(sd >> 8))] = key;
+      const uint32_t mult = gram_mult(sd & 0xFFu);
+      const int sh = 24 - (int)(sd >> 8);
+      // the sentinel: the smallest key in 1..64 whose slot is not 0
+      const uint64_t off0 = __ballot(((uint32_t)__umul24(lane + 1u, mult) >> sh) != 0u);
+      if (off0 == 0ull) {
+        if (lane == 0) qv[a].seed = kGramSeedNone;  // (no such key: the sorted-list path)
+      } else {
+        if (lane == 0) tab[0] = (uint16_t)(__builtin_ctzll(off0) + 1);  // a real key in slot 0 overwrites it
+        if (lane < m1) {
+          const uint32_t key = gram_key(D.grams[D.goff[q] + lane]);
+          tab[(uint32_t)__umul24(key, mult) >> sh] = (uint16_t)key;
+        }
       }
     }
   }
@@ -686,14 +709,14 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
   // |Q ∩ C| of role a: the rows held in registers, then the rest kTailRows at a time
   auto role_common = [&](GQLds* H, auto ic, uint32_t g, uint32_t nw, uint32_t sdv, const uint64_t* w) -> int {
     constexpr int a = decltype(ic)::value;
-    const uint32_t* tab = tabs + a * kTabWords;
+    const uint16_t* tab = tabs + a * kTabWords;
     const uint32_t mult = gram_mult(sdv & 0xFFu);
     const int sh = 24 - (int)(sdv >> 8);  // 32 - lt
     int common = 0;
 #pragma unroll
     for (int j = 0; j < GQRows<a>::v; ++j)
       if (!DK_GQ_GUARD || __builtin_amdgcn_ballot_w64((uint32_t)j < nw))  // uniform: a lane has row j
-        if (!(DK_GQ_ABL & 1)) common += probe_word(tab, w[j], mult, sh);
+        if (!(DK_GQ_ABL & 1)) common += probe_word16(tab, w[j], mult, sh);
     if (__builtin_amdgcn_ballot_w64(nw > (uint32_t)GQRows<a>::v)) {
       const rsrc_t rt = gq_rsrc(gq_uptr(H->q[a].tail), gq_u(H->q[a].tail_bytes));
       const uint32_t rowb = gq_u(H->q[a].rowb);
@@ -708,7 +731,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
                                                    rt, (uint32_t)(j + i) < nw ? off : 0xFFFFFFFFu, 0, 0));
         }
 #pragma unroll
-        for (int i = 0; i < kTailRows; ++i) common += probe_word(tab, wt[i], mult, sh);
+        for (int i = 0; i < kTailRows; ++i) common += probe_word16(tab, wt[i], mult, sh);
         if (!__builtin_amdgcn_ballot_w64(nw > (uint32_t)(j + kTailRows))) break;
       }
     }
