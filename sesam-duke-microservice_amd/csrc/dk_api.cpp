@@ -560,6 +560,8 @@ struct dk_ctx {
   // per-(key, query) bucket positions, owner results, chunk boundaries
   DevBuf ocounts, oqoff, owq, obase, ores, mcounts, mqoff, mbase, mres, bidx, bval;
   DevBuf lsim;             // the long-value DP pre-pass's similarities (k_long_pre)
+  DevBuf raised;           // k_score_geo: a compared GeopositionComparator value without ','
+  PinnedBuf h_raised;
   DevBuf symkey, symval;   // symmetric owner launches: block sort keys / bucket-order permutation
   PinnedBuf h_bounds;
   DevBuf counters;
@@ -773,7 +775,8 @@ static int create_impl(const dk_schema* schema, int device, dk_ctx** out) {
     return fail(DK_E_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
   }
   if (c->counters.reserve(4 * sizeof(uint64_t), 0, c->stream) != hipSuccess ||
-      c->h_small.reserve(64) != hipSuccess) {
+      c->h_small.reserve(64) != hipSuccess || c->raised.reserve(64, 0, c->stream) != hipSuccess ||
+      c->h_raised.reserve(64) != hipSuccess) {
     delete c;
     return fail(DK_E_DEVICE, "counter allocation failed");
   }
@@ -1041,11 +1044,9 @@ static int stage_column(dk_ctx* c, int pidx, const dk_column* col, uint64_t n, C
       else memcpy(v16.data(), u16 + a, L * 2);
       if (nw == 2) {
         const int r = parse_geoposition(v16.data(), L, &S.num[2 * i], &S.num[2 * i + 1]);
-        if (r < 0) {
-          pbad[t] = i | (1ull << 63);
-          return;
-        }
-        S.numok[i] = (uint8_t)r;
+        // no ',': stock Duke raises when it COMPARES such a value -- kept with numok 2, and a
+        // dk_match / compare that scores it fails (k_score_geo sets P.raised)
+        S.numok[i] = (uint8_t)(r < 0 ? 2 : r);
       } else if (is_num) {
         double v = 0.0;
         S.numok[i] = java_parse_double(v16.data(), L, &v) ? 1 : 0;
@@ -1700,6 +1701,7 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
   P.oclass = c->oclass.as<uint8_t>();
   // the long-value DP's properties (k_long_pre): WeightedLevenshtein, and Levenshtein (its
   // queries over 64 units); the buffer is set per launch (long_sim_buffer)
+  P.raised = c->raised.as<uint32_t>();
   P.lsim = nullptr;
   P.lstride = 0;
   P.long_word = ~0ull;
@@ -2688,6 +2690,22 @@ static int tile_match(dk_ctx* c, const ScoreParams& P, const BlockTables& T, uin
   return DK_OK;
 }
 
+// GeopositionComparator values without ',' (numok 2): cleared before a geo schema's scoring,
+// read after it; set -> the call fails as stock Duke's compare would raise
+static int geo_raise_clear(dk_ctx* c, const ScoreParams& P) {
+  if (P.has_geo) HIPCHK(hipMemsetAsync(c->raised.p, 0, 4, c->stream));
+  return DK_OK;
+}
+static int geo_raise_check(dk_ctx* c, const ScoreParams& P) {
+  if (!P.has_geo) return DK_OK;
+  HIPCHK(hipMemcpyAsync(c->h_raised.p, c->raised.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (*c->h_raised.as<uint32_t>())
+    return fail(DK_E_UNSUPPORTED, "GeopositionComparator compared a value without ',' "
+                                  "(stock Duke raises: Geoposition.parse)");
+  return DK_OK;
+}
+
 static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
                      ResultHolder* R, bool contiguous) {
   hipStream_t s = c->stream;
@@ -2719,6 +2737,10 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     if (rc) return rc;
   }
   const ScoreParams P = make_params(c, c->rep, c->rowof_p, c->rstride);
+  {
+    const int rg = geo_raise_clear(c, P);
+    if (rg) return rg;
+  }
   c->prof.replica_positions = P.rstride;
   c->prof.gram_row_bytes = 0;
   for (int p = 0; p < P.nprops; ++p)
@@ -3170,6 +3192,10 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   }
   HIPCHK(hipMemcpyAsync(c->h_small.p, c->counters.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  {
+    const int rg = geo_raise_check(c, P);
+    if (rg) return rg;
+  }
   const uint64_t scored = c->h_small.as<uint64_t>()[0];
   const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
   if (sym) c->prof.sym_matches += 1;
@@ -3425,6 +3451,8 @@ static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double
   src.mpad = 64;
   src.same_ok = 1;  // Processor.compare scores a record against itself too
   if (!long_sim_buffer(c, P, 1)) return fail(DK_E_DEVICE, "long-value DP buffer");
+  rc = geo_raise_clear(c, P);
+  if (rc) return rc;
   HIPCHK(launch_score(P, src, 0, 1, st, s));
   uint32_t n = 0;
   double p = NAN;
@@ -3440,6 +3468,8 @@ static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double
     HIPCHK(hipMemcpyAsync(&lev, base + 120, 8, hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
+  rc = geo_raise_check(c, P);
+  if (rc) return rc;
   *prob = n ? (lev == lev ? lev : p) : NAN;
   return DK_OK;
 }

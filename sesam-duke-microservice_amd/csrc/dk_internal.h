@@ -139,6 +139,9 @@ struct ScoreParams {
   double* lsim;
   uint64_t lstride;
   uint64_t long_word;
+  // GeopositionComparator: set (non-zero) by a kernel that compared a value without ','
+  // (numok 2) -- stock Duke raises there; the host then fails the call
+  uint32_t* raised;
   DevProp props[kMaxProps];
 };
 

@@ -1330,8 +1330,13 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
       if (cmp) bytes += 9u;   // rnum + rnumok
       rev = sim;
     } else if (GEO && D.op == DK_CMP_GEOPOSITION) {
-      if (cmp) sim = geoposition(D.num[2 * q], D.num[2 * q + 1], D.numok[q] != 0, D.rnum[2 * g], D.rnum[2 * g + 1],
-                                 D.rnumok[g] != 0, D.min_ratio);
+      if (cmp) {
+        const uint32_t ok1 = D.numok[q], ok2 = D.rnumok[g];
+        if (ok1 == 2u || ok2 == 2u)  // a value without ',': Duke raises on this comparison
+          __hip_atomic_fetch_or(P.raised, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sim = geoposition(D.num[2 * q], D.num[2 * q + 1], ok1 == 1u, D.rnum[2 * g], D.rnum[2 * g + 1],
+                          ok2 == 1u, D.min_ratio);
+      }
       if (cmp) bytes += 17u;  // rnum pair + rnumok
       rev = sim;
     } else if (D.op != DK_CMP_NONE) {

@@ -697,7 +697,8 @@ def test_geoposition(mode):
     see oracle/duke_oracle.c dko_geoposition): positions scattered within a few km, some
     unparsable ("x,1" -> 0.5) and some missing, next to a Levenshtein name; the GPU path
     against the oracle at the north star's tolerance, and each similarity through
-    dk_property_similarity.  A value without ',' is refused at upsert (stock Duke raises)."""
+    dk_property_similarity.  A value without ',' is accepted; comparing it fails the call
+    (stock Duke raises there)."""
     rng = random.Random(31)
     n = 600
     pos = []
@@ -726,7 +727,25 @@ def test_geoposition(mode):
             continue
         want = O.geoposition(pos[a], pos[b], 4000.0)
         assert abs(got - want) <= 1e-12 * abs(want), (pos[a], pos[b], got, want)
+    # a value without ',' (ADVICE r4): accepted at upsert; stock Duke raises only when it
+    # compares it (Geoposition.parse), so does the GPU path -- here every pair is compared
+    rows = eng.upsert(1, np.array([99], np.uint64), [dh.Column.from_strings(["59.9"]), dh.Column.from_strings(["a"])])
     with pytest.raises(dh.DukeHipError) as e:
-        eng.upsert(1, np.array([99], np.uint64), [dh.Column.from_strings(["59.9"]), dh.Column.from_strings(["a"])])
+        eng.property_similarity(0, int(rows[0]), 1)
     assert e.value.code == A.DK_E_UNSUPPORTED
+    with pytest.raises(dh.DukeHipError) as e:
+        eng.match(np.arange(61, dtype=np.uint32))
+    assert e.value.code == A.DK_E_UNSUPPORTED
+    assert eng.property_similarity(0, 7, 11) == eng.property_similarity(0, 7, 11)   # others still fine
     eng.close()
+    # key blocking: the record's key is its own, it is never compared, the batch scores as
+    # without it (bit-exact against the oracle on the rest)
+    if mode == "dedup":
+        eng = dh.GpuEngine(schema_of(props, 0.8, 0.6, "dedup", 1))
+        eng.upsert(n + 1, np.arange(n + 1, dtype=np.uint64),
+                   [dh.Column.from_strings(pos + ["59.9"]), dh.Column.from_strings(names + ["a"])],
+                   key_columns=[dh.Column.from_strings(keys[0] + ["zzz"])])
+        res2 = eng.match(np.arange(n + 1, dtype=np.uint32))
+        assert res2.pairs_scored == res.pairs_scored
+        assert np.array_equal(res2.candidate, res.candidate) and np.array_equal(res2.prob, res.prob)
+        eng.close()
