@@ -328,10 +328,10 @@ bool is_norm_ws(char16_t c) {  // the runs LowerCaseNormalizeCleaner collapses
   return c == u' ' || c == u'\t' || c == u'\n' || c == u'\r' || c == 0x00A0;
 }
 
-bool py_isspace(uint32_t c) {  // Python str.isspace (str.split() / strip())
-  return (c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x20) || c == 0x85 || c == 0xA0 ||
-         c == 0x1680 || (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 ||
-         c == 0x202F || c == 0x205F || c == 0x3000;
+inline bool py_isspace(uint32_t c) {  // Python str.isspace (str.split() / strip())
+  if (c < 0x80) return (c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x20);
+  return c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) || c == 0x2028 ||
+         c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
 }
 
 void lowercase_normalize(std::u16string& s) {  // in place: the output is never longer
@@ -420,25 +420,35 @@ void py_slice(int64_t n, int32_t start, int32_t end, int64_t* a, int64_t* b) {
 void key_part_bmp(const std::u16string& v, const dk_key_part& kp, std::u16string& out) {
   size_t lo = 0, hi = v.size();
   if (kp.token != INT32_MIN) {  // str.split() then toks[token], without materialising toks
-    // count the tokens, then find token t (negative: from the end)
-    int64_t nt = 0;
-    for (size_t i = 0; i < v.size();) {
-      while (i < v.size() && py_isspace(v[i])) ++i;
-      if (i >= v.size()) break;
-      ++nt;
-      while (i < v.size() && !py_isspace(v[i])) ++i;
-    }
-    int64_t t = kp.token;
-    if (t < -nt || t >= nt) return;
-    if (t < 0) t += nt;
-    for (size_t i = 0, k = 0; i < v.size(); ++k) {
-      while (i < v.size() && py_isspace(v[i])) ++i;
-      const size_t a = i;
-      while (i < v.size() && !py_isspace(v[i])) ++i;
-      if ((int64_t)k == t) {
-        lo = a;
-        hi = i;
-        break;
+    // token t >= 0: the t-th from the front; t < 0: the (-t)-th from the back (absent: "")
+    const size_t n = v.size();
+    if (kp.token >= 0) {
+      int64_t k = 0;
+      size_t i = 0;
+      for (;; ++k) {
+        while (i < n && py_isspace(v[i])) ++i;
+        if (i >= n) return;
+        const size_t a = i;
+        while (i < n && !py_isspace(v[i])) ++i;
+        if (k == kp.token) {
+          lo = a;
+          hi = i;
+          break;
+        }
+      }
+    } else {
+      int64_t k = -1;
+      size_t i = n;
+      for (;; --k) {
+        while (i > 0 && py_isspace(v[i - 1])) --i;
+        if (i == 0) return;
+        const size_t b = i;
+        while (i > 0 && !py_isspace(v[i - 1])) --i;
+        if (k == kp.token) {
+          lo = i;
+          hi = b;
+          break;
+        }
       }
     }
   }
@@ -901,23 +911,78 @@ void split_entities(const char* J, uint64_t len, Split& S) {
   }
 }
 
-// One worker's slice of a column: values back to back, offsets relative to the slice.
+// One worker's slice of a column: values back to back, offsets relative to the slice.  The
+// units are kept one byte wide while every unit so far is <= 0xFF (the common case: half the
+// scratch, and the merge copies them as they are), two bytes from the first wider one on
+// (or from the start: the record-ID column, which the interner reads as UTF-16).
 struct ColPart {
-  std::vector<uint32_t> off{0};
-  std::vector<char16_t> u;
-  std::vector<uint8_t> present;
-  bool missing = false;
-  char16_t maxu = 0;
-  void add(const std::u16string& v) {
-    char16_t m = maxu;
-    for (char16_t c : v) m = c > m ? c : m;
-    maxu = m;
-    u.insert(u.end(), v.begin(), v.end());
-    off.push_back((uint32_t)u.size());
+  PodVec<uint32_t> off;
+  PodVec<uint8_t> u8;
+  PodVec<char16_t> u16;
+  PodVec<uint8_t> present;
+  bool missing = false, wide = false;
+  char16_t orv = 0;  // the OR of every unit: <= 0xFF iff the slice is narrow
+  void init(uint64_t n, uint64_t units, bool wide16) {
+    wide = wide16;
+    off.reserve(n + 1);
+    off.push_back(0);
+    present.reserve(n);
+    if (wide) u16.reserve(units);
+    else u8.reserve(units);
+  }
+  uint64_t units() const { return wide ? u16.size() : u8.size(); }
+  void widen() {
+    u16.reserve(std::max<uint64_t>(2 * u8.size(), 64));
+    u16.resize_uninit(u8.size());
+    for (uint64_t i = 0; i < u8.size(); ++i) u16[i] = u8[i];
+    u8 = PodVec<uint8_t>();
+    wide = true;
+  }
+  void add(const char16_t* v, size_t n) {
+    char16_t o = 0;
+    for (size_t i = 0; i < n; ++i) o |= v[i];
+    orv |= o;
+    if (!wide && o > 0xFF) widen();
+    if (wide) {
+      u16.append(v, n);
+    } else {
+      const uint64_t b = u8.size();
+      u8.resize_uninit(b + n);
+      uint8_t* d = u8.data() + b;
+      for (size_t i = 0; i < n; ++i) d[i] = (uint8_t)v[i];
+    }
+    off.push_back((uint32_t)units());
     present.push_back(1);
   }
+  void add(const std::u16string& v) { add(v.data(), v.size()); }
+  void add_bytes(const char* v, size_t n) {  // ASCII: the units are the bytes
+    if (wide) {
+      const uint64_t b = u16.size();
+      u16.resize_uninit(b + n);
+      for (size_t i = 0; i < n; ++i) u16[b + i] = (unsigned char)v[i];
+    } else {
+      u8.append(reinterpret_cast<const uint8_t*>(v), n);
+    }
+    off.push_back((uint32_t)units());
+    present.push_back(1);
+  }
+  // pre (UTF-16) then the ASCII bytes v, as two-byte units; returns where the value starts
+  const char16_t* add_prefixed(const char16_t* pre, size_t np, const char* v, size_t n) {
+    if (!wide) widen();
+    char16_t o = 0;
+    for (size_t i = 0; i < np; ++i) o |= pre[i];
+    orv |= o;
+    const uint64_t b = u16.size();
+    u16.resize_uninit(b + np + n);
+    char16_t* d = u16.data() + b;
+    memcpy(d, pre, np * 2);
+    for (size_t i = 0; i < n; ++i) d[np + i] = (unsigned char)v[i];
+    off.push_back((uint32_t)units());
+    present.push_back(1);
+    return d;
+  }
   void add_missing() {
-    off.push_back((uint32_t)u.size());
+    off.push_back((uint32_t)units());
     present.push_back(0);
     missing = true;
   }
@@ -940,21 +1005,103 @@ struct SourceView {
   std::u16string ds;
 };
 
+// ---- the ASCII fast path ---------------------------------------------------------------
+// [a, b) holds no '\\' and no byte >= 0x80: its JSON string content is its UTF-16 units
+inline bool plain_ascii(const char* a, const char* b) {
+  uint64_t acc = 0, bs = 0, w;
+  for (; b - a >= 8; a += 8) {
+    memcpy(&w, a, 8);
+    acc |= w;
+    bs |= zero_byte(w ^ 0x5C5C5C5C5C5C5C5Cull);
+  }
+  for (; a < b; ++a) {
+    acc |= (unsigned char)*a;
+    bs |= *a == '\\';
+  }
+  return !((acc & 0x8080808080808080ull) | bs);
+}
+
+// key_part_bmp over an ASCII value (code points = bytes; the same token and slice rules)
+void key_part_ascii(const char* v, size_t n, const dk_key_part& kp, std::string& out) {
+  size_t lo = 0, hi = n;
+  if (kp.token != INT32_MIN) {
+    if (kp.token >= 0) {
+      size_t i = 0;
+      for (int64_t k = 0;; ++k) {
+        while (i < n && py_isspace((unsigned char)v[i])) ++i;
+        if (i >= n) return;
+        const size_t a = i;
+        while (i < n && !py_isspace((unsigned char)v[i])) ++i;
+        if (k == kp.token) {
+          lo = a;
+          hi = i;
+          break;
+        }
+      }
+    } else {
+      size_t i = n;
+      for (int64_t k = -1;; --k) {
+        while (i > 0 && py_isspace((unsigned char)v[i - 1])) --i;
+        if (i == 0) return;
+        const size_t b = i;
+        while (i > 0 && !py_isspace((unsigned char)v[i - 1])) --i;
+        if (k == kp.token) {
+          lo = i;
+          hi = b;
+          break;
+        }
+      }
+    }
+  }
+  int64_t a, b;
+  py_slice((int64_t)(hi - lo), kp.start, kp.end, &a, &b);
+  out.append(v + lo + a, (size_t)(b - a));
+}
+
+// Does the entity take the fast path?  Every member read is a string without escapes or
+// non-ASCII bytes, a number or a boolean literal (getAsString: the text as written), `_id`
+// is one of those and not empty, `_deleted` (if present) is a boolean literal, no column
+// cleans (checked per source) and no property gets a second value; the property values are
+// then the members' raw spans (pa, pl).  Anything else -- arrays, null, escapes, UTF-8,
+// errors -- goes through the general path, which decodes, or reports, it.
+bool ascii_record(const SourceView& V, const std::vector<Val>& got, const std::vector<char>& has,
+                  std::vector<const char*>& pa, std::vector<uint32_t>& pl, std::vector<char>& pset) {
+  auto plain = [](const Val& v) {
+    return v.kind == J_NUM || v.kind == J_BOOL || (v.kind == J_STR && plain_ascii(v.a, v.b));
+  };
+  const Val& id = got[V.i_id];
+  if (!has[V.i_id] || !plain(id) || id.a == id.b) return false;
+  if (has[V.i_del] && got[V.i_del].kind != J_BOOL) return false;
+  std::fill(pset.begin(), pset.end(), 0);
+  const dk_source* src = V.src;
+  for (int c = 0; c < src->ncolumns; ++c) {
+    if (!has[c]) continue;
+    const Val& v = got[c];
+    if (!plain(v)) return false;
+    const int p = src->columns[c].prop;
+    if (v.a == v.b || p < 0) continue;  // RecordBuilder.addValue skips ""
+    if (pset[p]) return false;
+    pset[p] = 1;
+    pa[p] = v.a;
+    pl[p] = (uint32_t)(v.b - v.a);
+  }
+  return true;
+}
+
 // IncrementalDataSource.DatasetDataSourceRecordIterator.next for entities [e0, e1)
 void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out) {
   clear_upper();  // the calling thread's (a worker's is clean)
   const dk_source* src = V.src;
   const int np = src->nprops, nk = src->nkeys;
-  out.cols.assign(np + nk + 2, ColPart());
+  out.cols.clear();
+  out.cols.resize(np + nk + 2);
   const uint64_t n = out.e1 - out.e0;
-  // a value is at most as long as its JSON text (keys and IDs: their parts' lengths): the
-  // slice's bytes bound every column's units, so the buffers never grow and copy
+  // a value is at most as long as its JSON text: the slice's bytes bound every property
+  // column's units, so those buffers never grow and copy (reserved, untouched pages cost
+  // nothing); keys and IDs grow geometrically from a per-record guess
   const uint64_t bytes = n ? S.spans[out.e1 - 1].second - S.spans[out.e0].first : 0;
-  for (auto& c : out.cols) {
-    c.off.reserve(n + 1);
-    c.present.reserve(n);
-  }
-  for (int p = 0; p < np; ++p) out.cols[p].u.reserve(bytes / 2 + 64);
+  for (int c = 0; c < np + nk + 2; ++c)
+    out.cols[c].init(n, c < np ? bytes + 64 : 16 * n + 64, c == np + nk);
   out.deleted.reserve(n);
   out.hash.reserve(n);
   std::vector<Val> got(V.names.size()), side;
@@ -963,7 +1110,20 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
   std::vector<std::u16string> pv(np + kMaxKeyOnly);
   std::vector<char> pset(np + kMaxKeyOnly);
   std::u16string s, key, mname, eid, rid;
+  if (src->group_no) {  // "<group>__<dataset>__" / "<dataset>__", then the entity id
+    rid.push_back((char16_t)(u'0' + src->group_no));
+    rid += u"__";
+  }
+  rid += V.ds;
+  rid += u"__";
+  const size_t rid_prefix = rid.size();
   KeyScratch ks;
+  // the ASCII fast path (ascii_record): no column cleans (a cleaner rewrites the value)
+  bool fast_src = !getenv("DK_INGEST_NOFAST");
+  for (int c = 0; c < src->ncolumns; ++c) fast_src = fast_src && src->columns[c].cleaner == DK_CLEAN_NONE;
+  std::vector<const char*> pa(np + kMaxKeyOnly);
+  std::vector<uint32_t> pl(np + kMaxKeyOnly);
+  std::string kb;
   uint64_t r = out.e0;
   try {
     for (; r < out.e1; ++r) {
@@ -1012,6 +1172,30 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
       }
       R.ws();
       if (R.p != R.e) fail(DK_E_UNSUPPORTED, "JSON: trailing characters");
+      if (fast_src && ascii_record(V, got, has, pa, pl, pset)) {
+        // every value read is ASCII text as written: its bytes are its UTF-16 units, the
+        // same values the general path below produces, without decoding
+        for (int p = 0; p < np; ++p) {
+          if (pset[p]) out.cols[p].add_bytes(pa[p], pl[p]);
+          else out.cols[p].add_missing();
+        }
+        for (int k = 0; k < nk; ++k) {
+          kb.clear();
+          const dk_key_function& kf = src->keys[k];
+          for (int i = 0; i < kf.nparts; ++i) {
+            const dk_key_part& kp = kf.parts[i];
+            if (kp.prop < 0 || kp.prop >= np + kMaxKeyOnly) fail(DK_E_INVALID, "key part property out of range");
+            if (pset[kp.prop]) key_part_ascii(pa[kp.prop], pl[kp.prop], kp, kb);
+          }
+          out.cols[np + k].add_bytes(kb.data(), kb.size());
+        }
+        const Val& id = got[V.i_id];
+        const char16_t* rp = out.cols[np + nk].add_prefixed(rid.data(), rid_prefix, id.a, (size_t)(id.b - id.a));
+        out.hash.push_back(U16Table::hash(rp, rid_prefix + (size_t)(id.b - id.a)));
+        out.cols[np + nk + 1].add_bytes(id.a, (size_t)(id.b - id.a));
+        out.deleted.push_back(has[V.i_del] && got[V.i_del].a[0] == 't' ? 1 : 0);
+        continue;
+      }
       // entity id (IncrementalDataSource.java:54-61)
       eid.clear();
       if (has[V.i_id]) as_string(got[V.i_id], side, eid, "_id");
@@ -1036,7 +1220,7 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
           if (pset[sc.prop])
             fail(DK_E_UNSUPPORTED, std::string("column ") + sc.name +
                                        ": a second value for one property (the GPU path holds one)");
-          pv[sc.prop] = s;
+          pv[sc.prop].swap(s);  // s takes the old buffer (cleared by the next as_string)
           pset[sc.prop] = 1;
         }
       }
@@ -1056,13 +1240,7 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
         out.cols[np + k].add(key);
       }
       // synthetic properties (IncrementalDataSource.java:76-98)
-      rid.clear();
-      if (src->group_no) {
-        rid.push_back((char16_t)(u'0' + src->group_no));
-        rid += u"__";
-      }
-      rid += V.ds;
-      rid += u"__";
+      rid.resize(rid_prefix);
       rid += eid;
       out.cols[np + nk].add(rid);
       out.cols[np + nk + 1].add(eid);
@@ -1109,15 +1287,15 @@ void merge_columns(std::vector<Slice>& sl, uint64_t n, std::vector<FinalCol>& F,
   for (int c = 0; c < NC; ++c) {
     ColPlan& L = plan[c];
     L.ubase.assign(T + 1, 0);
-    char16_t maxu = 0;
+    char16_t orv = 0;
     for (int t = 0; t < T; ++t) {
       const ColPart& P = sl[t].cols[c];
-      L.ubase[t + 1] = L.ubase[t] + P.u.size();
+      L.ubase[t + 1] = L.ubase[t] + P.units();
       L.missing = L.missing || P.missing;
-      maxu = std::max(maxu, P.maxu);
+      orv |= P.orv;
     }
     if (L.ubase[T] >= (1ull << 32)) fail(DK_E_UNSUPPORTED, "a column of over 4G units in one batch");
-    L.narrow = maxu <= 0xFF;
+    L.narrow = orv <= 0xFF;
     F[c].off.reset_uninit(n + 1);
     F[c].off[0] = 0;
     if (L.narrow) F[c].u8.reset_uninit(L.ubase[T] + 1);
@@ -1132,14 +1310,24 @@ void merge_columns(std::vector<Slice>& sl, uint64_t n, std::vector<FinalCol>& F,
       const uint32_t b = (uint32_t)L.ubase[t];
       uint32_t* o = F[c].off.data() + r0 + 1;
       for (uint64_t i = 0; i < m; ++i) o[i] = P.off[i + 1] + b;
-      const size_t nu = P.u.size();
-      if (L.narrow) {
+      const size_t nu = P.units();
+      if (L.narrow) {  // every part's units are <= 0xFF
         uint8_t* d = F[c].u8.data() + L.ubase[t];
-        const char16_t* u = P.u.data();
-        for (size_t i = 0; i < nu; ++i) d[i] = (uint8_t)u[i];
+        if (!P.wide) {
+          if (nu) memcpy(d, P.u8.data(), nu);
+        } else {
+          const char16_t* u = P.u16.data();
+          for (size_t i = 0; i < nu; ++i) d[i] = (uint8_t)u[i];
+        }
         if (t == T - 1) F[c].u8[L.ubase[T]] = 0;
       } else {
-        if (nu) memcpy(F[c].u16.data() + L.ubase[t], P.u.data(), nu * 2);
+        uint16_t* d = F[c].u16.data() + L.ubase[t];
+        if (P.wide) {
+          if (nu) memcpy(d, P.u16.data(), nu * 2);
+        } else {
+          const uint8_t* u = P.u8.data();
+          for (size_t i = 0; i < nu; ++i) d[i] = u[i];
+        }
         if (t == T - 1) F[c].u16[L.ubase[T]] = 0;
       }
       if (L.missing && m) memcpy(F[c].present.data() + r0, P.present.data(), m);
@@ -1282,7 +1470,7 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
         const Slice& x = sl[t];
         const ColPart& C = x.cols[np + nk];
         for (uint64_t i = 0; i < x.e1 - x.e0; ++i) {
-          ptr[x.e0 + i] = C.u.data() + C.off[i];
+          ptr[x.e0 + i] = C.u16.data() + C.off[i];   // the ID column is always wide
           ln[x.e0 + i] = C.off[i + 1] - C.off[i];
           hs[x.e0 + i] = x.hash[i];
         }

@@ -127,6 +127,77 @@ def test_pack_json_key_only_property(seed):
         I.NativeSource(src, PROPS, [dh.PartsKey(("NOWHERE", None, 0, 2))])
 
 
+def plain_source(group=None):
+    """No column cleans: plain entities take dk_pack_json's ASCII fast path."""
+    cols = [DataSourceColumn("name", "NAME", None), DataSourceColumn("city", "CITY", None),
+            DataSourceColumn("note", "NOTE", None), DataSourceColumn("area", "AREA", None),
+            DataSourceColumn("raw", "RAW", None), DataSourceColumn("extra", "UNSCORED", None)]
+    return DataSource("ds-1", cols, group)
+
+
+def plain_entities(rng, n):
+    """Mostly plain ASCII entities (the fast path), every few one the general path takes:
+    escapes, UTF-8, arrays, a JSON null, a string `_deleted`."""
+    ascii_ = list("abcdeXYZ019 -\t")
+    odd = ["é", "\U0001F600", "\\", '"', "\n", "€"]
+    ents = []
+    for i in range(n):
+        e = {"_id": rng.choice([str(i), i, f"x {i}", True])}
+        for k in ("name", "city", "note", "raw", "extra"):
+            if rng.random() < 0.85:
+                e[k] = rand_text(rng, ascii_, 0, 16)
+        if rng.random() < 0.5:
+            e["area"] = rng.choice([rng.randint(-5, 50), rng.random() * 100, "7", True, False, ""])
+        if rng.random() < 0.1:
+            e["_deleted"] = rng.choice([True, False])
+        r = rng.random()
+        if r < 0.05:
+            e["note"] = rand_text(rng, ascii_ + odd, 1, 10)
+        elif r < 0.08:
+            e["city"] = [rand_text(rng, ascii_, 1, 6)]
+        elif r < 0.10:
+            e["_deleted"] = rng.choice(["TRUE", "no", [True]])
+        elif r < 0.11:
+            e["extra"] = None
+        ents.append(e)
+    return ents
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_pack_json_ascii_fast_path(seed, monkeypatch):
+    """dk_pack_json's ASCII fast path (plain entities, no cleaners) gives the Python path's
+    values, keys, IDs and flags, and exactly the general path's columns (DK_INGEST_NOFAST)."""
+    rng = random.Random(200 + seed)
+    src = plain_source(group=None if seed % 2 == 0 else 1 + (seed // 2) % 2)
+    kfs = [dh.PartsKey(("NAME", -1, 0, 3), ("AREA", None, 0, 4)), dh.PartsKey(("NAME", 0, 0, 2),
+           ("UNSCORED", None, 5, 10)), dh.PartsKey(("NOTE", -2, -3, None)), dh.PartsKey(("RAW", 1, None, None))]
+    ents = [e for e in plain_entities(rng, 400) if e.get("extra", "") is not None]   # null: an error
+    body = json.dumps(ents, ensure_ascii=bool(seed % 2))
+    if seed == 3:
+        monkeypatch.setenv("DK_INGEST_THREADS", "4")
+    recs = dh.records_from_entities(dh.parse_entities(body)[0], src)
+    ns = I.NativeSource(src, PROPS, kfs)
+    packs = []
+    for nofast in (False, True):
+        if nofast:
+            monkeypatch.setenv("DK_INGEST_NOFAST", "1")
+        pk = ns.pack(body, I.Interner())
+        assert pk.n == len(recs)
+        for p in range(len(PROPS)):
+            assert pk.values(p) == [r.get_value(PROPS[p]) for r in recs], PROPS[p]
+        for k, kf in enumerate(kfs):
+            assert pk.keys(k) == [kf.make_key(r) for r in recs]
+        assert pk.ids() == [r.get_value("ID") for r in recs]
+        assert pk.entity_ids() == [r.get_value("dukeOriginalEntityId") for r in recs]
+        assert list(pk.deleted) == [r.get_value("dukeDeleted") == "true" for r in recs]
+        packs.append(pk)
+    a, b = packs
+    assert list(a.ident) == list(b.ident)
+    for p in range(len(PROPS)):
+        ca, cb = a.ptr.contents.columns[p], b.ptr.contents.columns[p]
+        assert ca.width == cb.width and bool(ca.present) == bool(cb.present)
+
+
 def C_u32(p):
     import ctypes as C
     return C.cast(p, C.POINTER(C.c_uint32))
@@ -154,8 +225,10 @@ def test_single_entity_body_and_duplicate_members():
     ('[{"_id": "1", "_deleted": null}]', A.DK_E_INVALID),
     ('[1, 2]', A.DK_E_INVALID),                           # entities must be objects
 ])
-def test_pack_json_errors(body, code):
-    ns = I.NativeSource(source(), PROPS, KEYS)
+@pytest.mark.parametrize("plain", [False, True])
+def test_pack_json_errors(body, code, plain):
+    # plain: a source without cleaners (its plain entities take the ASCII fast path)
+    ns = I.NativeSource(plain_source() if plain else source(), PROPS, KEYS)
     with pytest.raises(A.DukeHipError) as e:
         ns.pack(body, I.Interner())
     assert e.value.code == code
