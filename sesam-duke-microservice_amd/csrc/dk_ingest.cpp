@@ -66,9 +66,11 @@ struct Val {
 // a zero byte in x (the classic SWAR test)
 inline uint64_t zero_byte(uint64_t x) { return (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull; }
 // does the 8-byte word hold a '"', a '\\' or a byte below 0x20?
-inline bool word_special(uint64_t w) {
-  return (zero_byte(w ^ 0x2222222222222222ull) | zero_byte(w ^ 0x5C5C5C5C5C5C5C5Cull) |
-          ((w - 0x2020202020202020ull) & ~w & 0x8080808080808080ull)) != 0;
+// per byte: 0x80 where it is one of those; the lowest flagged byte is always a true one (a
+// borrow only propagates upwards, from a byte that is flagged itself)
+inline uint64_t special_bytes(uint64_t w) {
+  return zero_byte(w ^ 0x2222222222222222ull) | zero_byte(w ^ 0x5C5C5C5C5C5C5C5Cull) |
+         ((w - 0x2020202020202020ull) & ~w & 0x8080808080808080ull);
 }
 
 struct Reader {
@@ -93,26 +95,38 @@ struct Reader {
     if ((size_t)(e - p) < n || memcmp(p, w, n) != 0) fail(DK_E_UNSUPPORTED, "JSON: bad literal");
     p += n;
   }
+  bool esc = false;  // the last str() held a '\\'
   // string starting at '"': returns [a, b) of the raw content
   void str(const char** a, const char** b) {
     ++p;  // '"'
     *a = p;
-    // 8 bytes at a time while none is '"', '\\' or a control character
-    while (e - p >= 8) {
-      uint64_t w;
-      memcpy(&w, p, 8);
-      if (word_special(w)) break;
-      p += 8;
-    }
-    while (p < e && *p != '"') {
-      if ((unsigned char)*p < 0x20) fail(DK_E_UNSUPPORTED, "JSON: control character in a string");
-      if (*p == '\\') {
-        ++p;
-        if (p >= e) break;
+    esc = false;
+    for (;;) {
+      // 8 bytes at a time to the first '"', '\\' or control character (the lowest flagged
+      // byte of the SWAR masks is exact)
+      if (e - p >= 8) {
+        uint64_t w;
+        memcpy(&w, p, 8);
+        const uint64_t m = special_bytes(w);
+        if (!m) {
+          p += 8;
+          continue;
+        }
+        p += __builtin_ctzll(m) >> 3;
+      } else if (p >= e) {
+        fail(DK_E_UNSUPPORTED, "JSON: unterminated string");
       }
-      ++p;
+      const unsigned char c = (unsigned char)*p;
+      if (c == '"') break;
+      if (c < 0x20) fail(DK_E_UNSUPPORTED, "JSON: control character in a string");
+      if (c == '\\') {
+        esc = true;
+        p += 2;  // the escaped character (validated when decoded)
+        if (p > e) fail(DK_E_UNSUPPORTED, "JSON: unterminated string");
+        continue;
+      }
+      ++p;  // an ordinary byte of the tail (< 8 bytes left)
     }
-    if (p >= e) fail(DK_E_UNSUPPORTED, "JSON: unterminated string");
     *b = p;
     ++p;
   }
@@ -1141,6 +1155,7 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
           const char *ka, *kb2;
           if (R.peek() != '"') fail(DK_E_UNSUPPORTED, "JSON: expected a member name");
           R.str(&ka, &kb2);
+          const bool name_esc = R.esc;
           R.expect(':');
           Val v;
           R.value(v, 2);
@@ -1148,7 +1163,7 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
           const char* na = ka;
           size_t nn = (size_t)(kb2 - ka);
           std::string esc_name;
-          if (memchr(ka, '\\', nn)) {
+          if (name_esc) {
             mname.clear();
             decode_string(ka, kb2, mname);
             for (char16_t c : mname) {
@@ -1159,7 +1174,8 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
             nn = esc_name.size();
           }
           for (size_t i = 0; i < V.names.size(); ++i) {  // the first column of that name
-            if (V.names[i].size() == nn && memcmp(V.names[i].data(), na, nn) == 0) {
+            if (V.names[i].size() == nn && (nn == 0 || (V.names[i][0] == na[0] &&
+                                                        memcmp(V.names[i].data(), na, nn) == 0))) {
               got[i] = v;
               has[i] = 1;
               break;
