@@ -1416,6 +1416,7 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   std::vector<uint8_t> flags(n, 0);
   std::vector<uint32_t> dead;
   std::vector<std::pair<uint64_t, uint32_t>> undo;
+  if (!transient && !c->overwrite) undo.reserve(n);  // no regrowth copies (10M records: 160 MB)
   c->ident_row.plan(row0 + n);
   for (uint64_t i = 0; i < n && !transient; ++i) {
     flags[i] = kAlive | kIndexed | ((b->deleted && b->deleted[i]) ? kDeleted : 0);

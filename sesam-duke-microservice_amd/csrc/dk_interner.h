@@ -100,6 +100,20 @@ struct PodVec {
     p = q;
     cap = c;
   }
+  // reserve, the old contents copied by T threads (a 10M-ID arena is hundreds of MB)
+  void reserve_par(uint64_t c, int threads) {
+    if (c <= cap) return;
+    c = std::max<uint64_t>(c, 2 * cap);
+    T* q = alloc(c);
+    const uint64_t bytes = n * sizeof(T), parts = bytes >= (64u << 20) ? (uint64_t)std::max(1, threads) : 1;
+    dk_run_parts((int)parts, [&](int t) {
+      const uint64_t a = bytes * t / parts, b = bytes * (t + 1) / parts;
+      if (b > a) memcpy(reinterpret_cast<char*>(q) + a, reinterpret_cast<const char*>(p) + a, b - a);
+    });
+    free(p);
+    p = q;
+    cap = c;
+  }
   void resize_uninit(uint64_t m) {
     reserve(m);
     n = m;
@@ -127,6 +141,7 @@ struct PodVec {
 struct U16Table {
   static constexpr int kShardBits = 4, kShards = 1 << kShardBits;
   static constexpr uint32_t kProv = 0x80000000u;  // slot id field: batch index of a new string
+  static constexpr uint64_t kAhead = 8;            // slot prefetch distance of the batch probes
 
   PodVec<char16_t> arena;
   PodVec<uint64_t> start;          // id -> [start[id], start[id + 1]) in the arena
@@ -227,10 +242,19 @@ struct U16Table {
       }
     }
     shard_lo[kShards] = acc;
-    std::vector<uint32_t> order(cnt);
+    // order[k]: the batch index at shard-order position k; oh[k] its hash, so the probe
+    // passes read the hashes in sequence (prefetching the slots ahead) instead of gathering
+    PodVec<uint32_t> order;
+    PodVec<uint64_t> oh;
+    order.reset_uninit(cnt);
+    oh.reset_uninit(cnt);
     run(T, [&](int t) {
       uint64_t* b = base.data() + (size_t)t * kShards;
-      for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) order[b[shard_of(h[i])]++] = (uint32_t)i;
+      for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) {
+        const uint64_t k = b[shard_of(h[i])]++;
+        order[k] = (uint32_t)i;
+        oh[k] = h[i];
+      }
     });
     // room for the batch's new strings (load <= 1/2 per shard): bounded by the batch's count
     // per shard, or -- when that bound would grow the table -- by a read-only lookup pass
@@ -242,17 +266,22 @@ struct U16Table {
       known.assign(cnt, 0);
       std::vector<uint64_t> miss(kShards, 0);
       run(T, [&](int t) {
-        for (int s = t; s < kShards; s += T)
+        for (int s = t; s < kShards; s += T) {
+          const uint64_t* sh = slots.data() + (uint64_t)s * shard_cap;
+          uint64_t ms = 0;  // a local count: the shared array would bounce between workers
           for (uint64_t k = shard_lo[s]; k < shard_lo[s + 1]; ++k) {
+            if (k + kAhead < shard_lo[s + 1]) __builtin_prefetch(sh + (oh[k + kAhead] & (shard_cap - 1)));
             const uint32_t i = order[k];
             uint64_t id;
-            if (find(ptr[i], n[i], h[i], &id)) {
+            if (find(ptr[i], n[i], oh[k], &id)) {
               out[i] = id;
               known[k] = 1;
             } else {
-              ++miss[s];
+              ++ms;
             }
           }
+          miss[s] = ms;
+        }
       });
       need = 0;
       for (int s = 0; s < kShards; ++s) need = std::max(need, fill[s] + miss[s]);
@@ -261,32 +290,38 @@ struct U16Table {
     // Every allocation happens before the first provisional slot is written (the workers
     // and the numbering pass below allocate nothing): a std::bad_alloc leaves the table as
     // it was.  Worst case: every string of the batch is new.
-    std::vector<std::vector<uint64_t>> placed(kShards);  // slot positions of new strings
+    // slot positions of new strings: shard s's at placed[shard_lo[s] ..], placed_n[s] of them
+    // (the workers keep their counts local: adjacent shared counters would bounce)
+    PodVec<uint64_t> placed;
+    placed.reset_uninit(cnt);
+    std::vector<uint64_t> placed_n(kShards, 0);
     uint64_t units_max = 0;
-    for (int s = 0; s < kShards; ++s) placed[s].reserve(shard_lo[s + 1] - shard_lo[s]);
     for (uint64_t i = 0; i < cnt; ++i) units_max += n[i];
-    arena.reserve(arena.size() + units_max);
-    start.reserve(start.size() + cnt);
-    hashes.reserve(hashes.size() + cnt);
+    arena.reserve_par(arena.size() + units_max, T);
+    start.reserve_par(start.size() + cnt, T);
+    hashes.reserve_par(hashes.size() + cnt, T);
     std::vector<uint32_t> fresh;
     fresh.reserve(cnt);
+    std::vector<uint64_t> rfresh(T + 1, 0), runits(T + 1, 0);  // the numbering's range prefixes
     // per shard, in batch order: existing id, or provisional (kProv | first index)
     run(T, [&](int t) {
       for (int s = t; s < kShards; s += T) {
         uint64_t* sh = slots.data() + (uint64_t)s * shard_cap;
-        const uint64_t m = shard_cap - 1;
-        for (uint64_t k = shard_lo[s]; k < shard_lo[s + 1]; ++k) {
+        const uint64_t m = shard_cap - 1, k1 = shard_lo[s + 1];
+        uint64_t* pl = placed.data() + shard_lo[s];
+        uint64_t npl = 0;
+        for (uint64_t k = shard_lo[s]; k < k1; ++k) {
+          if (k + kAhead < k1) __builtin_prefetch(sh + (oh[k + kAhead] & m), 1);
           if (!known.empty() && known[k]) continue;
           const uint32_t i = order[k];
-          const uint64_t hh = h[i], tag = hh >> 32;
+          const uint64_t hh = oh[k], tag = hh >> 32;
           uint64_t pos = hh & m;
           for (;; pos = (pos + 1) & m) {
             const uint64_t e = sh[pos];
             if (!e) {
               sh[pos] = (tag << 32) | (kProv | i);
-              placed[s].push_back(pos);
+              pl[npl++] = pos;
               out[i] = kProv | (uint64_t)i;
-              ++fill[s];
               break;
             }
             if ((e >> 32) != tag) continue;
@@ -306,23 +341,42 @@ struct U16Table {
             }
           }
         }
+        placed_n[s] = npl;
+        fill[s] += npl;
       }
     });
-    // number the new strings in first-appearance order
+    // number the new strings in first-appearance order: per batch range, its first
+    // appearances counted, then numbered from the range's prefix, then the repeats copy
+    // their first appearance's id (final by then)
     const uint64_t id0 = size();
-    uint64_t nid = id0, units = 0;
-    for (uint64_t i = 0; i < cnt; ++i) {
-      const uint64_t v = out[i];
-      if (!(v & kProv)) continue;
-      const uint64_t j = v & ~(uint64_t)kProv;
-      if (j == i) {
-        out[i] = nid++;
-        fresh.push_back((uint32_t)i);
-        units += n[i];
-      } else {
-        out[i] = out[j];
-      }
+    run(T, [&](int t) {
+      uint64_t f = 0, u = 0;
+      for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i)
+        if (out[i] == (kProv | i)) {
+          ++f;
+          u += n[i];
+        }
+      rfresh[t + 1] = f;
+      runits[t + 1] = u;
+    });
+    for (int t = 0; t < T; ++t) {
+      rfresh[t + 1] += rfresh[t];
+      runits[t + 1] += runits[t];
     }
+    const uint64_t units = runits[T];
+    fresh.resize(rfresh[T]);
+    run(T, [&](int t) {
+      uint64_t f = rfresh[t];
+      for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i)
+        if (out[i] == (kProv | i)) {
+          out[i] = id0 + f;
+          fresh[f++] = (uint32_t)i;
+        }
+    });
+    run(T, [&](int t) {
+      for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i)
+        if (out[i] & kProv) out[i] = out[out[i] & ~(uint64_t)kProv];
+    });
     // slots, ids -> strings, arena
     const uint64_t a0 = arena.size();
     arena.resize_uninit(a0 + units);
@@ -336,7 +390,10 @@ struct U16Table {
     run(T, [&](int t) {
       for (int s = t; s < kShards; s += T) {
         uint64_t* sh = slots.data() + (uint64_t)s * shard_cap;
-        for (uint64_t pos : placed[s]) {
+        const uint64_t* pl = placed.data() + shard_lo[s];
+        for (uint64_t q = 0; q < placed_n[s]; ++q) {
+          if (q + kAhead < placed_n[s]) __builtin_prefetch(sh + pl[q + kAhead], 1);
+          const uint64_t pos = pl[q];
           const uint32_t i = (uint32_t)sh[pos] & ~kProv;
           sh[pos] = (sh[pos] & ~0xFFFFFFFFull) | (out[i] + 1);
         }
@@ -373,11 +430,13 @@ struct U16Table {
     ++fill[s];
   }
   void ensure_shard(int, uint64_t n) { ensure_all(n, 1); }
-  // every shard holds n entries at load <= 1/2 (all shards share one capacity)
+  // every shard holds n entries at load <= 1/2 (all shards share one capacity); a growth
+  // leaves load <= 1/4, so a next batch as large as this one neither rehashes nor needs the
+  // lookup pass (a cold database taking two 10M-record bodies rehashed 10M IDs otherwise)
   void ensure_all(uint64_t n, int T) {
     if (shard_cap && 2 * n <= shard_cap) return;
     uint64_t cap = shard_cap ? shard_cap : 64;
-    while (cap < 2 * n) cap *= 2;
+    while (cap < 4 * n) cap *= 2;
     slots.reset_uninit((uint64_t)kShards * cap);
     shard_cap = cap;
     std::fill(fill, fill + kShards, 0);
