@@ -541,8 +541,9 @@ inline bool has_quote_or_bs(uint64_t w) {
 }
 
 struct Split {
-  std::vector<std::pair<uint64_t, uint64_t>> spans;  // [first byte '{', one past '}')
-  int code = DK_OK;                                    // a structural error after the spans
+  PodVec<uint64_t> starts, ends;  // entity k: [starts[k] ('{'), ends[k] (one past '}'))
+  uint64_t n = 0;                 // entities (the arrays may hold one more start)
+  int code = DK_OK;               // a structural error after the spans
   std::string msg;
 };
 
@@ -822,7 +823,9 @@ void split_entities(const char* J, uint64_t len, Split& S) {
       S.msg = "entity 0 is not a JSON object";
       return;
     }
-    S.spans.emplace_back(p, len);
+    S.starts.push_back(p);
+    S.ends.push_back(len);
+    S.n = 1;
     return;
   }
   const uint64_t lo = p + 1;
@@ -880,10 +883,14 @@ void split_entities(const char* J, uint64_t len, Split& S) {
     so[t + 1] = so[t] + CS[t].starts.size();
     eo[t + 1] = eo[t] + CS[t].ends.size();
   }
-  std::vector<uint64_t> starts(so[tl + 1]), ends(eo[tl + 1]);
+  // uninitialised: each chunk's worker writes (and first-touches) its part
+  PodVec<uint64_t>& starts = S.starts;
+  PodVec<uint64_t>& ends = S.ends;
+  starts.reset_uninit(so[tl + 1]);
+  ends.reset_uninit(eo[tl + 1]);
   parallel_for(tl + 1, [&](int t) {
-    std::copy(CS[t].starts.begin(), CS[t].starts.end(), starts.begin() + so[t]);
-    std::copy(CS[t].ends.begin(), CS[t].ends.end(), ends.begin() + eo[t]);
+    if (!CS[t].starts.empty()) memcpy(starts.data() + so[t], CS[t].starts.data(), CS[t].starts.size() * 8);
+    if (!CS[t].ends.empty()) memcpy(ends.data() + eo[t], CS[t].ends.data(), CS[t].ends.size() * 8);
   });
   lap("concat");
   const uint64_t ns = starts.size(), ne = ends.size();  // ne == ns or ns - 1
@@ -900,11 +907,7 @@ void split_entities(const char* J, uint64_t len, Split& S) {
   uint64_t kbad = UINT64_MAX;
   for (int t = 0; t < T && kbad == UINT64_MAX; ++t) kbad = first_bad[t];
   const uint64_t nspans = kbad != UINT64_MAX ? kbad : ne;
-  S.spans.resize(nspans);
-  parallel_for(T, [&](int t) {
-    const uint64_t k0 = nspans * (uint64_t)t / (uint64_t)T, k1 = nspans * (uint64_t)(t + 1) / (uint64_t)T;
-    for (uint64_t k = k0; k < k1; ++k) S.spans[k] = {starts[k], ends[k]};
-  });
+  S.n = nspans;
   if (kbad != UINT64_MAX) {  // entity kbad follows a malformed gap
     element_check(classify_gap(J, kbad ? ends[kbad - 1] : lo, starts[kbad]), kbad, kEntity, S);
     return;
@@ -1113,7 +1116,7 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
   // a value is at most as long as its JSON text: the slice's bytes bound every property
   // column's units, so those buffers never grow and copy (reserved, untouched pages cost
   // nothing); keys and IDs grow geometrically from a per-record guess
-  const uint64_t bytes = n ? S.spans[out.e1 - 1].second - S.spans[out.e0].first : 0;
+  const uint64_t bytes = n ? S.ends[out.e1 - 1] - S.starts[out.e0] : 0;
   for (int c = 0; c < np + nk + 2; ++c)
     out.cols[c].init(n, c < np ? bytes + 64 : 16 * n + 64, c == np + nk);
   out.deleted.reserve(n);
@@ -1141,7 +1144,7 @@ void parse_slice(const SourceView& V, const char* J, const Split& S, Slice& out)
   uint64_t r = out.e0;
   try {
     for (; r < out.e1; ++r) {
-      Reader R{J + S.spans[r].first, J + S.spans[r].second, &side};
+      Reader R{J + S.starts[r], J + S.ends[r], &side};
       // one entity: its members in one pass (a repeated name: the last wins, as Gson's
       // JsonObject keeps it); nested containers are skipped
       side.clear();
@@ -1440,7 +1443,7 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
     Split S;
     split_entities(json, len, S);
     clear_upper();
-    const uint64_t n = S.spans.size();
+    const uint64_t n = S.n;
     lap("split");
     // 2. entity slices, parsed in parallel
     const int T = pack_threads(n, 4096);
