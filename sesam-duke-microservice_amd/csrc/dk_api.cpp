@@ -96,6 +96,11 @@ struct IdentMap {
     const auto it = sparse.find(id);
     return it == sparse.end() ? kNoRow : it->second;
   }
+  // the dense table grown once to cover identity id (a batch's largest), as set() would
+  void reserve_dense(uint64_t id) {
+    if (id >= dense.size() && id < dense_limit)
+      dense.resize(std::min<uint64_t>(dense_limit, std::max<uint64_t>(id + 1, 2 * dense.size())), kNoRow);
+  }
   void set(uint64_t id, uint32_t row) {
     if (id >= dense.size() && id < dense_limit && row != kNoRow)
       dense.resize(std::min<uint64_t>(dense_limit, std::max<uint64_t>(id + 1, 2 * dense.size())), kNoRow);
@@ -1418,6 +1423,11 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   std::vector<std::pair<uint64_t, uint32_t>> undo;
   if (!transient && !c->overwrite) undo.reserve(n);  // no regrowth copies (10M records: 160 MB)
   c->ident_row.plan(row0 + n);
+  if (!transient && !c->overwrite) {  // the dense ID table grown once, not doubled in the loop
+    uint64_t mx = 0;
+    for (uint64_t i = 0; i < n; ++i) mx = std::max(mx, b->ident[i]);
+    c->ident_row.reserve_dense(mx);
+  }
   for (uint64_t i = 0; i < n && !transient; ++i) {
     flags[i] = kAlive | kIndexed | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
     if (c->overwrite) continue;
