@@ -1232,7 +1232,7 @@ static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, uint64_t* k
   h.reset_uninit(n);
   if (kc.width == 1) wide.reset_uninit(tot);
   const uint8_t* u8 = (const uint8_t*)kc.units + base;
-  parallel_ranges(n, n >= (1u << 16) ? 4 : 1, [&](uint64_t lo, uint64_t hi) {
+  parallel_ranges(n, n >= (1u << 16) ? 8 : 1, [&](uint64_t lo, uint64_t hi) {
     for (uint64_t i = lo; i < hi; ++i) {
       const uint64_t a = kc.offsets[i] - base, e = kc.offsets[i + 1] - base;
       if (kc.width == 1) {
@@ -1254,7 +1254,7 @@ static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, uint64_t* k
     ptr[i] = units + (kc.offsets[i] - base);
     ln[i] = kc.offsets[i + 1] - kc.offsets[i];
   }
-  tab.intern_batch(n, ptr.data(), ln.data(), h.data(), dst, n >= (1u << 16) ? 4 : 1);
+  tab.intern_batch(n, ptr.data(), ln.data(), h.data(), dst, n >= (1u << 16) ? 8 : 1);
   return DK_OK;
 }
 

@@ -605,7 +605,7 @@ void for_brackets(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr,
 // prefix XOR of the unescaped quotes (one PCLMULQDQ by all-ones), carried as a sign mask.
 // The same state machine as quote_parity / for_brackets, 64 bytes per step.
 struct BlockMasks {
-  uint64_t quote, bs, open, close;
+  uint64_t quote, bs, open, close, square;  // square: '[' or ']'
 };
 
 __attribute__((target("avx2"))) inline BlockMasks block_masks(const char* p) {
@@ -614,7 +614,8 @@ __attribute__((target("avx2"))) inline BlockMasks block_masks(const char* p) {
 #define DK_EQ64(c)                                                                               \
   ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(a, _mm256_set1_epi8(c))) |          \
    ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(b, _mm256_set1_epi8(c))) << 32))
-  const BlockMasks m{DK_EQ64('"'), DK_EQ64('\\'), DK_EQ64('{') | DK_EQ64('['), DK_EQ64('}') | DK_EQ64(']')};
+  const uint64_t sqo = DK_EQ64('['), sqc = DK_EQ64(']');
+  const BlockMasks m{DK_EQ64('"'), DK_EQ64('\\'), DK_EQ64('{') | sqo, DK_EQ64('}') | sqc, sqo | sqc};
 #undef DK_EQ64
   return m;
 }
@@ -681,21 +682,28 @@ __attribute__((target("avx2,pclmul"))) uint32_t quote_parity_simd(const char* J,
   return q;
 }
 
-// the positions of the brackets outside strings in [c0, c1), in order
-__attribute__((target("avx2,pclmul"))) void brackets_simd(const char* J, uint64_t c0, uint64_t c1, bool esc,
-                                                         bool instr, std::vector<uint64_t>& out) {
+// the brackets outside strings in [c0, c1), in order, as position | kCloser | kSquare (the
+// depth walk then never re-reads the body), and their depth change
+constexpr uint64_t kCloser = 1ull << 63, kSquare = 1ull << 62, kPosMask = kSquare - 1;
+__attribute__((target("avx2,pclmul"))) int64_t brackets_simd(const char* J, uint64_t c0, uint64_t c1, bool esc,
+                                                            bool instr, std::vector<uint64_t>& out) {
   uint64_t carry = esc ? 1u : 0u;
   uint64_t inmask = instr ? ~0ull : 0ull;  // in a string at the block's start: all ones
+  int64_t d = 0;
   for_blocks(J, c0, c1, [&](uint64_t base, const BlockMasks& m) {
     const uint64_t e = escaped_bits(m.bs, &carry);
     const uint64_t s = prefix_xor(m.quote & ~e) ^ inmask;
     inmask = (uint64_t)((int64_t)s >> 63);
-    uint64_t br = (m.open | m.close) & ~s;
+    const uint64_t op = m.open & ~s, cl = m.close & ~s;
+    d += __builtin_popcountll(op) - __builtin_popcountll(cl);
+    uint64_t br = op | cl;
     while (br) {
-      out.push_back(base + (uint64_t)__builtin_ctzll(br));
+      const int b = __builtin_ctzll(br);
+      out.push_back((base + (uint64_t)b) | ((cl >> b & 1) ? kCloser : 0) | ((m.square >> b & 1) ? kSquare : 0));
       br &= br - 1;
     }
   });
+  return d;
 }
 
 // One chunk of the top-level array, its depth at the start known: entity starts ('{' at
@@ -738,12 +746,14 @@ void scan_chunk(const char* J, uint64_t c0, uint64_t c1, bool esc, bool instr, i
   walk_chunk([&](auto&& f) { for_brackets(J, c0, c1, esc, instr, f); }, depth, C);
 }
 
-// the same over a chunk's bracket positions found by brackets_simd
-void scan_chunk_list(const char* J, const std::vector<uint64_t>& br, int64_t depth, ChunkScan& C) {
+// the same over a chunk's brackets found by brackets_simd (their kinds in the flag bits)
+void scan_chunk_list(const std::vector<uint64_t>& br, int64_t depth, ChunkScan& C) {
   walk_chunk(
       [&](auto&& f) {
-        for (uint64_t pos : br)
-          if (!f(pos, J[pos])) return;
+        for (uint64_t x : br) {
+          const char ch = (x & kCloser) ? ((x & kSquare) ? ']' : '}') : ((x & kSquare) ? '[' : '{');
+          if (!f(x & kPosMask, ch)) return;
+        }
       },
       depth, C);
 }
@@ -853,8 +863,7 @@ void split_entities(const char* J, uint64_t len, Split& S) {
     int64_t d = 0;
     if (simd) {  // one pass: the positions (the depth walk reads their characters later)
       BR[t].reserve((cut[t + 1] - cut[t]) / 32 + 16);
-      brackets_simd(J, cut[t], cut[t + 1], esc0[t], instr[t], BR[t]);
-      for (uint64_t pos : BR[t]) d += (J[pos] == '{' || J[pos] == '[') ? 1 : -1;
+      d = brackets_simd(J, cut[t], cut[t + 1], esc0[t], instr[t], BR[t]);
     } else {
       for_brackets(J, cut[t], cut[t + 1], esc0[t], instr[t], [&](uint64_t, char ch) {
         d += (ch == '{' || ch == '[') ? 1 : -1;
@@ -867,7 +876,7 @@ void split_entities(const char* J, uint64_t len, Split& S) {
   for (int t = 0; t < T; ++t) d0[t] = t ? d0[t - 1] + delta[t - 1] : 1;
   parallel_for(T, [&](int t) {
     if (d0[t] <= 0) return;
-    if (simd) scan_chunk_list(J, BR[t], d0[t], CS[t]);
+    if (simd) scan_chunk_list(BR[t], d0[t], CS[t]);
     else scan_chunk(J, cut[t], cut[t + 1], esc0[t], instr[t], d0[t], CS[t]);
   });
   lap("walk");

@@ -246,14 +246,17 @@ struct U16Table {
     // passes read the hashes in sequence (prefetching the slots ahead) instead of gathering
     PodVec<uint32_t> order;
     PodVec<uint64_t> oh;
+    PodVec<const char16_t*> op;  // and its string (prefetched ahead: a hit compares it)
     order.reset_uninit(cnt);
     oh.reset_uninit(cnt);
+    op.reset_uninit(cnt);
     run(T, [&](int t) {
       uint64_t* b = base.data() + (size_t)t * kShards;
       for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) {
         const uint64_t k = b[shard_of(h[i])]++;
         order[k] = (uint32_t)i;
         oh[k] = h[i];
+        op[k] = ptr[i];
       }
     });
     // room for the batch's new strings (load <= 1/2 per shard): bounded by the batch's count
@@ -270,10 +273,13 @@ struct U16Table {
           const uint64_t* sh = slots.data() + (uint64_t)s * shard_cap;
           uint64_t ms = 0;  // a local count: the shared array would bounce between workers
           for (uint64_t k = shard_lo[s]; k < shard_lo[s + 1]; ++k) {
-            if (k + kAhead < shard_lo[s + 1]) __builtin_prefetch(sh + (oh[k + kAhead] & (shard_cap - 1)));
+            if (k + kAhead < shard_lo[s + 1]) {
+              __builtin_prefetch(sh + (oh[k + kAhead] & (shard_cap - 1)));
+              __builtin_prefetch(op[k + kAhead]);
+            }
             const uint32_t i = order[k];
             uint64_t id;
-            if (find(ptr[i], n[i], oh[k], &id)) {
+            if (find(op[k], n[i], oh[k], &id)) {
               out[i] = id;
               known[k] = 1;
             } else {
@@ -311,7 +317,10 @@ struct U16Table {
         uint64_t* pl = placed.data() + shard_lo[s];
         uint64_t npl = 0;
         for (uint64_t k = shard_lo[s]; k < k1; ++k) {
-          if (k + kAhead < k1) __builtin_prefetch(sh + (oh[k + kAhead] & m), 1);
+          if (k + kAhead < k1) {
+            __builtin_prefetch(sh + (oh[k + kAhead] & m), 1);
+            __builtin_prefetch(op[k + kAhead]);
+          }
           if (!known.empty() && known[k]) continue;
           const uint32_t i = order[k];
           const uint64_t hh = oh[k], tag = hh >> 32;
