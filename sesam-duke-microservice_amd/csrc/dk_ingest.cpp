@@ -1506,6 +1506,9 @@ int dk_pack_json(const dk_source* src, const char* json, uint64_t len, dk_intern
       ids->intern_batch(n, ptr.data(), ln.data(), hs.data(), P->ident.data(), pack_threads(n, 4096));
     }
     lap("intern");
+    std::vector<Slice>().swap(sl);  // the scratch goes now (timed), not at the scope's end
+    S = Split();
+    lap("free");
     P->pub.n = n;
     P->pub.columns = P->cols.data();
     P->pub.key_columns = P->keys.data();
