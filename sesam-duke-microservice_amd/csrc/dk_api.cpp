@@ -145,15 +145,20 @@ static int run_tasks(int n, bool parallel, F&& task) {
   return DK_OK;
 }
 
-// DK_HOST_TIMING=1: host phase times of dk_upsert on stderr (diagnostics)
+// DK_HOST_TIMING=1: host phase times of dk_upsert / dk_match on stderr (diagnostics; with a
+// stream, each lap first waits for it, so device work lands in the lap that queued it)
 struct HostLap {
   bool on;
+  const char* who;
+  hipStream_t s;
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-  HostLap() : on(getenv("DK_HOST_TIMING") != nullptr) {}
+  explicit HostLap(const char* w = "dk_upsert", hipStream_t st = nullptr)
+      : on(getenv("DK_HOST_TIMING") != nullptr), who(w), s(st) {}
   void operator()(const char* what) {
     if (!on) return;
+    if (s) (void)hipStreamSynchronize(s);
     const auto t1 = std::chrono::steady_clock::now();
-    fprintf(stderr, "dk_upsert %s %.2f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+    fprintf(stderr, "%s %s %.2f ms\n", who, what, std::chrono::duration<double, std::milli>(t1 - t0).count());
     t0 = t1;
   }
 };
@@ -1985,11 +1990,13 @@ static uint64_t delta_capacity(uint64_t m) {
 // replica, no tables).
 static int build_full(dk_ctx* c, BlockTables& T, uint64_t* Mout) {
   hipStream_t s = c->stream;
+  HostLap lap("dk_match build", s);
   const int nk = c->schema.nkeys;
   const bool allpairs = c->schema.mode == DK_MODE_ALLPAIRS;
   uint64_t M = 0;
   int rc = build_usable(c, 0, c->nrows, &M);
   if (rc) return rc;
+  lap("usable");
   c->base_ok = false;
   c->base_dead.clear();
   if (allpairs) {
@@ -2015,6 +2022,7 @@ static int build_full(dk_ctx* c, BlockTables& T, uint64_t* Mout) {
     rc = sort_segment(c, T, k, k, k, (uint64_t)k * kstride, M);
     if (rc) return rc;
   }
+  lap("sort");
   T.rowof = c->rowof.as<uint32_t>();
   c->rowof_p = T.rowof;
   c->rstride = npos;
@@ -2023,12 +2031,14 @@ static int build_full(dk_ctx* c, BlockTables& T, uint64_t* Mout) {
   HIPCHK(c->rident.reserve(npos * 8 + 8, 0, s));
   for (int k = 0; k + 1 < nk; ++k) HIPCHK(c->rkeys[k].reserve(npos * 8 + 8, 0, s));
   T.rident = c->rident.as<uint64_t>();
+  lap("layout");
   for (int k = 0; k < nk; ++k) {
     rc = fill_replica(c, c->rep, T.rowof, T.seg_off[k], M);
     if (rc) return rc;
     rc = fill_rows(c, T, T.seg_off[k], M);
     if (rc) return rc;
   }
+  lap("fill");
   c->base_ok = dcap > 0;
   c->base_rows = rb;
   c->base_m = M;
@@ -2732,12 +2742,14 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
 
   // ---- index: usable rows + per key function sort by (key, group, row) ----
+  HostLap lap("dk_match", s);
   Timer t_index(c, &c->prof.ms_index, s);
   uint64_t M = 0;
   BlockTables T{};
   int rc = ensure_tables(c, &T, &M);
   if (rc) return rc;
   t_index.stop();
+  lap("index");
 
   // ---- candidate counts per query -> slot offsets ----
   Timer t_gen(c, &c->prof.ms_generate, s);
@@ -2897,6 +2909,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     }
   }
   t_gen.stop();
+  lap("generate");
 
   uint64_t chunk = 1;
   for (size_t i = 0; i + 1 < bounds.size(); ++i) chunk = std::max(chunk, bounds[i + 1] - bounds[i]);
@@ -3207,6 +3220,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     const int rg = geo_raise_check(c, P);
     if (rg) return rg;
   }
+  lap("score+emit");
   const uint64_t scored = c->h_small.as<uint64_t>()[0];
   const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
   if (sym) c->prof.sym_matches += 1;
