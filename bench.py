@@ -758,10 +758,14 @@ def json_batch(w, n, queries, device, torch):
             rows = np.concatenate([eng.upsert_packed(pk) for pk in pks])
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-            res = eng.match(rows[queries], on_device=True)   # the batch's new rows
+            qrows = rows[queries]
+            t2a = time.perf_counter()
+            res = eng.match(qrows, on_device=True)   # the batch's new rows
+            t2b = time.perf_counter()
             torch.cuda.synchronize()
             t3 = time.perf_counter()
             out[leg] = {"pack_s": t1 - t0, "upsert_s": t2 - t1, "match_s": t3 - t2,
+                        "match_parts_s": {"query_rows": t2a - t2, "dk_match": t2b - t2a, "sync": t3 - t2b},
                         "pairs_scored": int(res.pairs_scored),
                         "records_per_s": len(queries) / (t3 - t0),
                         "posted_records_per_s": total / (t3 - t0)}

@@ -2743,6 +2743,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
 
   // ---- index: usable rows + per key function sort by (key, group, row) ----
   HostLap lap("dk_match", s);
+  lap("queries");
   Timer t_index(c, &c->prof.ms_index, s);
   uint64_t M = 0;
   BlockTables T{};
@@ -3271,6 +3272,7 @@ static int match_impl(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fl
   if (!c->members.empty()) return group_match(c, query_rows, nq, flags, out);
   if (nq && !query_rows) return fail(DK_E_INVALID, "query_rows is NULL");
   if (flags & ~DK_MATCH_DEVICE) return fail(DK_E_INVALID, "unknown flags 0x%x", flags);
+  HostLap lap("dk_match call");
   bool contiguous = true;  // query rows r0, r0+1, ... (Processor.deduplicate's batch)
   for (uint64_t i = 0; i < nq; ++i) {
     if (query_rows[i] >= c->nrows)
@@ -3289,7 +3291,9 @@ static int match_impl(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fl
   R->bufs = c->pool->take();
   R->device = c->device;
   R->stream = c->stream;
+  lap("validate");
   int rc = run_match(c, query_rows, nq, flags, R, contiguous);
+  lap("run");
   if (rc) {
     R->pool->give(std::move(R->bufs));
     delete R;
