@@ -2822,7 +2822,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     if (need > fr / 3) sym = false;
   }
   if (sym) {
-    HIPCHK(c->ores.reserve(otot * 8 + 64, 0, s));
     HIPCHK(c->mres.reserve(mtot * 8 + 64, 0, s));
     HIPCHK(c->mbase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
     HIPCHK(hipMemsetAsync(c->mres.p, 0xFF, mtot * 8, s));  // all-ones: a NaN (no entry)
@@ -2932,9 +2931,13 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
                      G.qidx.as<uint32_t>()};
   }
   StageOut so{};  // SYM: the owner phase's block counters (it stages no entries)
+  uint64_t ochunk = 1;  // SYM: the largest chunk's owner slots
   if (sym) {
-    uint64_t ochunk = 1;
     for (size_t i = 0; i + 1 < obounds.size(); ++i) ochunk = std::max(ochunk, obounds[i + 1] - obounds[i]);
+    // owner results live for one chunk (its emission reads only its own queries' owner
+    // slots; what crosses chunks is the mirror results): two chunk-sized halves, chunk ci
+    // in half ci & 1, instead of 8 B per owner slot of the whole call
+    HIPCHK(c->ores.reserve(2 * ochunk * 8 + 64, 0, s));
     const uint64_t onblk = (ochunk + kScoreBlock - 1) / kScoreBlock;
     dk_ctx::StageBufs& G = c->owner_stage;
     HIPCHK(G.bcnt.reserve(onblk * 4 + 4, 0, s));
@@ -2974,7 +2977,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     src.wq = c->owq.as<uint32_t>();
     src.qoff = c->oqoff.as<uint64_t>();
     src.sranges = c->ranges.as<uint4>();
-    src.ores = c->ores.as<double>();
     src.mres = c->mres.as<double>();
     src.mbase = c->mbase.as<uint64_t>();
     src.r0 = r0;
@@ -2983,7 +2985,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     esrc.qoff = c->qoff.as<uint64_t>();
     esrc.sranges = c->ranges.as<uint4>();
     esrc.obase = c->obase.as<uint64_t>();
-    esrc.ores = c->ores.as<double>();
     esrc.mres = c->mres.as<double>();
     esrc.mbase = c->mbase.as<uint64_t>();
     esrc.rowof = c->rowof.as<uint32_t>();
@@ -3144,6 +3145,13 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       // kernel time, 26.45 vs 26.50 ms per configs[1] step -- VALU-bound, not L2 -- plus the
       // sort), else launch order
       PairSource osrc = src;
+      // chunk ci's owner results in half b, indexed by the absolute owner slot o0..o1-1
+      double* const oh = reinterpret_cast<double*>(
+          reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - o0 * sizeof(double));
+      osrc.ores = oh;
+      esrc.ores = oh;
+      // half b was last read by chunk ci-2's emission: on its own stream, wait for it
+      if (es != s && ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->count_ready[b], 0));
       static const bool sym_sort = getenv("DK_SYM_SORT") && getenv("DK_SYM_SORT")[0] == '1';
       const uint64_t onb = (o1 - o0 + kScoreBlock - 1) / kScoreBlock;
       if (sym_sort && onb > 1) {
