@@ -1569,9 +1569,12 @@ __global__ __launch_bounds__(256) void k_reduce_blocks(const StageOut st, uint64
 }
 
 // Concatenate the per-block staged entries in block order.  A wave takes kCompactRun
-// consecutive staging blocks at a time: their counts in one read, then only the non-empty
-// blocks' entries, 64 per step (a launch of one workgroup per staging block spent most of
-// its time dispatching workgroups with nothing to copy: sparse match lists, configs[2]).
+// consecutive staging blocks at a time: their counts in one read, then the run's entries as
+// ONE sequence, 64 per step (entry i of the run: the block whose inclusive count prefix first
+// exceeds i), so a step's lanes are full across block boundaries -- configs[1] stages ~70
+// entries per block, which a step per block left half idle -- and the run's destination is
+// contiguous.  (One workgroup per staging block spent most of its time dispatching
+// workgroups with nothing to copy: sparse match lists, configs[2].)
 constexpr int kCompactRun = 16;
 
 __global__ __launch_bounds__(256) void k_compact(const StageOut st, const uint64_t* __restrict__ boff,
@@ -1582,20 +1585,32 @@ __global__ __launch_bounds__(256) void k_compact(const StageOut st, const uint64
   for (uint64_t b0 = wave * kCompactRun; b0 < nblocks; b0 += nwaves * kCompactRun) {
     const uint64_t b = b0 + lane;
     const uint32_t n = lane < (uint32_t)kCompactRun && b < nblocks ? st.bcnt[b] : 0u;
-    uint64_t m = __ballot(n != 0u);
-    while (m) {  // wave-uniform
-      const int l = __builtin_ctzll(m);
-      m &= m - 1ull;
-      const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane((int)n, l);
-      const uint64_t src0 = (b0 + (uint64_t)l) * kScoreBlock;
-      const uint64_t dst0 = base + boff[b0 + (uint64_t)l];
-      for (uint32_t i = lane; i < cnt; i += 64) {
-        const uint32_t w = st.cand[src0 + i];
-        out.cand[dst0 + i] = w & ((1u << kKindShift) - 1u);
-        out.kind[dst0 + i] = (uint8_t)(w >> kKindShift);
-        out.prob[dst0 + i] = st.prob[src0 + i];
-        out.qidx[dst0 + i] = st.qidx[src0 + i];
-      }
+    uint32_t incl = n;  // inclusive prefix over the run's blocks (lanes past them add 0)
+#pragma unroll
+    for (int o = 1; o < kCompactRun; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, (unsigned)o);
+      if (lane >= (uint32_t)o) incl += y;
+    }
+    uint32_t pre[kCompactRun];  // wave-uniform
+#pragma unroll
+    for (int k = 0; k < kCompactRun; ++k) pre[k] = (uint32_t)__builtin_amdgcn_readlane((int)incl, k);
+    const uint32_t total = pre[kCompactRun - 1];
+    if (total == 0u) continue;  // wave-uniform
+    const uint64_t dst0 = base + boff[b0];  // the run's first entry (boff: exclusive prefix)
+    for (uint32_t i = lane; i < total; i += 64) {
+      uint32_t j = 0, start = 0;  // block of entry i within the run, its first entry
+#pragma unroll
+      for (int k = 0; k < kCompactRun - 1; ++k)
+        if (pre[k] <= i) {
+          j = (uint32_t)k + 1u;
+          start = pre[k];
+        }
+      const uint64_t src = (b0 + j) * kScoreBlock + (i - start);
+      const uint32_t w = st.cand[src];
+      out.cand[dst0 + i] = w & ((1u << kKindShift) - 1u);
+      out.kind[dst0 + i] = (uint8_t)(w >> kKindShift);
+      out.prob[dst0 + i] = st.prob[src];
+      out.qidx[dst0 + i] = st.qidx[src];
     }
   }
 }
