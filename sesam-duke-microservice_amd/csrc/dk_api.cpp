@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -1428,12 +1429,61 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
   std::vector<std::pair<uint64_t, uint32_t>> undo;
   if (!transient && !c->overwrite) undo.reserve(n);  // no regrowth copies (10M records: 160 MB)
   c->ident_row.plan(row0 + n);
+  IdentMap& IM = c->ident_row;
+  bool par = false;  // the batch's identities resolved on parallel ranges (below)
   if (!transient && !c->overwrite) {  // the dense ID table grown once, not doubled in the loop
     uint64_t mx = 0;
     for (uint64_t i = 0; i < n; ++i) mx = std::max(mx, b->ident[i]);
-    c->ident_row.reserve_dense(mx);
+    IM.reserve_dense(mx);
+    par = n >= (1u << 16) && IM.sparse.empty() && mx < IM.dense.size();
   }
-  for (uint64_t i = 0; i < n && !transient; ++i) {
+  if (par) {
+    // Every identity dense and the sparse map empty: (1) each identity's row before the
+    // batch, (2) the batch's rows written, (3) a repeated identity (some copy's row lost) ->
+    // phase 2 undone and the serial loop below; otherwise flags, tombstones and the undo
+    // log exactly as the serial loop gives them (no copy supersedes another in the batch).
+    constexpr int kParts = 8;
+    PodVec<uint32_t> oldv;
+    oldv.reset_uninit(n);
+    uint32_t* dn = IM.dense.data();
+    auto ranges = [&](auto&& f) {
+      dk_run_parts(kParts, [&](int t) { f(t, n * (uint64_t)t / kParts, n * (uint64_t)(t + 1) / kParts); });
+    };
+    ranges([&](int, uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i) oldv[i] = dn[b->ident[i]];
+    });
+    // every allocation before the first write (a std::bad_alloc leaves the map as it was)
+    std::vector<std::vector<uint32_t>> pdead(kParts);
+    for (int t = 0; t < kParts; ++t) pdead[t].reserve(n * (uint64_t)(t + 1) / kParts - n * (uint64_t)t / kParts);
+    dead.reserve(n);
+    ranges([&](int, uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i) __atomic_store_n(&dn[b->ident[i]], (uint32_t)(row0 + i), __ATOMIC_RELAXED);
+    });
+    std::atomic<bool> dup{false};
+    ranges([&](int, uint64_t lo, uint64_t hi) {
+      bool d = false;
+      for (uint64_t i = lo; i < hi && !d; ++i) d = __atomic_load_n(&dn[b->ident[i]], __ATOMIC_RELAXED) != row0 + i;
+      if (d) dup.store(true);
+    });
+    if (dup.load()) {
+      ranges([&](int, uint64_t lo, uint64_t hi) {  // every copy of an identity read the same old row
+        for (uint64_t i = lo; i < hi; ++i) __atomic_store_n(&dn[b->ident[i]], oldv[i], __ATOMIC_RELAXED);
+      });
+      par = false;
+    } else {
+      undo.resize(n);  // reserved above: no allocation
+      ranges([&](int t, uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i) {
+          flags[i] = kAlive | kIndexed | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
+          const uint32_t old = oldv[i];
+          if (old != IdentMap::kNoRow) pdead[t].push_back(old);  // a row before the batch
+          undo[i] = {b->ident[i], old};
+        }
+      });
+      for (const auto& d : pdead) dead.insert(dead.end(), d.begin(), d.end());
+    }
+  }
+  for (uint64_t i = 0; i < n && !transient && !par; ++i) {
     flags[i] = kAlive | kIndexed | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
     if (c->overwrite) continue;
     const uint32_t old = c->ident_row.get(b->ident[i]);

@@ -751,3 +751,26 @@ def test_geoposition(mode):
         assert res2.pairs_scored == res.pairs_scored
         assert np.array_equal(res2.candidate, res.candidate) and np.array_equal(res2.prob, res.prob)
         eng.close()
+
+
+@pytest.mark.parametrize("dups", [False, True])
+def test_large_batch_identity_map(dups):
+    """dk_upsert resolves a batch of >= 65536 dense identities on parallel ranges when none
+    repeats inside the batch (identities re-posted from an earlier batch become tombstones),
+    and falls back to the serial loop when one does: the match list against the oracle's
+    alive rows either way."""
+    rng = random.Random(70 + int(dups))
+    n1 = n2 = 70000
+    n = n1 + n2
+    vals = ["".join(rng.choice("abcdefghij") for _ in range(3)) for _ in range(n)]
+    ident = np.arange(n, dtype=np.uint64)
+    npr = np.random.default_rng(70 + int(dups))
+    ident[n1:n1 + n2 // 2] = npr.choice(n1, n2 // 2, replace=False)   # re-posted in batch 2
+    if dups:
+        ident[100:200] = ident[5000:5100]                            # repeats inside batch 1
+        ident[n1 + 10:n1 + 20] = ident[n1 + 30:n1 + 40]              # and inside batch 2
+    q = np.concatenate([np.arange(0, 1000), np.arange(4950, 5150), np.arange(n1, n1 + 1000)]).astype(np.uint32)
+    res, ref = run_both([{"comparator": EX, "low": 0.1, "high": 0.9}], [vals], keys=[vals], ident=ident,
+                        threshold=0.8, queries=q, batches=[(0, n1), (n1, n)])
+    assert res.n > 0
+    assert_same(res, ref)
