@@ -1225,42 +1225,49 @@ static int stage_key(dk_ctx* c, const dk_batch* b, int style, int k, uint64_t* k
   if (!kc.offsets || (kc.width != 1 && kc.width != 2) ||
       (n && !kc.units && kc.offsets[n] != kc.offsets[0]))
     return fail(DK_E_INVALID, "key function %d: bad key column", k);
-  for (uint64_t i = 0; i < n; ++i)
-    if (kc.offsets[i + 1] < kc.offsets[i])
-      return fail(DK_E_INVALID, "key function %d: offsets not monotone at %llu", k,
-                  (unsigned long long)i);
-  // the key strings as UTF-16 and their hashes (row ranges in parallel), then the ordered
-  // insert into the key function's table
+  const int parts = n >= (1u << 16) ? 8 : 1;
+  {  // offsets monotone (row ranges in parallel; the first failing row is reported)
+    std::vector<uint64_t> bad(parts, UINT64_MAX);
+    dk_run_parts(parts, [&](int t) {
+      for (uint64_t i = n * t / parts; i < n * (t + 1) / parts; ++i)
+        if (kc.offsets[i + 1] < kc.offsets[i]) {
+          bad[t] = i;
+          break;
+        }
+    });
+    for (uint64_t i : bad)
+      if (i != UINT64_MAX)
+        return fail(DK_E_INVALID, "key function %d: offsets not monotone at %llu", k, (unsigned long long)i);
+  }
+  auto& tab = c->intern[k];
+  if (tab.size() + n >= (1ull << 31)) return fail(DK_E_UNSUPPORTED, "key function %d: over 2^31 keys", k);
+  // the key strings as UTF-16, their hashes, pointers and lengths (row ranges in parallel),
+  // then the ordered insert into the key function's table
   const uint64_t base = n ? kc.offsets[0] : 0, tot = n ? kc.offsets[n] - base : 0;
   PodVec<char16_t> wide;  // uninitialised: filled by the range workers
   const char16_t* units = reinterpret_cast<const char16_t*>(kc.units) + (kc.width == 2 ? base : 0);
   PodVec<uint64_t> h;
-  h.reset_uninit(n);
-  if (kc.width == 1) wide.reset_uninit(tot);
-  const uint8_t* u8 = (const uint8_t*)kc.units + base;
-  parallel_ranges(n, n >= (1u << 16) ? 8 : 1, [&](uint64_t lo, uint64_t hi) {
-    for (uint64_t i = lo; i < hi; ++i) {
-      const uint64_t a = kc.offsets[i] - base, e = kc.offsets[i + 1] - base;
-      if (kc.width == 1) {
-        for (uint64_t j = a; j < e; ++j) wide[j] = u8[j];
-        h[i] = U16Table::hash(wide.data() + a, e - a);
-      } else {
-        h[i] = U16Table::hash(units + a, e - a);
-      }
-    }
-  });
-  if (kc.width == 1) units = wide.data();
-  auto& tab = c->intern[k];
-  if (tab.size() + n >= (1ull << 31)) return fail(DK_E_UNSUPPORTED, "key function %d: over 2^31 keys", k);
   PodVec<const char16_t*> ptr;
   PodVec<uint32_t> ln;
+  h.reset_uninit(n);
   ptr.reset_uninit(n);
   ln.reset_uninit(n);
-  for (uint64_t i = 0; i < n; ++i) {
-    ptr[i] = units + (kc.offsets[i] - base);
-    ln[i] = kc.offsets[i + 1] - kc.offsets[i];
-  }
-  tab.intern_batch(n, ptr.data(), ln.data(), h.data(), dst, n >= (1u << 16) ? 8 : 1);
+  if (kc.width == 1) wide.reset_uninit(tot);
+  const uint8_t* u8 = (const uint8_t*)kc.units + base;
+  dk_run_parts(parts, [&](int t) {
+    for (uint64_t i = n * t / parts; i < n * (t + 1) / parts; ++i) {
+      const uint64_t a = kc.offsets[i] - base, e = kc.offsets[i + 1] - base;
+      const char16_t* v = units + a;
+      if (kc.width == 1) {
+        for (uint64_t j = a; j < e; ++j) wide[j] = u8[j];
+        v = wide.data() + a;
+      }
+      h[i] = U16Table::hash(v, e - a);
+      ptr[i] = v;
+      ln[i] = (uint32_t)(e - a);
+    }
+  });
+  tab.intern_batch(n, ptr.data(), ln.data(), h.data(), dst, parts);
   return DK_OK;
 }
 
