@@ -3130,10 +3130,19 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     const uint64_t add = hs[4 + 2 * b] + (hs[5 + 2 * b] & 0xFFFFFFFFu);
     if (add) {
       const uint64_t need = nm + add;
-      HIPCHK(B.d_cand.reserve(need * 4, nm * 4, cs));
-      HIPCHK(B.d_kind.reserve(need, nm, cs));
-      HIPCHK(B.d_prob.reserve(need * 8, nm * 8, cs));
-      HIPCHK(B.d_qidx.reserve(need * 4, nm * 4, cs));
+      // a list that outgrows its buffers is given the whole call's extrapolated size (entries
+      // per slot so far x 1.1, at most one per slot): every regrowth copies the list so far
+      // and frees the old buffer, which waits for the device
+      const uint64_t done = bounds[ci + 1], all = bounds.back();
+      const uint64_t want = done < all ? std::max(need, std::min<uint64_t>(all, (uint64_t)((double)need * (double)all / (double)done * 1.1)))
+                                       : need;
+      auto grow = [&](DevBuf& d, uint64_t el) {
+        return d.reserve((need * el > d.bytes ? want : need) * el, nm * el, cs);
+      };
+      HIPCHK(grow(B.d_cand, 4));
+      HIPCHK(grow(B.d_kind, 1));
+      HIPCHK(grow(B.d_prob, 8));
+      HIPCHK(grow(B.d_qidx, 4));
       MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(),
                    B.d_qidx.as<uint32_t>()};
       HIPCHK(hipStreamWaitEvent(cs, c->count_ready[b], 0));
@@ -3159,9 +3168,9 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
         } else {  // the pooled pinned buffers
           if (need * 8 > B.h_prob.bytes || need * 4 > B.h_cand.bytes || need > B.h_kind.bytes) {
             HIPCHK(hipStreamSynchronize(cs));
-            HIPCHK(B.h_cand.reserve(need * 4, nm * 4));
-            HIPCHK(B.h_prob.reserve(need * 8, nm * 8));
-            HIPCHK(B.h_kind.reserve(need, nm));
+            HIPCHK(B.h_cand.reserve(want * 4, nm * 4));
+            HIPCHK(B.h_prob.reserve(want * 8, nm * 8));
+            HIPCHK(B.h_kind.reserve(want, nm));
           }
           hc = B.h_cand.as<uint32_t>();
           hp = B.h_prob.as<double>();
