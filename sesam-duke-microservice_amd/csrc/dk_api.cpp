@@ -2787,9 +2787,11 @@ static int geo_raise_check(dk_ctx* c, const ScoreParams& P) {
 static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int flags,
                      ResultHolder* R, bool contiguous) {
   hipStream_t s = c->stream;
+  HostLap lap("dk_match", s);
   c->spans.clear();   // left over by a failed call
   HIPCHK(hipStreamSynchronize(c->emit_stream));  // (idle unless a failed call left work)
   HIPCHK(hipStreamSynchronize(c->copy_stream));
+  lap("streams");
   c->ev_next = 0;
   const auto t0 = std::chrono::steady_clock::now();
   const int nk = c->schema.nkeys;
@@ -2799,7 +2801,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   HIPCHK(hipMemcpyAsync(c->d_queries.p, query_rows, nq * 4, hipMemcpyHostToDevice, s));
 
   // ---- index: usable rows + per key function sort by (key, group, row) ----
-  HostLap lap("dk_match", s);
   lap("queries");
   Timer t_index(c, &c->prof.ms_index, s);
   uint64_t M = 0;
@@ -3333,6 +3334,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   HIPCHK(hipStreamSynchronize(s));
   t_gather.stop();
   resolve_spans(c);
+  lap("first");
   c->prof.ms_total +=
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return DK_OK;
