@@ -571,6 +571,8 @@ hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, c
                        hipStream_t s);
 hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
                              hipStream_t s);
+// out[i] = start + i (a contiguous batch's query rows, written on the device)
+hipError_t launch_iota_u32(uint32_t* out, uint64_t n, uint32_t start, hipStream_t s);
 hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s);
 bool long_dp_split();  // dk_kernels.hip built with DK_LONG_SPLIT (k_long_pre + P.lsim)
 hipError_t launch_sym_block_keys(const PairSource& src, uint64_t slot0, uint64_t nblocks, uint64_t* key,

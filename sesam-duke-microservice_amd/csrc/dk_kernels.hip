@@ -1917,6 +1917,11 @@ __global__ void k_gather_u64(const uint64_t* __restrict__ src, const uint64_t* _
   if (i < n) out[i] = src[idx[i]];
 }
 
+__global__ void k_iota_u32(uint32_t* __restrict__ out, uint64_t n, uint32_t start) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = start + (uint32_t)i;
+}
+
 // wq[w] = qi for every wave w of query qi's slots (one thread per query, its waves in a
 // short loop: a query spans a few waves on average)
 __global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32_t* __restrict__ wq) {
@@ -2331,6 +2336,12 @@ hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t 
                              hipStream_t s) {
   DK_LAUNCH_GUARD(n);
   k_gather_u64<<<grid1d(n), 256, 0, s>>>(src, idx, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_iota_u32(uint32_t* out, uint64_t n, uint32_t start, hipStream_t s) {
+  DK_LAUNCH_GUARD(n);
+  k_iota_u32<<<grid1d(n), 256, 0, s>>>(out, n, start);
   return hipGetLastError();
 }
 
