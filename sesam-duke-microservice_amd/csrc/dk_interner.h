@@ -354,6 +354,9 @@ struct U16Table {
         fill[s] += npl;
       }
     });
+    uint64_t nplaced = 0;
+    for (int s = 0; s < kShards; ++s) nplaced += placed_n[s];
+    if (nplaced == 0) return;  // every string was known (a re-posted batch): out[] is final
     // number the new strings in first-appearance order: per batch range, its first
     // appearances counted, then numbered from the range's prefix, then the repeats copy
     // their first appearance's id (final by then)
