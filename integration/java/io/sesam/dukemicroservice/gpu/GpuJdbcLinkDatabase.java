@@ -31,8 +31,9 @@ import no.priv.garshol.duke.links.JDBCLinkDatabase;
  * ones, one statement each, and reads the table once per record (getAllLinksFor).  Here
  * GpuProcessor opens a listener window around each batch (its writes are dropped, as with
  * GpuLinkDatabase) and hands the batch's match arrays to applyBatch, which
- *   1. reads the INFERRED links touching the batch's records in one SELECT (the IDs through a
- *      temporary table),
+ *   1. reads the stored links touching the batch's records in one SELECT (the IDs through a
+ *      temporary table; an ASSERTED link is kept as [Duke 1.2, recalled] assertLink keeps it,
+ *      Link.overrides),
  *   2. replays the listener's per-record rules in memory, in batch order (a later record sees
  *      what an earlier one wrote), and
  *   3. writes the final row of every touched link with one PreparedStatement batch (MERGE),
@@ -62,8 +63,18 @@ public class GpuJdbcLinkDatabase extends JDBCLinkDatabase {
         this.props = props == null ? new Properties() : props;
     }
 
-    /** GpuProcessor, around a batch's batchReady .. batchDone. */
+    /**
+     * GpuProcessor, around a batch's batchReady .. batchDone.  Opening the window commits the
+     * superclass connection's pending writes first -- the routes' retractions of deleted
+     * records' links (App.java:994-999) go through it before deduplicate runs, and with
+     * auto-commit off they would stay uncommitted across the window: this class's own
+     * connection would not see them in applyBatch's SELECT, and its MERGE of a link they
+     * touched would wait on their row locks (tests/test_jdbc_links.py,
+     * test_retraction_between_batches_two_connections, is the sqlite3 mirror).  Inside the
+     * window the superclass connection writes nothing.
+     */
     void setListenerWindow(boolean open) {
+        if (open && !listenerWindow) super.commit();
         listenerWindow = open;
     }
 
@@ -104,7 +115,8 @@ public class GpuJdbcLinkDatabase extends JDBCLinkDatabase {
         try {
             Connection c = connection();
             statements = 0;
-            // 1. the INFERRED links of the batch's records
+            final int asserted = LinkStatus.ASSERTED.getId();
+            // 1. the stored links of the batch's records (every status: an ASSERTED one stays)
             Map<String, Object[]> state = new HashMap<>();   // "id1\0id2" -> {id1, id2, kind, status, perhaps, ts}
             Map<String, Set<String>> byId = new HashMap<>();
             try (Statement st = c.createStatement()) {
@@ -119,9 +131,8 @@ public class GpuJdbcLinkDatabase extends JDBCLinkDatabase {
                 statements += 1;
             }
             try (PreparedStatement sel = c.prepareStatement(
-                     "select id1, id2, kind, status, perhaps, timestamp from " + TABLE + " where status = ? and "
-                     + "(id1 in (select id from dk_batch_ids) or id2 in (select id from dk_batch_ids))")) {
-                sel.setInt(1, inferred);
+                     "select id1, id2, kind, status, perhaps, timestamp from " + TABLE + " where "
+                     + "id1 in (select id from dk_batch_ids) or id2 in (select id from dk_batch_ids)")) {
                 try (ResultSet rs = sel.executeQuery()) {
                     while (rs.next()) {
                         Object[] row = {rs.getString(1), rs.getString(2), rs.getInt(3), rs.getInt(4),
@@ -156,6 +167,8 @@ public class GpuJdbcLinkDatabase extends JDBCLinkDatabase {
                 }
                 for (Map.Entry<String, Object[]> en : cur.entrySet()) {
                     Object[] r = en.getValue();
+                    Object[] old = state.get(en.getKey());
+                    if (old != null && (Integer) old[3] == asserted) continue;   // Link.overrides
                     state.put(en.getKey(), r);
                     fin.put(en.getKey(), r);
                     byId.computeIfAbsent((String) r[0], x -> new HashSet<>()).add(en.getKey());

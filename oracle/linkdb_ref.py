@@ -18,7 +18,7 @@ absent from /root/reference; the reference's own SinceAware rules are followed e
 """
 from __future__ import annotations
 
-INFERRED, RETRACTED = 1, 2
+INFERRED, RETRACTED, ASSERTED = 1, 2, 3
 SAME, MAYBE = 1, 2
 
 
@@ -93,13 +93,28 @@ class SqlLinkDB:
         return [Link(a, b, s, k, p, t) for a, b, k, s, p, t in rows]
 
     def assert_link(self, link):
+        # [Duke 1.2, recalled] JDBCLinkDatabase.assertLink reads the stored row first and
+        # keeps it when it is ASSERTED and the new link is not (Link.overrides: asserted
+        # information overrides inferred)
         self.statements += 1
+        old = self.conn.execute(f"select status from {self.table} where id1 = ? and id2 = ?",
+                                (link.id1, link.id2)).fetchone()
+        if old is not None and old[0] == ASSERTED and link.status != ASSERTED:
+            return False
         self.conn.execute(f"insert into {self.table} (id1, id2, kind, status, perhaps, timestamp) "
                           "values (?, ?, ?, ?, ?, ?) on conflict (id1, id2) do update set "
                           "kind = excluded.kind, status = excluded.status, perhaps = excluded.perhaps, "
                           "timestamp = excluded.timestamp",
                           (link.id1, link.id2, link.kind, link.status, link.confidence, link.timestamp))
         return True
+
+    def retract(self, rid, timestamp):
+        """App.java:994-999 (a deleted record): getAllLinksFor(id), link.retract() [recalled:
+        status RETRACTED, timestamp now], assertLink -- outside the listener, so uncommitted
+        until the next commit on this connection."""
+        for l in self.all_links_for(rid):
+            l.status, l.timestamp = RETRACTED, timestamp
+            self.assert_link(l)
 
     def commit(self):   # JDBCLinkDatabase.commit at batchDone
         self.conn.commit()

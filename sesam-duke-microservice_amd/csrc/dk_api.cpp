@@ -510,9 +510,6 @@ struct dk_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // device->host copies of finished chunks
-  // symmetric schedule: chunk i's emission pass runs here beside chunk i+1's owner scoring
-  hipStream_t emit_stream = nullptr;
-  hipEvent_t score_done = nullptr;  // a chunk's owner results are complete
   hipEvent_t chunk_done = nullptr;
   uint64_t nrows = 0, cap = 0;
   DevBuf ident, flags, group;
@@ -556,30 +553,18 @@ struct dk_ctx {
   DevBuf ranges, counts, qoff, wq, rident, rkeys[kMaxKeys], tmp;
   // k_score_grouped's execution order: task sort keys / values (double-buffered), chunk starts
   DevBuf task_key, task_val, task_cb, gprops, gqargs;
-  // k_tile (dk_tile.hip): per QGram role the bigram dictionary (keys marked from the gram
-  // arena up to tile_marked codes, their ids), and the per-call bucket / entry buffers
-  DevBuf tile_present[kGroupedTabs], tile_scan[kGroupedTabs], tile_lut[kGroupedTabs];
-  uint64_t tile_marked[kGroupedTabs] = {0, 0};
-  uint32_t tile_dict[kGroupedTabs] = {0, 0};
-  bool tile_key0[kGroupedTabs] = {false, false};
-  DevBuf tile_qids, tile_qrec, tile_bkey, tile_bval, tile_head, tile_bid, tile_bfirst, tile_bpos, tile_bseg,
-      tile_blen, tile_bnq, tile_nitems, tile_bitem, tile_ibucket, tile_ekey, tile_eval, tile_eprob, tile_ecand,
-      tile_small;
-  uint64_t tile_ecap = 1ull << 22;
   DevBuf gram_tmp, gram_scratch;  // dk_upsert's device q-gram sets (dk_grams.hip)
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
-  DevBuf ocounts, oqoff, owq, obase, ores, mcounts, mqoff, mbase, mres, bidx, bval;
+  DevBuf ocounts, oqoff, owq, obase, okind, ores, mcounts, mqoff, mbase, mkind, mres, ecount, eincl, bidx, bval;
   DevBuf lsim;             // the long-value DP pre-pass's similarities (k_long_pre)
   DevBuf raised;           // k_score_geo: a compared GeopositionComparator value without ','
   PinnedBuf h_raised;
-  DevBuf symkey, symval;   // symmetric owner launches: block sort keys / bucket-order permutation
   PinnedBuf h_bounds;
   DevBuf counters;
   struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx; };
   StageBufs stage[2];                          // double-buffered per-chunk staging
   StageBufs owner_stage;  // block counters of the owner phase (it emits no entries)
-  DevBuf etmp;            // scan scratch of the emission stream
   hipEvent_t count_ready[2] = {nullptr, nullptr};  // a chunk's entry count reached hs[]
   hipEvent_t compact_done[2] = {nullptr, nullptr}; // a chunk's staging set was drained
   // deferred profiling spans (Timer), resolved after dk_match's final synchronisation
@@ -774,8 +759,6 @@ static int create_impl(const dk_schema* schema, int device, dk_ctx** out) {
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->emit_stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->score_done, hipEventDisableTiming);
   for (int b = 0; b < 2 && e == hipSuccess; ++b)
     e = hipEventCreateWithFlags(&c->count_ready[b], hipEventDisableTiming);
   for (int b = 0; b < 2 && e == hipSuccess; ++b)
@@ -809,11 +792,10 @@ void dk_destroy(dk_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->copy_stream);
-  if (c->emit_stream) (void)hipStreamSynchronize(c->emit_stream);
   if (c->region.base) (void)hipHostUnregister(c->region.base);
   if (c->pair_ctx) dk_destroy(c->pair_ctx);
-  hipStream_t s = c->stream, cs = c->copy_stream, es = c->emit_stream;
-  hipEvent_t ev = c->chunk_done, sd = c->score_done;
+  hipStream_t s = c->stream, cs = c->copy_stream;
+  hipEvent_t ev = c->chunk_done;
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->count_ready)
     if (e) (void)hipEventDestroy(e);
@@ -821,8 +803,6 @@ void dk_destroy(dk_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   delete c;
   if (ev) (void)hipEventDestroy(ev);
-  if (sd) (void)hipEventDestroy(sd);
-  if (es) (void)hipStreamDestroy(es);
   if (cs) (void)hipStreamDestroy(cs);
   (void)hipStreamDestroy(s);
 }
@@ -1463,31 +1443,37 @@ static int upsert_rows(dk_ctx* c, const dk_batch* b, uint32_t* rows_out, bool tr
     std::vector<std::vector<uint32_t>> pdead(kParts);
     for (int t = 0; t < kParts; ++t) pdead[t].reserve(n * (uint64_t)(t + 1) / kParts - n * (uint64_t)t / kParts);
     dead.reserve(n);
-    ranges([&](int, uint64_t lo, uint64_t hi) {
-      for (uint64_t i = lo; i < hi; ++i) __atomic_store_n(&dn[b->ident[i]], (uint32_t)(row0 + i), __ATOMIC_RELAXED);
-    });
-    std::atomic<bool> dup{false};
-    ranges([&](int, uint64_t lo, uint64_t hi) {
-      bool d = false;
-      for (uint64_t i = lo; i < hi && !d; ++i) d = __atomic_load_n(&dn[b->ident[i]], __ATOMIC_RELAXED) != row0 + i;
-      if (d) dup.store(true);
-    });
-    if (dup.load()) {
-      ranges([&](int, uint64_t lo, uint64_t hi) {  // every copy of an identity read the same old row
-        for (uint64_t i = lo; i < hi; ++i) __atomic_store_n(&dn[b->ident[i]], oldv[i], __ATOMIC_RELAXED);
+    // phases 2-4 start threads (dk_run_parts may allocate): a throw there restores every
+    // identity's old row serially (no allocation; copies of one identity read the same old
+    // row) before it leaves, so the map is as it was
+    try {
+      ranges([&](int, uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i) __atomic_store_n(&dn[b->ident[i]], (uint32_t)(row0 + i), __ATOMIC_RELAXED);
       });
-      par = false;
-    } else {
-      undo.resize(n);  // reserved above: no allocation
-      ranges([&](int t, uint64_t lo, uint64_t hi) {
-        for (uint64_t i = lo; i < hi; ++i) {
-          flags[i] = kAlive | kIndexed | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
-          const uint32_t old = oldv[i];
-          if (old != IdentMap::kNoRow) pdead[t].push_back(old);  // a row before the batch
-          undo[i] = {b->ident[i], old};
-        }
+      std::atomic<bool> dup{false};
+      ranges([&](int, uint64_t lo, uint64_t hi) {
+        bool d = false;
+        for (uint64_t i = lo; i < hi && !d; ++i) d = __atomic_load_n(&dn[b->ident[i]], __ATOMIC_RELAXED) != row0 + i;
+        if (d) dup.store(true);
       });
-      for (const auto& d : pdead) dead.insert(dead.end(), d.begin(), d.end());
+      if (dup.load()) {
+        for (uint64_t i = 0; i < n; ++i) dn[b->ident[i]] = oldv[i];  // every copy read the same old row
+        par = false;
+      } else {
+        undo.resize(n);  // reserved above: no allocation
+        ranges([&](int t, uint64_t lo, uint64_t hi) {
+          for (uint64_t i = lo; i < hi; ++i) {
+            flags[i] = kAlive | kIndexed | ((b->deleted && b->deleted[i]) ? kDeleted : 0);
+            const uint32_t old = oldv[i];
+            if (old != IdentMap::kNoRow) pdead[t].push_back(old);  // a row before the batch
+            undo[i] = {b->ident[i], old};
+          }
+        });
+        for (const auto& d : pdead) dead.insert(dead.end(), d.begin(), d.end());
+      }
+    } catch (...) {
+      for (uint64_t i = 0; i < n; ++i) dn[b->ident[i]] = oldv[i];
+      throw;
     }
   }
   for (uint64_t i = 0; i < n && !transient && !par; ++i) {
@@ -2253,15 +2239,6 @@ static int ensure_tables(dk_ctx* c, BlockTables* Tout, uint64_t* Mout) {
   return DK_OK;
 }
 
-// DK_EMIT_OVERLAP=1: the symmetric schedule's emission pass on its own stream, beside the
-// next chunk's owner scoring.  Off by default: measured on configs[1] the step gained 0.1 ms
-// (34.36 vs 34.45, 2 x 20 steps) because the two kernels share the CUs, while k_score's
-// launches stretched by the emission's work (profiles/r03/ab_emit_ne_tail/).
-static bool emit_overlap() {
-  const char* e = getenv("DK_EMIT_OVERLAP");
-  return e && e[0] == '1';
-}
-
 static bool sym_enabled() {
   const char* e = getenv("DK_SYM");
   return !(e && e[0] == '0');
@@ -2493,281 +2470,6 @@ static int lucene_candidates(dk_ctx* c, uint64_t nq, uint64_t* total, uint64_t* 
   return DK_OK;
 }
 
-// ---------------------------------------------------------------------------------------
-// The bucket-tiled schedule (k_tile, dk_tile.hip) for GQArgs schemas on the direct schedule:
-// the same list as k_score_gq (tests/test_gpu_configs.py compares both with the oracle).
-// DK_TILE=1 selects it (k_score_gq is the default).  Eligible: key functions <= 2 (the duplicate filter reads
-// rkeys[0]), per QGram role a dictionary of <= kTileMaxDict keys without the key-0 bigram.
-// ---------------------------------------------------------------------------------------
-static bool tile_enabled() {  // DK_TILE=1: measured slower than k_score_gq, opt-in
-  const char* e = getenv("DK_TILE");
-  return e && e[0] == '1';
-}
-
-// the dictionary of QGram role a (property p): mark the gram arena's codes not marked yet,
-// ids = exclusive prefix of the marks; returns DK_OK and fills tile_dict / tile_key0
-static int tile_dictionary(dk_ctx* c, int a, int p) {
-  hipStream_t s = c->stream;
-  PropState& S = c->P[p];
-  HIPCHK(c->tile_present[a].reserve(65536 * 4, 0, s));
-  HIPCHK(c->tile_scan[a].reserve(65536 * 4 + 4, 0, s));
-  HIPCHK(c->tile_lut[a].reserve(65536 * 2, 0, s));
-  if (S.grams_used < c->tile_marked[a]) c->tile_marked[a] = 0;  // the arena was rebuilt
-  if (c->tile_marked[a] == 0) HIPCHK(hipMemsetAsync(c->tile_present[a].p, 0, 65536 * 4, s));
-  if (S.grams_used > c->tile_marked[a])
-    HIPCHK(launch_tile_mark(S.grams.as<uint64_t>(), c->tile_marked[a], S.grams_used - c->tile_marked[a],
-                            c->tile_present[a].as<uint32_t>(), s));
-  c->tile_marked[a] = S.grams_used;
-  HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
-    return exclusive_scan_u32(t, b, c->tile_present[a].as<uint32_t>(), c->tile_scan[a].as<uint32_t>(), 65536, s);
-  }));
-  HIPCHK(launch_tile_lut(c->tile_scan[a].as<uint32_t>(), c->tile_lut[a].as<uint16_t>(), s));
-  uint32_t h[3];
-  HIPCHK(hipMemcpyAsync(&h[0], c->tile_scan[a].as<uint32_t>() + 65535, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&h[1], c->tile_present[a].as<uint32_t>() + 65535, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&h[2], c->tile_present[a].as<uint32_t>(), 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  c->tile_dict[a] = h[0] + h[1];
-  c->tile_key0[a] = h[2] != 0;
-  return DK_OK;
-}
-
-// the tiled dk_match after the index is in place (T, P); returns 1 when the schema or the
-// index does not fit the tiled path (the caller goes on with the slot schedule)
-static int tile_match(dk_ctx* c, const ScoreParams& P, const BlockTables& T, uint64_t nq, int flags,
-                      ResultHolder* R, std::chrono::steady_clock::time_point t0) {
-  hipStream_t s = c->stream;
-  GQArgs gqa;
-  int nqr = 0, nnr = 0;
-  if (!tile_enabled() || c->schema.nkeys > 2 || !grouped_schema_ok(P) || !gq_args(P, &gqa, &nqr, &nnr)) return 1;
-  int planes = 6;
-  for (int a = 0; a < nqr; ++a) {
-    if (c->P[gqa.q[a].prop].maxgrams > kTileIdsPerRole) return 1;
-    if (c->P[gqa.q[a].prop].maxgrams >= 64) planes = 7;
-  }
-  Timer t_gen(c, &c->prof.ms_generate, s);
-  for (int a = 0; a < nqr; ++a) {
-    int rc = tile_dictionary(c, a, gqa.q[a].prop);
-    if (rc) return rc;
-    if (c->tile_dict[a] > kTileMaxDict || c->tile_key0[a]) return 1;
-  }
-  // candidate ranges per (segment, query)
-  HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
-  HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
-  HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
-  HIPCHK(launch_count(c->d_queries.as<uint32_t>(), nq, T, c->ranges.as<uint2>(), c->counts.as<uint64_t>(),
-                      c->counters.as<uint64_t>() + 2, 64, s));
-  PairSource src{};
-  src.queries = c->d_queries.as<uint32_t>();
-  src.ranges = c->ranges.as<uint2>();
-  src.nq = nq;
-  src.nkeys = c->schema.nkeys;
-  src.nseg = T.nseg;
-  src.seg_shift = T.seg_shift;
-  for (int k = 0; k < T.nseg; ++k) src.segoff[k] = T.seg_off[k];
-  src.rident = c->rident.as<uint64_t>();
-  for (int k = 0; k < c->schema.nkeys; ++k) {
-    src.qkeys[k] = c->keys[k].as<uint64_t>();
-    src.rkeys[k] = c->rkeys[k].as<uint64_t>();
-  }
-  // the roles' device copy, and each query's key ids
-  HIPCHK(c->gqargs.reserve(sizeof(GQArgs), 0, s));
-  HIPCHK(hipMemcpyAsync(c->gqargs.p, &gqa, sizeof(GQArgs), hipMemcpyHostToDevice, s));
-  HIPCHK(c->tile_qids.reserve(nq * nqr * kTileIdsPerRole * 2 + 16, 0, s));
-  HIPCHK(launch_tile_qids(P, c->d_queries.as<uint32_t>(), nq, c->gqargs.as<GQArgs>(), nqr,
-                          c->tile_lut[0].as<uint16_t>(), nqr > 1 ? c->tile_lut[1].as<uint16_t>() : nullptr,
-                          c->tile_qids.as<uint16_t>(), s));
-  HIPCHK(c->tile_qrec.reserve(nq * sizeof(TileQRec) + 64, 0, s));
-  HIPCHK(launch_tile_qrec(P, src, c->gqargs.as<GQArgs>(), c->tile_qrec.as<TileQRec>(), s));
-  // buckets: (range start << 32 | query index) of every (segment, query) with candidates, sorted
-  const uint64_t n = (uint64_t)T.nseg * nq;
-  HIPCHK(c->tile_bkey.reserve(2 * n * 8 + 16, 0, s));
-  HIPCHK(c->tile_bval.reserve(2 * n * 4 + 16, 0, s));
-  HIPCHK(c->tile_head.reserve(n * 4 + 4, 0, s));
-  HIPCHK(c->tile_bid.reserve(n * 4 + 4, 0, s));
-  uint64_t* k0 = c->tile_bkey.as<uint64_t>();
-  uint64_t* k1 = k0 + n;
-  uint32_t* v0 = c->tile_bval.as<uint32_t>();
-  HIPCHK(c->tile_small.reserve(64, 0, s));
-  HIPCHK(hipMemsetAsync(c->tile_small.p, 0, 16, s));
-  HIPCHK(launch_tile_bkeys(src, k0, c->tile_small.as<uint64_t>() + 1, s));
-  HIPCHK(with_tmp(c, [&](void* t, size_t& b) { return sort_pairs_u64_u32(t, b, k0, k1, v0, v0 + n, n, s); }));
-  HIPCHK(launch_tile_heads(k1, n, c->tile_head.as<uint32_t>(), s));
-  HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
-    return exclusive_scan_u32(t, b, c->tile_head.as<uint32_t>(), c->tile_bid.as<uint32_t>(), n, s);
-  }));
-  uint64_t* hs = c->h_small.as<uint64_t>();
-  uint32_t h4[2];
-  HIPCHK(hipMemcpyAsync(&h4[0], c->tile_bid.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&h4[1], c->tile_head.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&hs[2], c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&hs[5], c->tile_small.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  const uint64_t generated = hs[2];
-  const uint64_t nb = n ? (uint64_t)h4[0] + h4[1] : 0;
-  // the keys with candidates (k_tile_bkeys counted them): a prefix of the sorted keys
-  // (empty ranges sort last as ~0)
-  const uint64_t nvalid = hs[5];
-  HIPCHK(c->tile_bfirst.reserve(nb * 4 + 4, 0, s));
-  HIPCHK(c->tile_bpos.reserve(nb * 4 + 4, 0, s));
-  HIPCHK(c->tile_bseg.reserve(nb * 4 + 4, 0, s));
-  HIPCHK(c->tile_blen.reserve(nb * 4 + 4, 0, s));
-  HIPCHK(c->tile_bnq.reserve(nb * 4 + 4, 0, s));
-  HIPCHK(c->tile_nitems.reserve(nb * 8 + 8, 0, s));
-  HIPCHK(c->tile_bitem.reserve(nb * 8 + 16, 0, s));
-  HIPCHK(launch_tile_buckets(src, k1, n, nvalid, c->tile_head.as<uint32_t>(), c->tile_bid.as<uint32_t>(), nb,
-                             c->tile_bfirst.as<uint32_t>(), c->tile_bpos.as<uint32_t>(), c->tile_bseg.as<uint32_t>(),
-                             c->tile_blen.as<uint32_t>(), c->tile_bnq.as<uint32_t>(), c->tile_nitems.as<uint64_t>(), s));
-  uint64_t nitems = 0;
-  if (nb) {
-    HIPCHK(hipMemsetAsync(c->tile_nitems.as<uint64_t>() + nb, 0, 8, s));
-    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
-      return exclusive_scan_u64(t, b, c->tile_nitems.as<uint64_t>(), c->tile_bitem.as<uint64_t>(), nb + 1, s);
-    }));
-    HIPCHK(hipMemcpyAsync(&hs[3], c->tile_bitem.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    nitems = hs[3];
-  }
-  if (nitems >= (1ull << 31)) return 1;
-  HIPCHK(c->tile_ibucket.reserve(nitems * 4 + 4, 0, s));
-  HIPCHK(launch_tile_itemmap(c->tile_bitem.as<uint64_t>(), nb, nitems, c->tile_ibucket.as<uint32_t>(), s));
-  t_gen.stop();
-
-  TileArgs TA{};
-  TA.bkey = k1;
-  TA.bfirst = c->tile_bfirst.as<uint32_t>();
-  TA.bnq = c->tile_bnq.as<uint32_t>();
-  TA.bpos = c->tile_bpos.as<uint32_t>();
-  TA.bseg = c->tile_bseg.as<uint32_t>();
-  TA.blen = c->tile_blen.as<uint32_t>();
-  TA.bitem = c->tile_bitem.as<uint64_t>();
-  TA.ibucket = c->tile_ibucket.as<uint32_t>();
-  TA.nbuckets = nb;
-  TA.nitems = nitems;
-  uint32_t rows = 0;
-  for (int a = 0; a < nqr; ++a) {
-    TA.lut[a] = c->tile_lut[a].as<uint16_t>();
-    TA.dict[a] = c->tile_dict[a];
-    TA.toff[a] = rows;
-    rows += c->tile_dict[a] + 1;  // + the zero row
-  }
-  if (rows > kTileMaxRows) return 1;
-  TA.tsize = rows;
-  TA.qids = c->tile_qids.as<uint16_t>();
-  TA.qrec = c->tile_qrec.as<TileQRec>();
-  TA.counters = c->counters.as<uint64_t>();
-  TA.nq = nq;
-  TA.nvalid = nvalid;
-  TA.npos = P.rstride;
-  const bool tdebug = getenv("DK_TILE_DEBUG") != nullptr;
-  HIPCHK(c->tile_small.reserve(64, 0, s));
-  TA.dbg = reinterpret_cast<uint32_t*>(c->tile_small.as<uint64_t>() + 2);
-  if (tdebug) HIPCHK(hipMemsetAsync(TA.dbg, 0, 4, s));
-  uint64_t nm = 0;
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    const uint64_t cap = c->tile_ecap;
-    HIPCHK(c->tile_ekey.reserve(2 * cap * 8 + 16, 0, s));
-    HIPCHK(c->tile_eval.reserve(2 * cap * 4 + 16, 0, s));
-    HIPCHK(c->tile_eprob.reserve(cap * 8 + 16, 0, s));
-    HIPCHK(c->tile_ecand.reserve(cap * 4 + 16, 0, s));
-    TA.ecount = c->tile_small.as<uint64_t>();
-    TA.ecap = cap;
-    TA.ekey = c->tile_ekey.as<uint64_t>();
-    TA.eval = c->tile_eval.as<uint32_t>();
-    TA.eprob = c->tile_eprob.as<double>();
-    TA.ecand = c->tile_ecand.as<uint32_t>();
-    HIPCHK(hipMemsetAsync(c->tile_small.p, 0, 8, s));
-    HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * sizeof(uint64_t), s));
-    {
-      Timer t_score(c, &c->prof.ms_score, s);
-      HIPCHK(launch_tile(P, src, c->gqargs.as<GQArgs>(), nqr, nnr, planes, TA, s));
-      t_score.stop();
-    }
-    c->prof.score_launches += 1;
-    HIPCHK(hipMemcpyAsync(&hs[4], c->tile_small.p, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    nm = hs[4];
-    if (tdebug) {
-      uint32_t f = 0;
-      HIPCHK(hipMemcpy(&f, TA.dbg, 4, hipMemcpyDeviceToHost));
-      fprintf(stderr, "[dk_tile] items %llu buckets %llu nvalid %llu entries %llu dict %u/%u check flags 0x%x\n",
-              (unsigned long long)nitems, (unsigned long long)nb, (unsigned long long)nvalid,
-              (unsigned long long)nm, TA.dict[0], TA.dict[1], f);
-    }
-    if (nm <= cap) break;
-    c->tile_ecap = nm + nm / 4 + 1024;  // the list outgrew the entries: once more, sized
-    if (attempt == 1) return fail(DK_E_STATE, "tiled match: entry count changed between runs");
-  }
-
-  // ---- the list in Duke's order: entries sorted by (query index, slot) ----
-  Timer t_gather(c, &c->prof.ms_gather, s);
-  ResultBufs& B = *R->bufs;
-  uint64_t* ek = c->tile_ekey.as<uint64_t>();
-  uint32_t* ev = c->tile_eval.as<uint32_t>();
-  const uint64_t cap = c->tile_ecap;
-  if (nm) {
-    HIPCHK(with_tmp(c, [&](void* t, size_t& b) { return sort_pairs_u64_u32(t, b, ek, ek + cap, ev, ev + cap, nm, s); }));
-  }
-  HIPCHK(B.d_cand.reserve(nm * 4 + 4, 0, s));
-  HIPCHK(B.d_kind.reserve(nm + 1, 0, s));
-  HIPCHK(B.d_prob.reserve(nm * 8 + 8, 0, s));
-  HIPCHK(B.d_qidx.reserve(nm * 4 + 4, 0, s));
-  MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(), B.d_qidx.as<uint32_t>()};
-  HIPCHK(launch_tile_emit(ek + cap, ev + cap, nm, c->tile_eprob.as<double>(), c->tile_ecand.as<uint32_t>(), ml, s));
-  HIPCHK(hipMemcpyAsync(c->h_small.p, c->counters.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  const uint64_t scored = c->h_small.as<uint64_t>()[0];
-  const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
-  R->r.pairs_scored = scored;
-  R->r.pairs_generated = generated;
-  c->prof.pairs_scored += scored;
-  c->prof.pairs_generated += generated;
-  c->prof.score_bytes += sbytes;
-  HIPCHK(B.d_first.reserve((nq + 1) * 8, 0, s));
-  HIPCHK(launch_first(B.d_qidx.as<uint32_t>(), nm, nq, B.d_first.as<uint64_t>(), s));
-  R->r.nqueries = nq;
-  R->r.n = nm;
-  if (!(flags & DK_MATCH_DEVICE)) {
-    uint32_t* hc;
-    double* hp;
-    uint8_t* hk;
-    uint64_t* hf;
-    if (c->region.base) {
-      if (nm > c->region.cap)
-        return fail(DK_E_NOMEM, "match list needs more than %llu entries; the result region holds %llu",
-                    (unsigned long long)nm, (unsigned long long)c->region.cap);
-      hc = c->region.cand;
-      hp = c->region.prob;
-      hk = c->region.kind;
-      hf = c->region.first;
-    } else {
-      HIPCHK(B.h_first.reserve((nq + 1) * 8));
-      HIPCHK(B.h_cand.reserve(nm * 4 + 4, 0));
-      HIPCHK(B.h_prob.reserve(nm * 8 + 8, 0));
-      HIPCHK(B.h_kind.reserve(nm + 1, 0));
-      hc = B.h_cand.as<uint32_t>();
-      hp = B.h_prob.as<double>();
-      hk = B.h_kind.as<uint8_t>();
-      hf = B.h_first.as<uint64_t>();
-    }
-    Timer t_copy(c, &c->prof.ms_copy, s);
-    HIPCHK(hipMemcpyAsync(hc, B.d_cand.p, nm * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(hp, B.d_prob.p, nm * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(hk, B.d_kind.p, nm, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(hf, B.d_first.p, (nq + 1) * 8, hipMemcpyDeviceToHost, s));
-    t_copy.stop();
-    R->r.first = hf;
-    R->r.candidate = hc;
-    R->r.prob = hp;
-    R->r.kind = hk;
-  }
-  HIPCHK(hipStreamSynchronize(s));
-  t_gather.stop();
-  resolve_spans(c);
-  c->prof.ms_total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  return DK_OK;
-}
-
 // GeopositionComparator values without ',' (numok 2): cleared before a geo schema's scoring,
 // read after it; set -> the call fails as stock Duke's compare would raise
 static int geo_raise_clear(dk_ctx* c, const ScoreParams& P) {
@@ -2789,7 +2491,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   hipStream_t s = c->stream;
   HostLap lap("dk_match", s);
   c->spans.clear();   // left over by a failed call
-  HIPCHK(hipStreamSynchronize(c->emit_stream));  // (idle unless a failed call left work)
   HIPCHK(hipStreamSynchronize(c->copy_stream));
   lap("streams");
   c->ev_next = 0;
@@ -2832,11 +2533,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     if (P.props[p].op == DK_CMP_QGRAM)
       c->prof.gram_row_bytes = std::max(c->prof.gram_row_bytes, (uint64_t)P.props[p].rgrows * P.rstride * 8);
   bool sym = !lucene && contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
-  if (!sym && !lucene && !allpairs && nq > 0) {
-    t_gen.stop();
-    const int trc = tile_match(c, P, T, nq, flags, R, t0);
-    if (trc != 1) return trc;   // 1: not this schema / index -- the slot schedule below
-  }
   bool grouped = false;  // k_score_grouped: query slots padded to kScoreBlock
   const uint32_t r0 = nq ? query_rows[0] : 0;
   uint64_t* hs = c->h_small.as<uint64_t>();
@@ -2873,23 +2569,67 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     generated = hs[2];
     otot = hs[1];
     mtot = hs[0];
-    // owner and mirror results live for the whole call (a query's emission reads what
-    // earlier queries pushed): 8 B per owner and per mirror slot, within a third of the
-    // free HBM, else the direct schedule
+  }
+  // at least kMinChunks chunks (down to CH0/16 slots each): the emission pass and the list's
+  // copies of chunk i overlap the scoring of chunk i+1, so a small call (one GPU's tile of a
+  // multi-GPU match) still pipelines
+  constexpr uint64_t kMinChunks = 8;
+  const uint64_t CH0 = chunk_slots();
+  auto chunk_len = [&](uint64_t tot) {
+    return std::max<uint64_t>(kScoreBlock, (std::max(CH0 / 16, std::min(CH0, (tot + kMinChunks - 1) / kMinChunks)) +
+                                            kScoreBlock - 1) / kScoreBlock * kScoreBlock);
+  };
+  // SYM: chunks cut by queries (an emission chunk reads the owner results of its own queries
+  // and the mirror results earlier queries pushed): qb = the chunks' query bounds, obounds =
+  // their owner slots; ochunk = the largest chunk's owner slots
+  std::vector<uint64_t> qb, obounds;
+  uint64_t ochunk = 1;
+  if (sym) {
+    qb.push_back(0);
+    const uint64_t nch = std::max<uint64_t>(1, (total + chunk_len(total) - 1) / chunk_len(total));
+    for (uint64_t i = 1; i < nch; ++i) qb.push_back(nq * i / nch);
+    qb.push_back(nq);
+    if (!(flags & DK_MATCH_DEVICE)) {  // halve the last chunk twice
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t a = qb[qb.size() - 2], e = qb.back();
+        if (e - a >= 2) qb.insert(qb.end() - 1, a + (e - a) / 2);
+      }
+    }
+    const uint64_t nb = qb.size();
+    HIPCHK(c->bidx.reserve(nb * 8 + 8, 0, s));
+    HIPCHK(c->bval.reserve(nb * 8 + 8, 0, s));
+    HIPCHK(c->h_bounds.reserve(nb * 8 + 8));
+    uint64_t* hb = c->h_bounds.as<uint64_t>();
+    memcpy(hb, qb.data(), nb * 8);
+    HIPCHK(hipMemcpyAsync(c->bidx.p, hb, nb * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_gather_u64(c->oqoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb, c->bval.as<uint64_t>(), s));
+    HIPCHK(hipMemcpyAsync(hb, c->bval.p, nb * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    obounds.assign(hb, hb + nb);
+    for (size_t i = 0; i + 1 < obounds.size(); ++i) ochunk = std::max(ochunk, obounds[i + 1] - obounds[i]);
+    // mirror results live for the whole call (a query's emission reads what earlier
+    // queries pushed): a decision byte + 8 B per mirror slot; owner results for one chunk
+    // (its emission reads only its own queries' owner slots): two chunk-sized halves of a
+    // byte + 8 B per owner slot.  Within a third of the free HBM, else the direct schedule.
     size_t fr = 0, tot_mem = 0;
     HIPCHK(hipMemGetInfo(&fr, &tot_mem));
-    const size_t need = (otot * 8 + 64 > c->ores.bytes ? otot * 8 + 64 - c->ores.bytes : 0) +
-                        (mtot * 8 + 64 > c->mres.bytes ? mtot * 8 + 64 - c->mres.bytes : 0);
+    auto grow_by = [](const DevBuf& d, uint64_t want) { return want > d.bytes ? want - d.bytes : 0; };
+    const size_t need = grow_by(c->ores, 2 * ochunk * 8 + 64) + grow_by(c->okind, 2 * ochunk + 64) +
+                        grow_by(c->mres, mtot * 8 + 64) + grow_by(c->mkind, mtot + 64) +
+                        grow_by(c->ecount, nq * 4 + 4) + grow_by(c->eincl, nq * 8 + 8);
     if (need > fr / 3) sym = false;
   }
   if (sym) {
     HIPCHK(c->mres.reserve(mtot * 8 + 64, 0, s));
+    HIPCHK(c->mkind.reserve(mtot + 64, 0, s));
+    HIPCHK(c->ores.reserve(2 * ochunk * 8 + 64, 0, s));
+    HIPCHK(c->okind.reserve(2 * ochunk + 64, 0, s));
+    HIPCHK(c->ecount.reserve(nq * 4 + 4, 0, s));
+    HIPCHK(c->eincl.reserve(nq * 8 + 8, 0, s));
     HIPCHK(c->mbase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
-    HIPCHK(hipMemsetAsync(c->mres.p, 0xFF, mtot * 8, s));  // all-ones: a NaN (no entry)
-    HIPCHK(c->wq.reserve(total / 64 * 4 + 4, 0, s));
+    HIPCHK(hipMemsetAsync(c->mkind.p, 0, mtot, s));  // no entry unless an owner pushes one
     HIPCHK(c->owq.reserve(otot / 64 * 4 + 4, 0, s));
     HIPCHK(c->obase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
-    HIPCHK(launch_wavemap(c->qoff.as<uint64_t>(), nq, c->wq.as<uint32_t>(), s));
     HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s));
     HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), c->mqoff.as<uint64_t>(),
                         nq, T.nseg, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
@@ -2918,46 +2658,14 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     total = nq * mpad;
     generated = nq * M;
   }
-  // at least kMinChunks chunks (down to CH0/16 slots each): the emission pass and the list's
-  // copies of chunk i overlap the scoring of chunk i+1, so a small call (one GPU's tile of a
-  // multi-GPU match) still pipelines
-  constexpr uint64_t kMinChunks = 8;
-  const uint64_t CH0 = chunk_slots();
-  const uint64_t CH = std::max<uint64_t>(
-      kScoreBlock, (std::max(CH0 / 16, std::min(CH0, (total + kMinChunks - 1) / kMinChunks)) +
-                    kScoreBlock - 1) / kScoreBlock * kScoreBlock);
-  // chunk boundaries in slots: full chunks, then (host modes) the last two chunks' worth
-  // halved down to CH/16, so the copy of the final chunk's entries (not overlapped with
-  // scoring) is short.  The symmetric schedule cuts by queries instead (an emission chunk
-  // reads the owner results of its own and earlier queries): bounds = full slots and
-  // obounds = owner slots at the same query boundaries.
-  std::vector<uint64_t> bounds{0}, obounds;
+  // chunk boundaries: (direct schedules) in slots: full chunks, then (host modes) the last
+  // two chunks' worth halved down to CH/16, so the copy of the final chunk's entries (not
+  // overlapped with scoring) is short; (SYM) the query bounds qb
+  std::vector<uint64_t> bounds{0};
   if (sym) {
-    std::vector<uint64_t> qb{0};
-    const uint64_t nch = std::max<uint64_t>(1, (total + CH - 1) / CH);
-    for (uint64_t i = 1; i < nch; ++i) qb.push_back(nq * i / nch);
-    qb.push_back(nq);
-    if (!(flags & DK_MATCH_DEVICE)) {  // halve the last chunk twice
-      for (int h = 0; h < 2; ++h) {
-        const uint64_t a = qb[qb.size() - 2], e = qb.back();
-        if (e - a >= 2) qb.insert(qb.end() - 1, a + (e - a) / 2);
-      }
-    }
-    const uint64_t nb = qb.size();
-    HIPCHK(c->bidx.reserve(nb * 8 + 8, 0, s));
-    HIPCHK(c->bval.reserve(2 * nb * 8 + 8, 0, s));
-    HIPCHK(c->h_bounds.reserve(2 * nb * 8 + 8));
-    uint64_t* hb = c->h_bounds.as<uint64_t>();
-    memcpy(hb, qb.data(), nb * 8);
-    HIPCHK(hipMemcpyAsync(c->bidx.p, hb, nb * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_gather_u64(c->qoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb, c->bval.as<uint64_t>(), s));
-    HIPCHK(launch_gather_u64(c->oqoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb,
-                             c->bval.as<uint64_t>() + nb, s));
-    HIPCHK(hipMemcpyAsync(hb, c->bval.p, 2 * nb * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    bounds.assign(hb, hb + nb);
-    obounds.assign(hb + nb, hb + 2 * nb);
+    bounds = qb;
   } else {
+    const uint64_t CH = chunk_len(total);
     const uint64_t min_chunk = std::max<uint64_t>(kScoreBlock, CH / 16 / kScoreBlock * kScoreBlock);
     uint64_t at = 0;
     while (at < total) {
@@ -2972,33 +2680,29 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   t_gen.stop();
   lap("generate");
 
-  uint64_t chunk = 1;
-  for (size_t i = 0; i + 1 < bounds.size(); ++i) chunk = std::max(chunk, bounds[i + 1] - bounds[i]);
-  const uint64_t nblk_max = (chunk + kScoreBlock - 1) / kScoreBlock;
-  // two staging sets: chunk i+1 scores into one while chunk i's entries are compacted
-  // out of the other, so the host never waits between score launches
+  // two staging sets (direct schedules): chunk i+1 scores into one while chunk i's entries
+  // are compacted out of the other, so the host never waits between score launches
   StageOut st[2];
-  for (int b = 0; b < 2; ++b) {
-    dk_ctx::StageBufs& G = c->stage[b];
-    HIPCHK(G.bcnt.reserve(nblk_max * 4 + 4, 0, s));
-    HIPCHK(G.bscored.reserve(nblk_max * 4 + 4, 0, s));
-    HIPCHK(G.bbytes.reserve(nblk_max * 4 + 4, 0, s));
-    HIPCHK(G.boff.reserve(nblk_max * 8 + 8, 0, s));
-    HIPCHK(G.prob.reserve(nblk_max * kScoreBlock * 8, 0, s));
-    HIPCHK(G.cand.reserve(nblk_max * kScoreBlock * 4, 0, s));
-    HIPCHK(G.qidx.reserve(nblk_max * kScoreBlock * 4, 0, s));
-    st[b] = StageOut{c->counters.as<uint64_t>(), G.bcnt.as<uint32_t>(), G.bscored.as<uint32_t>(),
-                     G.bbytes.as<uint32_t>(), G.prob.as<double>(), G.cand.as<uint32_t>(),
-                     G.qidx.as<uint32_t>()};
+  if (!sym) {
+    uint64_t chunk = 1;
+    for (size_t i = 0; i + 1 < bounds.size(); ++i) chunk = std::max(chunk, bounds[i + 1] - bounds[i]);
+    const uint64_t nblk_max = (chunk + kScoreBlock - 1) / kScoreBlock;
+    for (int b = 0; b < 2; ++b) {
+      dk_ctx::StageBufs& G = c->stage[b];
+      HIPCHK(G.bcnt.reserve(nblk_max * 4 + 4, 0, s));
+      HIPCHK(G.bscored.reserve(nblk_max * 4 + 4, 0, s));
+      HIPCHK(G.bbytes.reserve(nblk_max * 4 + 4, 0, s));
+      HIPCHK(G.boff.reserve(nblk_max * 8 + 8, 0, s));
+      HIPCHK(G.prob.reserve(nblk_max * kScoreBlock * 8, 0, s));
+      HIPCHK(G.cand.reserve(nblk_max * kScoreBlock * 4, 0, s));
+      HIPCHK(G.qidx.reserve(nblk_max * kScoreBlock * 4, 0, s));
+      st[b] = StageOut{c->counters.as<uint64_t>(), G.bcnt.as<uint32_t>(), G.bscored.as<uint32_t>(),
+                       G.bbytes.as<uint32_t>(), G.prob.as<double>(), G.cand.as<uint32_t>(),
+                       G.qidx.as<uint32_t>()};
+    }
   }
   StageOut so{};  // SYM: the owner phase's block counters (it stages no entries)
-  uint64_t ochunk = 1;  // SYM: the largest chunk's owner slots
   if (sym) {
-    for (size_t i = 0; i + 1 < obounds.size(); ++i) ochunk = std::max(ochunk, obounds[i + 1] - obounds[i]);
-    // owner results live for one chunk (its emission reads only its own queries' owner
-    // slots; what crosses chunks is the mirror results): two chunk-sized halves, chunk ci
-    // in half ci & 1, instead of 8 B per owner slot of the whole call
-    HIPCHK(c->ores.reserve(2 * ochunk * 8 + 64, 0, s));
     const uint64_t onblk = (ochunk + kScoreBlock - 1) / kScoreBlock;
     dk_ctx::StageBufs& G = c->owner_stage;
     HIPCHK(G.bcnt.reserve(onblk * 4 + 4, 0, s));
@@ -3033,28 +2737,28 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   }
   EmitSource esrc{};
   if (sym) {
-    // owner slots: phase 1 scores them into ores; the emission pass walks the full slots
+    // owner slots: phase 1 scores them (okind / ores), the emission pass walks the queries
     src.sym = 1;
     src.wq = c->owq.as<uint32_t>();
     src.qoff = c->oqoff.as<uint64_t>();
     src.sranges = c->ranges.as<uint4>();
+    src.mkind = c->mkind.as<uint8_t>();
     src.mres = c->mres.as<double>();
     src.mbase = c->mbase.as<uint64_t>();
     src.r0 = r0;
     src.r1 = r0 + (uint32_t)nq;
-    esrc.wq = c->wq.as<uint32_t>();
-    esrc.qoff = c->qoff.as<uint64_t>();
     esrc.sranges = c->ranges.as<uint4>();
     esrc.obase = c->obase.as<uint64_t>();
-    esrc.mres = c->mres.as<double>();
     esrc.mbase = c->mbase.as<uint64_t>();
+    esrc.mkind = c->mkind.as<uint8_t>();
+    esrc.mres = c->mres.as<double>();
     esrc.rowof = c->rowof.as<uint32_t>();
     esrc.nq = nq;
     esrc.nseg = T.nseg;
     for (int k = 0; k < T.nseg; ++k) esrc.segoff[k] = T.seg_off[k];
-    esrc.r0 = r0;
-    esrc.threshold = P.threshold;
-    esrc.maybe = P.maybe;
+    esrc.ecount = c->ecount.as<uint32_t>();
+    esrc.eincl = c->eincl.as<uint64_t>();
+    HIPCHK(B.d_first.reserve((nq + 1) * 8, 0, s));  // k_sym_emit writes first[] per chunk
   }
   // k_score_grouped: the tasks of each chunk in the order of their first candidate's replica
   // position (bucket by bucket), DK_TASK_SORT=0: slot order (A/B)
@@ -3124,15 +2828,16 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(hipStreamSynchronize(s));  // h_bounds is reused below
   }
   hipStream_t cs = c->copy_stream;
-  // Chunk ci scores on the main stream; its block-ordered compaction onto the match list and
-  // (host modes) the copy of its entries run on the copy stream, beside the next chunk's
-  // scoring.  Staging set ci&1 is reused by chunk ci+2 once compact_done[ci&1] fired.
+  // Chunk ci scores on the main stream; its block-ordered compaction onto the match list (SYM:
+  // its emission's write pass) and (host modes) the copy of its entries run on the copy
+  // stream, beside the next chunk's scoring.  Staging set ci&1 (SYM: owner-result half ci&1)
+  // is reused by chunk ci+2 once compact_done[ci&1] fired.
   auto compact_chunk = [&](size_t ci) -> int {
     const int b = (int)(ci & 1);
     HIPCHK(hipEventSynchronize(c->count_ready[b]));  // entry count of chunk ci is in hs[]
     const uint64_t nblk = (bounds[ci + 1] - bounds[ci] + kScoreBlock - 1) / kScoreBlock;
     const uint64_t add = hs[4 + 2 * b] + (hs[5 + 2 * b] & 0xFFFFFFFFu);
-    if (add) {
+    if (add || sym) {  // SYM: the write pass also sets the chunk's first[] entries
       const uint64_t need = nm + add;
       // a list that outgrows its buffers is given the whole call's extrapolated size (entries
       // per slot so far x 1.1, at most one per slot): every regrowth copies the list so far
@@ -3141,21 +2846,31 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       const uint64_t want = done < all ? std::max(need, std::min<uint64_t>(all, (uint64_t)((double)need * (double)all / (double)done * 1.1)))
                                        : need;
       auto grow = [&](DevBuf& d, uint64_t el) {
-        return d.reserve((need * el > d.bytes ? want : need) * el, nm * el, cs);
+        return d.reserve(((need + 1) * el > d.bytes ? want + 1 : need + 1) * el, nm * el, cs);
       };
       HIPCHK(grow(B.d_cand, 4));
       HIPCHK(grow(B.d_kind, 1));
       HIPCHK(grow(B.d_prob, 8));
-      HIPCHK(grow(B.d_qidx, 4));
+      if (!sym) HIPCHK(grow(B.d_qidx, 4));
       MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(),
                    B.d_qidx.as<uint32_t>()};
       HIPCHK(hipStreamWaitEvent(cs, c->count_ready[b], 0));
       {
         Timer t_gather(c, &c->prof.ms_gather, cs);
-        HIPCHK(launch_compact(st[b], c->stage[b].boff.as<uint64_t>(), nblk, nm, ml, cs));
+        if (sym) {
+          EmitSource e = esrc;  // chunk ci's owner results: half b, indexed by absolute owner slot
+          const uint64_t o0 = obounds[ci];
+          e.okind = c->okind.as<uint8_t>() + (uint64_t)b * ochunk - o0;
+          e.ores = reinterpret_cast<const double*>(
+              reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - o0 * sizeof(double));
+          HIPCHK(launch_sym_emit(e, bounds[ci], bounds[ci + 1] - bounds[ci], true, nm, ml,
+                                 B.d_first.as<uint64_t>(), cs));
+        } else {
+          HIPCHK(launch_compact(st[b], c->stage[b].boff.as<uint64_t>(), nblk, nm, ml, cs));
+        }
         t_gather.stop();
       }
-      if (!(flags & DK_MATCH_DEVICE)) {
+      if (!(flags & DK_MATCH_DEVICE) && add) {
         uint32_t* hc;
         double* hp;
         uint8_t* hk;
@@ -3198,58 +2913,45 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     for (size_t ci = 0; ci < nchunks; ++ci) maxc = std::max(maxc, bounds[ci + 1] - bounds[ci]);
     if (!sym && !long_sim_buffer(c, PL, maxc)) return fail(DK_E_DEVICE, "long-value DP buffer");
   }
-  // SYM: chunk ci's owner scoring runs on the ctx stream and its emission pass, scan and
-  // count read-back on the emission stream, so emission (latency bound) overlaps the next
-  // chunk's scoring (VALU bound).  Emission of chunk ci reads owner / mirror results of
+  // SYM: chunk ci's owner scoring, its emission's count pass and the scan of the counts run
+  // on the ctx stream; its write pass on the copy stream (compact_chunk) beside chunk ci+1's
+  // scoring.  Emission of chunk ci reads owner results of chunk ci and mirror results of
   // chunks <= ci only: an owner pushes mirror results to candidates after it in bucket
   // order, i.e. to later queries.
-  hipStream_t es = sym && emit_overlap() ? c->emit_stream : s;
   for (size_t ci = 0; ci < nchunks; ++ci) {
     const int b = (int)(ci & 1);
     const uint64_t s0 = bounds[ci], s1 = bounds[ci + 1];
     const uint64_t nblk = (s1 - s0 + kScoreBlock - 1) / kScoreBlock;
+    if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging / half b drained
     if (sym) {
-      // phase 1: the chunk's owner slots, both directions of every owned pair -> ores
+      // phase 1: the chunk's owner slots, both directions of every owned pair -> okind / ores
+      // (half b, indexed by the absolute owner slot o0..o1-1) and the mirror results
       const uint64_t o0 = obounds[ci], o1 = obounds[ci + 1];
-      // DK_SYM_SORT=1: the launch's blocks in bucket order over the XCDs (measured: the same
-      // kernel time, 26.45 vs 26.50 ms per configs[1] step -- VALU-bound, not L2 -- plus the
-      // sort), else launch order
       PairSource osrc = src;
-      // chunk ci's owner results in half b, indexed by the absolute owner slot o0..o1-1
-      double* const oh = reinterpret_cast<double*>(
+      osrc.okind = c->okind.as<uint8_t>() + (uint64_t)b * ochunk - o0;
+      osrc.ores = reinterpret_cast<double*>(
           reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - o0 * sizeof(double));
-      osrc.ores = oh;
-      esrc.ores = oh;
-      // half b was last read by chunk ci-2's emission: on its own stream, wait for it
-      if (es != s && ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->count_ready[b], 0));
-      static const bool sym_sort = getenv("DK_SYM_SORT") && getenv("DK_SYM_SORT")[0] == '1';
-      const uint64_t onb = (o1 - o0 + kScoreBlock - 1) / kScoreBlock;
-      if (sym_sort && onb > 1) {
-        HIPCHK(c->symkey.reserve(2 * onb * 8 + 16, 0, s));
-        HIPCHK(c->symval.reserve(2 * onb * 4 + 16, 0, s));
-        uint64_t* k0 = c->symkey.as<uint64_t>();
-        uint32_t* v0 = c->symval.as<uint32_t>();
-        HIPCHK(launch_sym_block_keys(src, o0, onb, k0, v0, s));
-        HIPCHK(with_tmp(c, [&](void* t, size_t& bytes) {
-          return sort_pairs_u64_u32(t, bytes, k0, k0 + onb, v0, v0 + onb, onb, s);
-        }));
-        osrc.bperm = v0 + onb;
-      }
       {
         Timer t_score(c, &c->prof.ms_score, s);
         HIPCHK(launch_score(P, osrc, o0, o1 - o0, so, s));
         t_score.stop();
       }
       HIPCHK(launch_reduce_blocks(so, (o1 - o0 + kScoreBlock - 1) / kScoreBlock, s));
-      HIPCHK(hipEventRecord(c->score_done, s));
-      // phase 2: the chunk's full slots in Duke's candidate order -> staged entries
-      HIPCHK(hipStreamWaitEvent(es, c->score_done, 0));
-      if (ci >= 2) HIPCHK(hipStreamWaitEvent(es, c->compact_done[b], 0));  // staging b drained
-      Timer t_emit(c, &c->prof.ms_emit, es);
-      HIPCHK(launch_emit(esrc, s0, s1 - s0, st[b], es));
+      // phase 2: entries per query of the chunk, their inclusive scan, the chunk's total
+      EmitSource e = esrc;
+      e.okind = osrc.okind;
+      e.ores = osrc.ores;
+      Timer t_emit(c, &c->prof.ms_emit, s);
+      HIPCHK(launch_sym_emit(e, s0, s1 - s0, false, 0, MatchList{}, nullptr, s));
+      HIPCHK(with_tmp(c, [&](void* t, size_t& bytes) {
+        return inclusive_scan_u32_u64(t, bytes, c->ecount.as<uint32_t>() + s0, c->eincl.as<uint64_t>() + s0,
+                                      s1 - s0, s);
+      }));
+      hs[5 + 2 * b] = 0;
+      HIPCHK(hipMemcpyAsync(&hs[4 + 2 * b], c->eincl.as<uint64_t>() + (s1 - 1), 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipEventRecord(c->count_ready[b], s));
       t_emit.stop();
     } else {
-      if (ci >= 2) HIPCHK(hipStreamWaitEvent(s, c->compact_done[b], 0));  // staging b drained
       {
         Timer t_score(c, &c->prof.ms_score, s);
         if (gq)
@@ -3260,27 +2962,17 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
         t_score.stop();
       }
       HIPCHK(launch_reduce_blocks(st[b], nblk, s));
-    }
-    c->prof.score_launches += 1;
-    {
-      Timer t_gather(c, &c->prof.ms_gather, es);
-      auto scan = [&](void* t, size_t& bytes) {
-        return exclusive_scan_u32_u64(t, bytes, st[b].bcnt, c->stage[b].boff.as<uint64_t>(), nblk, es);
-      };
-      if (sym) {
-        size_t bytes = 0;
-        HIPCHK(scan(nullptr, bytes));
-        HIPCHK(c->etmp.reserve(bytes + 16, 0, es));
-        HIPCHK(scan(c->etmp.p, bytes));
-      } else {
-        HIPCHK(with_tmp(c, scan));
-      }
+      Timer t_gather(c, &c->prof.ms_gather, s);
+      HIPCHK(with_tmp(c, [&](void* t, size_t& bytes) {
+        return exclusive_scan_u32_u64(t, bytes, st[b].bcnt, c->stage[b].boff.as<uint64_t>(), nblk, s);
+      }));
       hs[5 + 2 * b] = 0;
-      HIPCHK(hipMemcpyAsync(&hs[4 + 2 * b], c->stage[b].boff.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost, es));
-      HIPCHK(hipMemcpyAsync(&hs[5 + 2 * b], st[b].bcnt + nblk - 1, 4, hipMemcpyDeviceToHost, es));
-      HIPCHK(hipEventRecord(c->count_ready[b], es));
+      HIPCHK(hipMemcpyAsync(&hs[4 + 2 * b], c->stage[b].boff.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(&hs[5 + 2 * b], st[b].bcnt + nblk - 1, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipEventRecord(c->count_ready[b], s));
       t_gather.stop();
     }
+    c->prof.score_launches += 1;
     // the previous chunk's count is ready once its scan ran (before this chunk's score
     // started): its compaction and copies are issued while this chunk scores
     if (ci > 0) {
@@ -3311,8 +3003,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
 
   // ---- per-query entry offsets, then (DK_MATCH_HOST) the copy into pinned host memory ----
   Timer t_gather(c, &c->prof.ms_gather, s);
-  HIPCHK(B.d_first.reserve((nq + 1) * 8, 0, s));
-  HIPCHK(launch_first(B.d_qidx.as<uint32_t>(), nm, nq, B.d_first.as<uint64_t>(), s));
+  HIPCHK(B.d_first.reserve((nq + 1) * 8, (sym ? nq + 1 : 0) * 8, s));
+  if (!sym) HIPCHK(launch_first(B.d_qidx.as<uint32_t>(), nm, nq, B.d_first.as<uint64_t>(), s));
   R->r.nqueries = nq;
   R->r.n = nm;
   if (!(flags & DK_MATCH_DEVICE) && c->region.base) {
@@ -3464,7 +3156,6 @@ static int set_result_region_impl(dk_ctx* c, void* base, uint64_t bytes, uint64_
     return fail(DK_E_UNSUPPORTED, "a multi-device ctx writes its list into its own host memory");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->copy_stream));
-  HIPCHK(hipStreamSynchronize(c->emit_stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (c->region.base) {
     (void)hipHostUnregister(c->region.base);

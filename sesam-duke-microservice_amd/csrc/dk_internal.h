@@ -177,21 +177,20 @@ struct PairSource {
   // The query OWNS candidates [lo, qa) and (pq, hi): it scores them and, for those that
   // are queries themselves, also the reverse direction; candidates in [qa, pq) are owned
   // by those (earlier) queries.  Owner slot t of a query is its t-th owned candidate over
-  // k; qoff / wq then describe owner slots.  Results: ores[s] = compare(query, cand) of
-  // owner slot s (NaN = filtered); compare(cand, query) goes to the candidate's MIRROR
-  // segment for key k, mres[mbase[k * nq + cand] + (pq - qa)] -- the candidate's mirror
-  // candidates are the bucket positions [qa, pq_cand) in order -- and only when it is a
-  // match / maybe (mres is pre-filled with NaN), so the emission pass reads both kinds of
-  // slots as contiguous runs.
+  // k; qoff / wq then describe owner slots.  Results: okind[s] = the decision (0 none,
+  // DK_KIND_*) of compare(query, cand) at owner slot s and, for an entry, ores[s] = its
+  // probability; compare(cand, query) goes to the candidate's MIRROR segment for key k,
+  // position m = mbase[k * nq + cand] + (pq - qa) -- the candidate's mirror candidates are
+  // the bucket positions [qa, pq_cand) in order -- as mkind[m] / mres[m], written only for
+  // an entry (mkind is cleared per call), so the emission pass (k_sym_emit) reads one
+  // decision byte per candidate from contiguous runs.
   const uint4* sranges;
+  uint8_t* okind;
   double* ores;
+  uint8_t* mkind;
   double* mres;
   const uint64_t* mbase;
   uint32_t r0, r1;
-  // the launch's blocks in bucket order (null: launch order): launch block b runs block
-  // bperm[xcd_slot(b)] -- consecutive sorted blocks on one XCD, so a bucket's replica rows
-  // are re-read from that XCD's L2 (the symmetric schedule's owner launches)
-  const uint32_t* bperm;
 };
 
 constexpr uint32_t kNoPos = 0xFFFFFFFFu;
@@ -283,22 +282,24 @@ struct alignas(16) GQArgs {
 constexpr int kGQQueue = 128;
 constexpr float kScreenLo = 0.011f, kScreenHi = 0.989f;
 
-// The emission pass of the symmetric schedule: slots of the full candidate order (qoff /
-// wq / ranges as in PairSource) read their probability from the owner results.
+// The emission pass of the symmetric schedule (k_sym_emit): per query of a chunk its
+// candidates in Duke's order, each read as a decision byte from the owner results (okind,
+// ores: the chunk's half, indexed by absolute owner slot) or the mirror results (mkind, mres).
 struct EmitSource {
-  const uint32_t* wq;
-  const uint64_t* qoff;
   const uint4* sranges;
   const uint64_t* obase;    // [k * nq + qi]: owner slot of candidate position qa of (k, qi)
   const uint64_t* mbase;    // [k * nq + qi]: mirror slot of candidate position qa of (k, qi)
+  const uint8_t* okind;
   const double* ores;
+  const uint8_t* mkind;
   const double* mres;
   const uint32_t* rowof;
   uint64_t nq;
   int32_t nseg;
-  uint32_t r0;
+  uint32_t pad;
   uint64_t segoff[kMaxSegs];
-  double threshold, maybe;
+  uint32_t* ecount;         // per query: its entries (the count pass)
+  const uint64_t* eincl;    // per query: inclusive prefix of ecount over its chunk's queries
 };
 
 // Per-chunk staging of the score kernel.  Block b (256 slots) writes its emitted entries,
@@ -483,75 +484,6 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
 hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uint64_t slot0,
                                 uint64_t nslots, const uint32_t* perm, const GroupedProp* gp,
                                 int mode, const StageOut& out, hipStream_t s);
-// k_tile (dk_tile.hip): the bucket-tiled schedule of GQArgs schemas.  Buckets are runs of
-// equal range starts in the sorted (range start << 32 | query index) keys of every (segment,
-// query) with candidates; an item is (bucket, chunk of 64 candidates, group of 256 queries).
-constexpr int kTileIdsPerRole = 64;  // per query and QGram role: its keys' dictionary ids
-constexpr uint32_t kTileMaxDict = 4095;  // dictionary ids per role (mask table rows + 1 <= 4096)
-constexpr uint32_t kTileMaxRows = 6144;  // mask-table rows of all roles (48 KB of LDS)
-constexpr uint32_t kTileQueryGroup = 512;  // queries of one item (its chunk's mask table reused)
-// per query (index qi): what k_tile reads of it, in one 64-B record (k_tile_qrec)
-struct TileQRec {
-  uint64_t ident;       // Processor.isSameAs
-  uint64_t key0;        // keys[0] (the duplicate filter)
-  uint16_t len[kGroupedTabs + kGQMaxNum];  // per role (QGram roles, then Numeric): len
-  uint8_t m1[kGroupedTabs];                // QGram roles: grams
-  uint8_t c0[kGroupedTabs];                // QGram roles: first unit
-  uint8_t ok[kGQMaxNum];                   // Numeric roles: parsed
-  uint8_t oc;                              // HashMap order class
-  uint8_t pad[6];
-  double num[kGQMaxNum];
-};
-static_assert(sizeof(TileQRec) == 64, "four 16-B loads");
-struct TileArgs {
-  const uint64_t* bkey;     // sorted keys (the bucket's queries: low 32 bits)
-  const uint32_t* bfirst;   // per bucket: its first key
-  const uint32_t* bnq;      // per bucket: queries
-  const uint32_t* bpos;     // per bucket: first replica position of the range
-  const uint32_t* bseg;     // per bucket: segment
-  const uint32_t* blen;     // per bucket: candidates
-  const uint64_t* bitem;    // per bucket: first item (exclusive prefix), nbuckets + 1
-  const uint32_t* ibucket;  // per item: its bucket
-  uint64_t nbuckets, nitems;
-  const uint16_t* lut[kGroupedTabs];  // per QGram role: bigram key -> dictionary id
-  uint32_t dict[kGroupedTabs];        // ids per role (row dict[a] of its mask table is zero)
-  uint32_t toff[kGroupedTabs];        // first mask-table row of role a
-  uint32_t tsize;                     // mask-table rows (dynamic LDS: 8 B each)
-  const uint16_t* qids;     // [qi][role][kTileIdsPerRole]
-  const TileQRec* qrec;     // [qi]
-  uint64_t* ecount;         // entries appended
-  uint64_t ecap;            // entry capacity (the host re-runs with more past it)
-  uint64_t* ekey;           // query index << 32 | slot t
-  uint32_t* eval;           // entry index (the sort's payload)
-  double* eprob;
-  uint32_t* ecand;          // candidate row | kind << kKindShift
-  uint64_t* counters;       // [0] pairs scored, [1] operand bytes
-  // DK_TILE_CHECK builds (bounds checks that flag instead of faulting): the bounds and the
-  // flag word the host prints under DK_TILE_DEBUG
-  uint64_t nq, nvalid, npos;
-  uint32_t* dbg;
-};
-// planes: 6 (every QGram set of at most 63 grams) or 7
-hipError_t launch_tile(const ScoreParams& P, const PairSource& src, const GQArgs* A, int nq, int nn,
-                       int planes, const TileArgs& T, hipStream_t s);
-hipError_t launch_tile_mark(const uint64_t* grams, uint64_t g0, uint64_t n, uint32_t* present, hipStream_t s);
-hipError_t launch_tile_lut(const uint32_t* scan, uint16_t* lut, hipStream_t s);
-hipError_t launch_tile_qids(const ScoreParams& P, const uint32_t* queries, uint64_t nq, const GQArgs* A,
-                            int nqr, const uint16_t* lut0, const uint16_t* lut1, uint16_t* qids,
-                            hipStream_t s);
-hipError_t launch_tile_qrec(const ScoreParams& P, const PairSource& src, const GQArgs* A, TileQRec* qrec,
-                            hipStream_t s);
-hipError_t launch_tile_bkeys(const PairSource& S, uint64_t* key, uint64_t* nvalid, hipStream_t s);
-hipError_t launch_tile_heads(const uint64_t* key, uint64_t n, uint32_t* head, hipStream_t s);
-hipError_t launch_tile_buckets(const PairSource& S, const uint64_t* key, uint64_t n, uint64_t nvalid,
-                               const uint32_t* head, const uint32_t* bid, uint64_t nb, uint32_t* bfirst,
-                               uint32_t* bpos, uint32_t* bseg, uint32_t* blen, uint32_t* bnq,
-                               uint64_t* nitems, hipStream_t s);
-hipError_t launch_tile_itemmap(const uint64_t* bitem, uint64_t nb, uint64_t nitems, uint32_t* ibucket,
-                               hipStream_t s);
-hipError_t launch_tile_emit(const uint64_t* skey, const uint32_t* sval, uint64_t n, const double* eprob,
-                            const uint32_t* ecand, const MatchList& out, hipStream_t s);
-
 // k_score_gq<nq, nn> (A: device copy of the host's GQArgs, whose nq / nn are passed too)
 hipError_t launch_score_gq(const ScoreParams& P, const PairSource& src, uint64_t slot0, uint64_t nslots,
                            const uint32_t* perm, const GQArgs* A, int nq, int nn, int defer, const StageOut& out,
@@ -567,16 +499,17 @@ hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTab
                             uint64_t* real, hipStream_t s);
 hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint64_t* mqoff,
                         uint64_t nq, int nseg, uint64_t* obase, uint64_t* mbase, hipStream_t s);
-hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, const StageOut& out,
-                       hipStream_t s);
+// k_sym_emit over the chunk's queries [q0, q0 + nqc): write = false counts each query's
+// entries into src.ecount; write = true writes them to `out` from list position base +
+// src.eincl[qi] - src.ecount[qi] on, and first[qi] (the chunk's last query: first[qi + 1] too)
+hipError_t launch_sym_emit(const EmitSource& src, uint64_t q0, uint64_t nqc, bool write, uint64_t base,
+                           const MatchList& out, uint64_t* first, hipStream_t s);
 hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
                              hipStream_t s);
 // out[i] = start + i (a contiguous batch's query rows, written on the device)
 hipError_t launch_iota_u32(uint32_t* out, uint64_t n, uint32_t start, hipStream_t s);
 hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s);
 bool long_dp_split();  // dk_kernels.hip built with DK_LONG_SPLIT (k_long_pre + P.lsim)
-hipError_t launch_sym_block_keys(const PairSource& src, uint64_t slot0, uint64_t nblocks, uint64_t* key,
-                                 uint32_t* val, hipStream_t s);
 hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nblocks,
                           uint64_t base, const MatchList& out, hipStream_t s);
 hipError_t launch_first(const uint32_t* qidx, uint64_t n, uint64_t nq, uint64_t* first,
@@ -596,6 +529,8 @@ hipError_t exclusive_scan_u64(void* tmp, size_t& tmp_bytes, const uint64_t* in, 
 hipError_t exclusive_scan_u32(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint32_t* out,
                               uint64_t n, hipStream_t s);
 hipError_t exclusive_scan_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint64_t* out,
+                                  uint64_t n, hipStream_t s);
+hipError_t inclusive_scan_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint64_t* out,
                                   uint64_t n, hipStream_t s);
 
 }  // namespace dk

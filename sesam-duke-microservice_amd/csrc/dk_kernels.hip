@@ -1177,7 +1177,7 @@ __device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, d
 
 // SYM: the owner slots of the symmetric dedup schedule (PairSource::sym): every owned pair
 // is scored in both directions in one pass and the two probabilities go to S.ores; the
-// emission pass (k_emit) turns them into the match list.
+// emission pass (k_sym_emit) turns them into the match list.
 // LB (long-value DP properties): 0 computed in place; 1 the pre-pass (k_long_pre: only those
 // properties, their similarities to P.lsim, no decisions); 2 read from P.lsim (k_score_long)
 template <int RMAX, int LR, bool SYM, bool DP, bool GR = true, bool GEO = false, int LB = 0, int VI = -1>
@@ -1186,13 +1186,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
   uint64_t* peq = g_wave_tables[threadIdx.x >> 6];
   for (int e = (int)lane_id(); e < kPeqEntries; e += 64) peq[e] = 0;
 
-  // the block this launch block runs: bucket order over the XCDs (S.bperm), or its own
-  uint64_t bid = blockIdx.x;
-  if (S.bperm) {
-    const uint64_t nb = gridDim.x, m = nb / 8;
-    const uint64_t sb = bid < 8 * m ? (bid % 8) * m + bid / 8 : bid;
-    bid = __builtin_amdgcn_readfirstlane(S.bperm[sb]);
-  }
+  const uint64_t bid = blockIdx.x;
   const uint64_t idx = bid * blockDim.x + threadIdx.x;
   const bool in_launch = idx < nslots;
   bool valid = in_launch;
@@ -1382,12 +1376,21 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
 
   if (LB == 1) return;  // the pre-pass: similarities only
   if (SYM) {
-    // owner result for this query's list; the reverse direction into the candidate's mirror
-    // segment (a scattered store while the VALU-bound wave keeps computing) when it will be
-    // an entry -- the rest of that segment keeps its NaN fill
-    if (in_launch) S.ores[s] = valid ? prob : __builtin_nan("");
-    if (mirror && decide(prob2, P.threshold, P.maybe) != 0u)
-      S.mres[S.mbase[(uint64_t)ksel * S.nq + (crow - S.r0)] + moff] = prob2;
+    // the owner decision byte for this query's list (its probability only for an entry); the
+    // reverse direction into the candidate's mirror segment (scattered stores while the
+    // VALU-bound wave keeps computing) when it is an entry -- the rest of that segment keeps
+    // its cleared decision bytes
+    const uint32_t kind = valid ? decide(prob, P.threshold, P.maybe) : 0u;
+    if (in_launch) {
+      S.okind[s] = (uint8_t)kind;
+      if (kind != 0u) S.ores[s] = prob;
+    }
+    const uint32_t kind2 = mirror ? decide(prob2, P.threshold, P.maybe) : 0u;
+    if (kind2 != 0u) {
+      const uint64_t m = S.mbase[(uint64_t)ksel * S.nq + (crow - S.r0)] + moff;
+      S.mkind[m] = (uint8_t)kind2;
+      S.mres[m] = prob2;
+    }
     block_emit_at(out, bid, 0u, 0.0, 0u, qi, valid ? (mirror ? 2u : 1u) : 0u, bytes);  // operands read once
   } else {
     const uint32_t kind = valid ? decide(prob, P.threshold, P.maybe) : 0u;
@@ -1467,77 +1470,118 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_LO
   score_body<64, 16, false, true, true, true>(P, S, slot0, nslots, out);
 }
 
-// Emission pass of the symmetric dedup schedule: the query's slots in Duke's candidate
-// order (key function, then bucket position); each reads its probability from the owner
-// results -- its own (owned candidates) or the candidate's (candidates in [qa, pq), which
-// own the pair) -- and goes through the same thresholds and block-ordered compaction as
-// k_score.  A chain of dependent loads per slot (wave map -> offsets -> bucket record ->
-// owner base -> result): each thread walks kEmitGroups slot groups of 64 with the chains
-// of all groups in flight together, instead of one short-lived wave per group.
-constexpr int kEmitGroups = 4;
+// Emission pass of the symmetric dedup schedule: one wave per query walks
+// its candidates in Duke's order -- per segment k the bucket positions [lo, hi) without
+// its own position pq: [lo, qa) and (pq, hi) it owns (okind / ores at its owner slots),
+// [qa, pq) are owned by the earlier queries there, which pushed their reverse decision to
+// its mirror run (mkind / mres) -- reading one decision byte per candidate, kEmitBatch
+// steps of 64 candidates with their loads issued together (the pass is latency bound).
+// WRITE = false: the query's entries -> ecount[qi].  WRITE = true (after the inclusive scan
+// of the chunk's counts): its entries in order at list position base + eincl[qi] -
+// ecount[qi] on, with their candidate rows and probabilities, and first[qi] (the chunk's
+// last query first[qi + 1] too).  No staging, no compaction and no per-entry query index:
+// the list is written where it ends up.
+constexpr int kEmitBatch = 8;
 
-struct EmitSlot {
-  uint32_t qi, crow;
-  double prob;
-  bool valid;
+struct EmitSeg {
+  uint64_t start;       // first index of the segment in the query's candidate order
+  uint64_t ob, mb, so;  // owner slot / mirror slot of position qa, first replica position
+  uint32_t lo, qa, pq, pad;
 };
 
-__device__ __forceinline__ EmitSlot emit_resolve(const EmitSource& S, uint64_t s, bool valid) {
-  EmitSlot o{0u, 0u, __builtin_nan(""), false};
-  const uint32_t qi = __builtin_amdgcn_readfirstlane(S.wq[s >> 6]);
-  o.qi = qi;
-  uint64_t t = s - S.qoff[qi];
-  int k = -1;
-  uint4 r = make_uint4(0, 0, 0, 0);
-  for (int kk = 0; kk < S.nseg; ++kk) {
-    const uint4 rr = S.sranges[(uint64_t)kk * S.nq + qi];
-    const uint64_t len = (uint64_t)(rr.y - rr.x);
-    if (k < 0) {
-      if (t < len) {
-        k = kk;
-        r = rr;
-      } else {
-        t -= len;
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_sym_emit(const EmitSource S, uint64_t q0, uint64_t nqc,
+                                                  uint64_t base, MatchList out,
+                                                  uint64_t* __restrict__ first) {
+  __shared__ EmitSeg seg[kScoreBlock / 64][kMaxSegs];
+  const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+  const uint64_t wi = (uint64_t)blockIdx.x * (kScoreBlock / 64) + wave;
+  if (wi >= nqc) return;  // wave-uniform; no block barrier follows
+  const uint64_t qi = q0 + wi;
+  const int nseg = S.nseg;
+  EmitSeg* sg = seg[wave];
+  uint64_t len = 0;
+  if ((int)lane < nseg) {  // lane k: segment k's record
+    const uint64_t at = (uint64_t)lane * S.nq + qi;
+    const uint4 r = S.sranges[at];
+    len = (uint64_t)(r.y - r.x) - (r.w != kNoPos ? 1u : 0u);
+    uint64_t so = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxSegs; ++j) so = (int)lane == j ? S.segoff[j] : so;
+    sg[lane].ob = S.obase[at];
+    sg[lane].mb = S.mbase[at];
+    sg[lane].so = so;
+    sg[lane].lo = r.x;
+    sg[lane].qa = r.z;
+    sg[lane].pq = r.w;
+  }
+  uint64_t incl = len;  // inclusive prefix over the segments (lanes past nseg add 0)
+#pragma unroll
+  for (int o = 1; o < kMaxSegs; o <<= 1) {
+    const uint64_t y = __shfl_up(incl, (unsigned)o);
+    if ((int)lane >= o) incl += y;
+  }
+  if ((int)lane < nseg) sg[lane].start = incl - len;
+  const uint64_t tot = __shfl(incl, nseg - 1);
+  const uint64_t L = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tot >> 32)) << 32) |
+                     __builtin_amdgcn_readfirstlane((uint32_t)tot);
+  wave_lds_sync();
+  uint64_t at0 = 0;
+  if (WRITE) at0 = base + S.eincl[qi] - S.ecount[qi];
+  uint64_t n = 0;  // entries so far (wave-uniform)
+  for (uint64_t t0 = 0; t0 < L; t0 += 64 * kEmitBatch) {
+    uint32_t kind[kEmitBatch], pos[kEmitBatch];
+    uint64_t idx[kEmitBatch];
+    bool mir[kEmitBatch];
+#pragma unroll
+    for (int u = 0; u < kEmitBatch; ++u) {
+      const uint64_t t = t0 + (uint64_t)u * 64 + lane;
+      int k = 0;
+      for (int j = 1; j < nseg; ++j) k = t >= sg[j].start ? j : k;
+      const EmitSeg& e = sg[k];
+      uint32_t x = e.lo + (uint32_t)(t - e.start);
+      if (x >= e.pq) ++x;  // past the query's own position (kNoPos: not in the table)
+      const bool m = x >= e.qa && x < e.pq;
+      idx[u] = m ? e.mb + (x - e.qa) : (x < e.qa ? e.ob - (uint64_t)(e.qa - x) : e.ob + (x - e.pq - 1u));
+      mir[u] = m;
+      pos[u] = (uint32_t)(e.so + x);
+      kind[u] = t < L ? (uint32_t)(m ? S.mkind[idx[u]] : S.okind[idx[u]]) : 0u;
+    }
+    if (WRITE) {
+      double pr[kEmitBatch];
+      uint32_t crow[kEmitBatch];
+#pragma unroll
+      for (int u = 0; u < kEmitBatch; ++u) {
+        pr[u] = 0.0;
+        crow[u] = 0u;
+        if (kind[u] != 0u) {
+          pr[u] = mir[u] ? S.mres[idx[u]] : S.ores[idx[u]];
+          crow[u] = S.rowof[pos[u]];
+        }
       }
-    }
-  }
-  valid = valid && k >= 0;
-  if (valid) {
-    const uint32_t x = r.x + (uint32_t)t;
-    o.crow = S.rowof[S.segoff[k] + x];
-    const bool in_t = r.w != kNoPos;
-    if (in_t && x == r.w) {
-      valid = false;  // the query itself (Processor.isSameAs)
-    } else if (in_t && x >= r.z && x < r.w) {
-      // the candidate owns the pair and pushed compare(this query, it) to our mirror run
-      o.prob = S.mres[S.mbase[(uint64_t)k * S.nq + qi] + (x - r.z)];
+#pragma unroll
+      for (int u = 0; u < kEmitBatch; ++u) {
+        const uint64_t em = __ballot(kind[u] != 0u);
+        if (kind[u] != 0u) {
+          const uint64_t o = at0 + n + mask_rank(em);
+          out.cand[o] = crow[u];
+          out.kind[o] = (uint8_t)kind[u];
+          out.prob[o] = pr[u];
+        }
+        n += (uint64_t)__popcll(em);
+      }
     } else {
-      const uint64_t base = S.obase[(uint64_t)k * S.nq + qi];
-      o.prob = S.ores[x < r.z ? base - (r.z - x) : base + (x - r.w - 1)];
+#pragma unroll
+      for (int u = 0; u < kEmitBatch; ++u) n += (uint64_t)__popcll(__ballot(kind[u] != 0u));
     }
   }
-  o.valid = valid;
-  return o;
-}
-
-__global__ __launch_bounds__(256) void k_emit(const EmitSource S, uint64_t slot0, uint64_t nslots,
-                                              StageOut out) {
-  // block b covers kEmitGroups consecutive 256-slot staging blocks; wave w of the block
-  // takes slot group g of each: slots (b * G + g) * 256 + w * 64 + lane
-  EmitSlot e[kEmitGroups];
-#pragma unroll
-  for (int g = 0; g < kEmitGroups; ++g) {
-    const uint64_t idx = ((uint64_t)blockIdx.x * kEmitGroups + g) * kScoreBlock + threadIdx.x;
-    const bool in = idx < nslots;
-    const uint64_t s = slot0 + min(idx, nslots - 1);
-    e[g] = emit_resolve(S, s, in);
-  }
-#pragma unroll
-  for (int g = 0; g < kEmitGroups; ++g) {
-    const uint64_t blk = (uint64_t)blockIdx.x * kEmitGroups + g;
-    if (blk * kScoreBlock >= nslots) break;  // block-uniform: past the chunk's staging blocks
-    const uint32_t kind = e[g].valid ? decide(e[g].prob, S.threshold, S.maybe) : 0u;
-    block_emit_at(out, blk, kind, e[g].prob, e[g].crow, e[g].qi, 0u, 0u);
+  if (lane == 0) {
+    if (!WRITE) {
+      S.ecount[qi] = (uint32_t)n;
+    } else {
+      first[qi] = at0;
+      if (wi + 1 == nqc) first[qi + 1] = at0 + n;
+    }
   }
 }
 
@@ -2325,10 +2369,12 @@ hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint6
   return hipGetLastError();
 }
 
-hipError_t launch_emit(const EmitSource& src, uint64_t slot0, uint64_t nslots, const StageOut& out,
-                       hipStream_t s) {
-  DK_LAUNCH_GUARD(nslots);
-  k_emit<<<grid1d(nslots, kScoreBlock * kEmitGroups), kScoreBlock, 0, s>>>(src, slot0, nslots, out);
+hipError_t launch_sym_emit(const EmitSource& src, uint64_t q0, uint64_t nqc, bool write, uint64_t base,
+                           const MatchList& out, uint64_t* first, hipStream_t s) {
+  DK_LAUNCH_GUARD(nqc);
+  const unsigned grid = grid1d(nqc, kScoreBlock / 64);
+  if (write) k_sym_emit<true><<<grid, kScoreBlock, 0, s>>>(src, q0, nqc, base, out, first);
+  else k_sym_emit<false><<<grid, kScoreBlock, 0, s>>>(src, q0, nqc, base, out, first);
   return hipGetLastError();
 }
 
@@ -2403,26 +2449,6 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
   else DK_SHORT(64);
 #undef DK_SHORT
 #undef DK_LONG
-  return hipGetLastError();
-}
-
-// Sort keys of a symmetric owner launch's blocks (256 owner slots from `slot0`): the
-// position of the block's first query in its first key function's sorted table (its own
-// position, else its bucket's start) -- a bucket's queries are then adjacent.
-__global__ void k_sym_block_keys(const PairSource S, uint64_t slot0, uint64_t nblocks,
-                                 uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
-  const uint32_t qi = S.wq[(slot0 + b * kScoreBlock) >> 6];
-  const uint4 r = S.sranges[qi];
-  key[b] = S.segoff[0] + (r.w != kNoPos ? r.w : r.x);
-  val[b] = (uint32_t)b;
-}
-
-hipError_t launch_sym_block_keys(const PairSource& src, uint64_t slot0, uint64_t nblocks, uint64_t* key,
-                                 uint32_t* val, hipStream_t s) {
-  if (nblocks == 0) return hipSuccess;
-  k_sym_block_keys<<<(unsigned)((nblocks + 255) / 256), 256, 0, s>>>(src, slot0, nblocks, key, val);
   return hipGetLastError();
 }
 
@@ -2511,6 +2537,11 @@ hipError_t exclusive_scan_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* 
                                   uint64_t n, hipStream_t s) {
   return rocprim::exclusive_scan(tmp, tmp_bytes, in, out, (uint64_t)0, (size_t)n,
                                  rocprim::plus<uint64_t>(), s);
+}
+
+hipError_t inclusive_scan_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint64_t* out,
+                                  uint64_t n, hipStream_t s) {
+  return rocprim::inclusive_scan(tmp, tmp_bytes, in, out, (size_t)n, rocprim::plus<uint64_t>(), s);
 }
 
 hipError_t exclusive_scan_u32(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint32_t* out,

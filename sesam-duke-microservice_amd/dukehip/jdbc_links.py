@@ -11,11 +11,26 @@ SELECT of the batch's records' INFERRED links, the per-record rules replayed in 
 batch order, so a later record sees what an earlier one wrote), and one executemany of the
 final row per touched link, in ONE transaction per batch (deduplicate).
 
+Transactions: the writer holds a connection of its own beside the link database's (Duke's
+JDBCLinkDatabase, `primary` here), through which the routes keep writing outside a batch --
+the deleted records' link retractions (App.java:994-999) go through it before deduplicate
+runs.  Opening the listener window (set_listener_window(True), GpuProcessor before
+batchReady) commits the primary connection's pending writes first, so this connection's
+SELECT sees them and its upserts never wait on their row locks; inside the window the
+primary connection writes nothing (the listener's writes are dropped).
+
+A stored ASSERTED link (a manual one) is never overwritten by the batch's INFERRED links or
+retractions: [Duke 1.2, recalled] JDBCLinkDatabase.assertLink keeps a row whose status is
+ASSERTED when the new link's is not (Link.overrides), and the listener retracts only
+INFERRED links.
+
 PARITY UNPINNED against Duke's table: JDBCLinkDatabase is in the absent Duke 1.2 jar, so the
 layout below (table `links`, columns id1 / id2 / kind / status / perhaps / timestamp, key
-(id1, id2), assertLink = update-or-insert of that row) is recalled.  Tested against the
-per-callback stream over the same layout (tests/test_jdbc_links.py, oracle/linkdb_ref.py).
-Works on any DB-API connection whose paramstyle is qmark (sqlite3 in the tests).
+(id1, id2), assertLink = update-or-insert of that row unless the stored one is ASSERTED) is
+recalled.  Tested against the per-callback stream over the same layout
+(tests/test_jdbc_links.py, oracle/linkdb_ref.py).  The statements are SQLite's (`insert or
+ignore`, `create temp table`, `on conflict ... do update`): this module drives sqlite3
+connections; the Java writer uses H2's `merge ... key` forms for the same steps.
 """
 from __future__ import annotations
 
@@ -26,7 +41,7 @@ TABLE = "links"
 CREATE = (f"create table if not exists {TABLE} (id1 varchar(200) not null, id2 varchar(200) not null, "
           "kind int not null, status int not null, perhaps float, timestamp bigint not null, "
           "primary key (id1, id2))")
-INFERRED, RETRACTED = 1, 2     # the sink's codes (dukehip.links); the Java side uses Duke's ids
+INFERRED, RETRACTED, ASSERTED = 1, 2, 3   # the sink's codes (dukehip.links); Java: Duke's ids
 SAME, MAYBE = 1, 2
 
 
@@ -40,26 +55,35 @@ def link_key(a, b):
 
 
 class JdbcBulkLinkWriter:
-    def __init__(self, conn, upsert=None):
-        """conn: a DB-API connection holding the link table (created if missing).  upsert:
-        the update-or-insert statement (default: SQLite / H2 'merge' forms)."""
-        self.conn = conn
+    def __init__(self, conn, primary=None, upsert=None):
+        """conn: this writer's sqlite3 connection to the link table (created if missing).
+        primary: the link database's own connection, whose pending writes the listener window
+        commits when it opens.  upsert: the update-or-insert statement."""
+        self.conn, self.primary = conn, primary
         conn.execute(CREATE)
+        conn.commit()
         self.upsert = upsert or (f"insert into {TABLE} (id1, id2, kind, status, perhaps, timestamp) "
                                  "values (?, ?, ?, ?, ?, ?) on conflict (id1, id2) do update set "
                                  "kind = excluded.kind, status = excluded.status, "
                                  "perhaps = excluded.perhaps, timestamp = excluded.timestamp")
         self.statements = 0     # SQL statements of the last batch (bulk: a handful)
+        self.window = False
 
-    def _inferred_links_of(self, ids):
-        """The INFERRED links touching any of `ids`: {key: [kind, status, perhaps, ts]}."""
+    def set_listener_window(self, open_):
+        """GpuProcessor around a batch (GpuJdbcLinkDatabase.setListenerWindow): opening it
+        commits the link database's pending writes (the routes' retractions)."""
+        if open_ and self.primary is not None:
+            self.primary.commit()
+        self.window = open_
+
+    def _links_of(self, ids):
+        """The stored links touching any of `ids`: {key: [kind, status, perhaps, ts]}."""
         cur = self.conn.cursor()
         cur.execute("create temp table if not exists dk_batch_ids (id varchar(200) primary key)")
         cur.execute("delete from dk_batch_ids")
         cur.executemany("insert or ignore into dk_batch_ids values (?)", [(i,) for i in ids])
-        cur.execute(f"select id1, id2, kind, status, perhaps, timestamp from {TABLE} where status = ? "
-                    "and (id1 in (select id from dk_batch_ids) or id2 in (select id from dk_batch_ids))",
-                    (INFERRED,))
+        cur.execute(f"select id1, id2, kind, status, perhaps, timestamp from {TABLE} where "
+                    "id1 in (select id from dk_batch_ids) or id2 in (select id from dk_batch_ids)")
         out = {(a, b): [k, s, p, t] for a, b, k, s, p, t in cur.fetchall()}
         self.statements = 4
         return out
@@ -67,7 +91,7 @@ class JdbcBulkLinkWriter:
     def apply(self, query_ids, first, candidate_ids, prob, kind, timestamp):
         """One batch's match list: query record i (ID query_ids[i]) has entries
         first[i] .. first[i+1]-1 (candidate ID, probability, SAME / MAYBE), in batch order."""
-        state = self._inferred_links_of(set(query_ids))
+        state = self._links_of(set(query_ids))
         by_id = {}
         for k in state:
             by_id.setdefault(k[0], set()).add(k)
@@ -87,6 +111,8 @@ class JdbcBulkLinkWriter:
                 state[k] = row
                 final[k] = row
             for k, row in cur.items():
+                if k in state and state[k][1] == ASSERTED:
+                    continue    # a manual link stays (Link.overrides)
                 state[k] = row
                 final[k] = row
                 by_id.setdefault(k[0], set()).add(k)

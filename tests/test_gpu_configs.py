@@ -102,22 +102,21 @@ def test_reference_schema_dedup_gpu():
 # configs[2] (QGram DICE/JACCARD + Numeric min-ratio 0.9, cross-group key blocking) and
 # configs[4] (WeightedLevenshtein + QGram q=3 JACCARD, key = first two tokens) in linkage
 # ---------------------------------------------------------------------------------------
-@pytest.mark.parametrize("variant", ["default", "gq_defer1", "gq_nodefer", "gq_noscreen", "tile",
+@pytest.mark.parametrize("variant", ["default", "gq_defer1", "gq_nodefer", "gq_noscreen",
                                      "legacy_grouped", "tail_resource", "row_resources",
                                      "no_grouped", "host_grams"])
 def test_config2_linkage_qgram_numeric(variant, monkeypatch):
     """configs[2]'s schema through each of its device paths, bit-exact against the oracle:
     k_score_gq (default: the screen with QGram role 0 deferred to the exact pass; role 1
     deferred; no role deferred; no screen -- every valid pair takes the exact pass; its head /
-    tail row resources are the layout a 10M x 10M replica takes, at any size), the
-    bucket-tiled k_tile (DK_TILE=1), k_score_grouped (DK_GQ=0) with one buffer resource per
+    tail row resources are the layout a 10M x 10M replica takes, at any size),
+    k_score_grouped (DK_GQ=0) with one buffer resource per
     property, with head and tail resources (DK_GROUPED_ROW=1) or a resource per tail row
     (DK_GROUPED_ROW=2: replicas past k_score_gq's resources), k_score_nodp (DK_GROUPED=0),
     and q-gram sets built on the host instead of the device (DK_DEV_GRAMS=0)."""
     env = {"gq_defer1": [("DK_GQ_DEFER", "1")],
            "gq_nodefer": [("DK_GQ_DEFER", "-1")],
            "gq_noscreen": [("DK_GQ_SCREEN", "0")],
-           "tile": [("DK_TILE", "1")],
            "legacy_grouped": [("DK_GQ", "0")],
            "tail_resource": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "1")],
            "row_resources": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "2")],
@@ -606,16 +605,15 @@ def test_symmetric_schedule_equals_direct(seed, monkeypatch):
     upsert_slice(eng, vals, keys, ident, 1500, n, deleted)
     ot = O.OracleTable(props, vals, keys=keys, ident=ident, deleted=deleted,
                        alive=alive_after(list(ident), n), threshold=0.75, maybe=0.55)
-    # the mirror results' NaN fill is restored by each call's emission passes and carried to
-    # the next call: shrinking then growing query sets on one engine
+    # the mirror decision bytes are cleared per call: shrinking then growing query sets on
+    # one engine, one chunk or many (every chunk's write pass sets its queries' first[])
     for q in (np.arange(n, dtype=np.uint32), np.arange(700, 1900, dtype=np.uint32),
               np.arange(1500, n, dtype=np.uint32), np.arange(n, dtype=np.uint32)):
-        for chunk, overlap in ((None, "0"), ("3000", "0"), ("3000", "1")):
+        for chunk in (None, "3000", "512"):
             if chunk:
                 monkeypatch.setenv("DK_CHUNK_SLOTS", chunk)
             else:
                 monkeypatch.delenv("DK_CHUNK_SLOTS", raising=False)
-            monkeypatch.setenv("DK_EMIT_OVERLAP", overlap)   # emission on its own stream
             eng.reset_profile()
             eng.set_profiling(True)
             res = eng.match(q)

@@ -608,17 +608,16 @@ def test_order_classes_wide_schema(mode):
     assert not (np.array_equal(flat.candidate, res.candidate) and np.array_equal(flat.prob, res.prob))
 
 
-@pytest.mark.parametrize("variant", ["gq", "grouped", "grouped_row1", "grouped_row2", "tile"])
+@pytest.mark.parametrize("variant", ["gq", "grouped", "grouped_row1", "grouped_row2"])
 def test_order_classes_grouped(variant, monkeypatch):
     """the order classes through the grouped kernels -- two bigram QGram and three
     Numeric properties (k_score_gq's roles; k_score_grouped with DK_GQ=0, its head / tail
-    and per-row resources with DK_GROUPED_ROW=1 / 2; k_tile with DK_TILE=1) in records of
+    and per-row resources with DK_GROUPED_ROW=1 / 2) in records of
     more than 12 keys (the unscored columns count), each row in its HashMap capacity's class,
     bit-exact against the oracle fed the same classes; the two classes' orders differ."""
     from dukehip import config as cfgmod
     env = {"grouped": [("DK_GQ", "0")], "grouped_row1": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "1")],
-           "grouped_row2": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "2")],
-           "tile": [("DK_TILE", "1")]}.get(variant, [])
+           "grouped_row2": [("DK_GQ", "0"), ("DK_GROUPED_ROW", "2")]}.get(variant, [])
     for kv in env:
         monkeypatch.setenv(*kv)
     rng = random.Random(23)
