@@ -2595,6 +2595,9 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
         if (e - a >= 2) qb.insert(qb.end() - 1, a + (e - a) / 2);
       }
     }
+    // more chunks than queries (small slot chunks): no empty chunk -- its count read-back
+    // would be the previous query's inclusive prefix
+    qb.erase(std::unique(qb.begin(), qb.end()), qb.end());
     const uint64_t nb = qb.size();
     HIPCHK(c->bidx.reserve(nb * 8 + 8, 0, s));
     HIPCHK(c->bval.reserve(nb * 8 + 8, 0, s));
@@ -2758,6 +2761,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     for (int k = 0; k < T.nseg; ++k) esrc.segoff[k] = T.seg_off[k];
     esrc.ecount = c->ecount.as<uint32_t>();
     esrc.eincl = c->eincl.as<uint64_t>();
+    esrc.oqoff = c->oqoff.as<uint64_t>();
+    esrc.mqoff = c->mqoff.as<uint64_t>();
     HIPCHK(B.d_first.reserve((nq + 1) * 8, 0, s));  // k_sym_emit writes first[] per chunk
   }
   // k_score_grouped: the tasks of each chunk in the order of their first candidate's replica
@@ -2854,20 +2859,25 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       if (!sym) HIPCHK(grow(B.d_qidx, 4));
       MatchList ml{B.d_cand.as<uint32_t>(), B.d_kind.as<uint8_t>(), B.d_prob.as<double>(),
                    B.d_qidx.as<uint32_t>()};
-      HIPCHK(hipStreamWaitEvent(cs, c->count_ready[b], 0));
-      {
+      if (sym) {
+        // the write pass on the ctx stream, behind chunk ci+1's scoring (the host waited for
+        // chunk ci's count above, which the device reached before that scoring started): the
+        // latency-bound pass never shares the CUs with k_score, and the stream never idles
+        Timer t_gather(c, &c->prof.ms_gather, s);
+        EmitSource e = esrc;  // chunk ci's owner results: half b, indexed by absolute owner slot
+        const uint64_t o0 = obounds[ci];
+        e.okind = c->okind.as<uint8_t>() + (uint64_t)b * ochunk - o0;
+        e.ores = reinterpret_cast<const double*>(
+            reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - o0 * sizeof(double));
+        HIPCHK(launch_sym_emit(e, bounds[ci], bounds[ci + 1] - bounds[ci], true, nm, ml,
+                               B.d_first.as<uint64_t>(), s));
+        t_gather.stop();
+        HIPCHK(hipEventRecord(c->compact_done[b], s));
+        HIPCHK(hipStreamWaitEvent(cs, c->compact_done[b], 0));  // the copies below
+      } else {
+        HIPCHK(hipStreamWaitEvent(cs, c->count_ready[b], 0));
         Timer t_gather(c, &c->prof.ms_gather, cs);
-        if (sym) {
-          EmitSource e = esrc;  // chunk ci's owner results: half b, indexed by absolute owner slot
-          const uint64_t o0 = obounds[ci];
-          e.okind = c->okind.as<uint8_t>() + (uint64_t)b * ochunk - o0;
-          e.ores = reinterpret_cast<const double*>(
-              reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - o0 * sizeof(double));
-          HIPCHK(launch_sym_emit(e, bounds[ci], bounds[ci + 1] - bounds[ci], true, nm, ml,
-                                 B.d_first.as<uint64_t>(), cs));
-        } else {
-          HIPCHK(launch_compact(st[b], c->stage[b].boff.as<uint64_t>(), nblk, nm, ml, cs));
-        }
+        HIPCHK(launch_compact(st[b], c->stage[b].boff.as<uint64_t>(), nblk, nm, ml, cs));
         t_gather.stop();
       }
       if (!(flags & DK_MATCH_DEVICE) && add) {
@@ -2903,7 +2913,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       }
       nm = need;
     }
-    HIPCHK(hipEventRecord(c->compact_done[b], cs));
+    if (!sym) HIPCHK(hipEventRecord(c->compact_done[b], cs));
     return DK_OK;
   };
   const size_t nchunks = bounds.size() - 1;

@@ -300,6 +300,8 @@ struct EmitSource {
   uint64_t segoff[kMaxSegs];
   uint32_t* ecount;         // per query: its entries (the count pass)
   const uint64_t* eincl;    // per query: inclusive prefix of ecount over its chunk's queries
+  const uint64_t* oqoff;    // per query: first owner slot (its owned run: up to oqoff[qi + 1])
+  const uint64_t* mqoff;    // per query: first mirror slot (its mirror runs: up to mqoff[qi + 1])
 };
 
 // Per-chunk staging of the score kernel.  Block b (256 slots) writes its emitted entries,
