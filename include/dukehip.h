@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DK_ABI_VERSION 8
+#define DK_ABI_VERSION 9
 
 /* status codes */
 #define DK_OK 0
@@ -181,14 +181,15 @@ typedef struct dk_profile {
   double ms_index;        /* blocking-table build (sort, segments) */
   double ms_generate;     /* candidate counting + pair emission */
   double ms_score;        /* fused scoring kernels (the dominant kernel) */
-  double ms_gather;       /* match compaction sort + device->host copy */
+  double ms_gather;       /* match compaction (symmetric schedule: the emission's write
+                             pass) + device->host copy */
   double ms_total;        /* wall time of dk_match */
   uint64_t score_launches;
   uint64_t pairs_scored;
   uint64_t pairs_generated;
   uint64_t score_bytes;   /* algorithmic operand bytes of the scored pairs */
   double ms_copy;         /* device->host copies of the match list (copy stream, overlapped) */
-  double ms_emit;         /* symmetric dedup schedule: the emission pass (k_emit) */
+  double ms_emit;         /* symmetric dedup schedule: the emission's count pass + scan */
   uint64_t sym_matches;   /* dk_match calls that ran the symmetric dedup schedule */
   uint64_t full_builds;   /* blocking-table builds that sorted every usable row */
   uint64_t delta_builds;  /* builds that re-sorted only the rows added since the last full
@@ -197,6 +198,8 @@ typedef struct dk_profile {
   uint64_t gram_row_bytes;    /* and the bytes of its largest QGram property's key-word rows
                                  (rows x positions x 8; past 4 GiB the grouped kernels address
                                  them through head / tail buffer resources) */
+  uint64_t sym2_matches;  /* symmetric dedup calls with two queries per wave (k_score_sym2:
+                             owner slots padded to 32; ABI 9) */
 } dk_profile;
 
 typedef struct dk_ctx dk_ctx;

@@ -848,6 +848,7 @@ int dk_get_profile(const dk_ctx* c, dk_profile* out) {
       t.pairs_generated += p.pairs_generated;
       t.score_bytes += p.score_bytes;
       t.sym_matches += p.sym_matches;
+      t.sym2_matches += p.sym2_matches;
       t.full_builds += p.full_builds;
       t.delta_builds += p.delta_builds;
       t.replica_positions = std::max(t.replica_positions, p.replica_positions);
@@ -2239,6 +2240,23 @@ static int ensure_tables(dk_ctx* c, BlockTables* Tout, uint64_t* Mout) {
   return DK_OK;
 }
 
+// k_score_sym2 (two queries per wave, owner slots padded to 32): schemas whose Levenshtein /
+// JaroWinkler / Exact columns are Latin-1 (the wave's two 256-entry Peq tables fill its LDS
+// slice), with a DP comparator and no gram sets; DK_SYM2=0 keeps one query per wave (A/B)
+static bool sym2_ok(const dk_ctx* c, const ScoreParams& P) {
+  const char* e = getenv("DK_SYM2");
+  if ((e && e[0] == '0') || !P.has_dp || P.has_grams || P.has_geo || P.norders > 1) return false;
+  for (int p = 0; p < P.nprops; ++p) {
+    const DevProp& D = P.props[p];
+    if (D.op != DK_CMP_LEVENSHTEIN && D.op != DK_CMP_JAROWINKLER && D.op != DK_CMP_EXACT &&
+        D.op != DK_CMP_NUMERIC && D.op != DK_CMP_NONE)
+      return false;
+    if ((D.op == DK_CMP_LEVENSHTEIN || D.op == DK_CMP_JAROWINKLER || D.op == DK_CMP_EXACT) && D.width != 1)
+      return false;
+  }
+  return true;
+}
+
 static bool sym_enabled() {
   const char* e = getenv("DK_SYM");
   return !(e && e[0] == '0');
@@ -2533,6 +2551,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     if (P.props[p].op == DK_CMP_QGRAM)
       c->prof.gram_row_bytes = std::max(c->prof.gram_row_bytes, (uint64_t)P.props[p].rgrows * P.rstride * 8);
   bool sym = !lucene && contiguous && nq > 0 && sym_enabled() && sym_schema_ok(c, P);
+  const bool two = sym && sym2_ok(c, P);  // k_score_sym2: half-wave queries
   bool grouped = false;  // k_score_grouped: query slots padded to kScoreBlock
   const uint32_t r0 = nq ? query_rows[0] : 0;
   uint64_t* hs = c->h_small.as<uint64_t>();
@@ -2547,7 +2566,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
     HIPCHK(launch_count_sym(c->d_queries.as<uint32_t>(), nq, T, r0, c->ranges.as<uint4>(),
                             c->counts.as<uint64_t>(), c->ocounts.as<uint64_t>(),
-                            c->mcounts.as<uint64_t>(), c->counters.as<uint64_t>() + 2, s));
+                            c->mcounts.as<uint64_t>(), c->counters.as<uint64_t>() + 2, two ? 32u : 64u, s));
     HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->ocounts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->mcounts.as<uint64_t>() + nq, 0, 8, s));
@@ -2631,9 +2650,9 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(c->eincl.reserve(nq * 8 + 8, 0, s));
     HIPCHK(c->mbase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
     HIPCHK(hipMemsetAsync(c->mkind.p, 0, mtot, s));  // no entry unless an owner pushes one
-    HIPCHK(c->owq.reserve(otot / 64 * 4 + 4, 0, s));
+    HIPCHK(c->owq.reserve(otot / 32 * 4 + 4, 0, s));
     HIPCHK(c->obase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
-    HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s));
+    HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s, two ? 5 : 6));
     HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), c->mqoff.as<uint64_t>(),
                         nq, T.nseg, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
   } else if (!allpairs && !lucene) {
@@ -2742,6 +2761,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   if (sym) {
     // owner slots: phase 1 scores them (okind / ores), the emission pass walks the queries
     src.sym = 1;
+    src.two = two ? 1 : 0;
     src.wq = c->owq.as<uint32_t>();
     src.qoff = c->oqoff.as<uint64_t>();
     src.sranges = c->ranges.as<uint4>();
@@ -3005,6 +3025,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   const uint64_t scored = c->h_small.as<uint64_t>()[0];
   const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
   if (sym) c->prof.sym_matches += 1;
+  if (sym && two) c->prof.sym2_matches += 1;
   R->r.pairs_scored = scored;
   R->r.pairs_generated = generated;
   c->prof.pairs_scored += scored;

@@ -170,6 +170,7 @@ struct PairSource {
   uint64_t mpad;            // m rounded up to a wave (64)
   int32_t same_ok;          // score pairs of one identity too (dk_compare_rows)
   int32_t sym;              // 1: owner slots of the symmetric dedup schedule (below)
+  int32_t two;              // SYM: owner slots padded to 32, wq per half-wave (k_score_sym2)
   // Symmetric dedup schedule: queries are the contiguous rows [r0, r1);
   // per (key function k, query qi) sranges[k * nq + qi] = {lo, hi, qa, pq}: the bucket
   // [lo, hi) of the query's key in sorted table k, qa = first position with row >= r0,
@@ -472,7 +473,8 @@ hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables&
 hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockTables& T,
                               uint2* ranges, uint64_t* counts, hipStream_t s);
 // wq[w] = qi for the waves of query qi's slots (qoff in slots, multiples of 64)
-hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s);
+// wq[w] = qi for every group w of 2^shift slots of query qi (shift 6: waves, 5: half-waves)
+hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s, int shift = 6);
 // replica-ordered identity and keys 0..nkeys-2 of the rows at replica positions
 hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t pos0, uint64_t npos,
                                  const uint64_t* ident, uint64_t* rident, const BlockTables& T,
@@ -498,7 +500,7 @@ hipError_t launch_task_keys(const PairSource& src, uint64_t ntask, const uint64_
 // counts (each padded to 64), real[0] += the unpadded full total
 hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
                             uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* mcounts,
-                            uint64_t* real, hipStream_t s);
+                            uint64_t* real, uint32_t opad, hipStream_t s);
 hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint64_t* mqoff,
                         uint64_t nq, int nseg, uint64_t* obase, uint64_t* mbase, hipStream_t s);
 // k_sym_emit over the chunk's queries [q0, q0 + nqc): write = false counts each query's

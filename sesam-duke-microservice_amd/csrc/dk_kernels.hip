@@ -170,7 +170,9 @@ __device__ __forceinline__ uint32_t pk_min3_u16(uint32_t a, uint32_t b, uint32_t
 // a cutoff, D(n1, n2) when the lane reaches its last column), as stated above; the raw
 // similarity of a cut-off pair comes from k_lev_exact.
 // ------------------------------------------------------------------------------------
-template <int R, typename CT>
+// PERLANE (k_score_sym2: two queries per wave): n1 differs between the wave's halves and
+// may lie anywhere in (0, R]; the result row is then looked up among all R rows.
+template <int R, typename CT, bool PERLANE = false>
 __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, const Str<CT>& s2,
                                                    int n2, bool act) {
   constexpr int UPW = Str<CT>::UPW;
@@ -239,9 +241,13 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
         live = false;
       } else if (t == fin) {
         uint32_t r = 0;
+        // PERLANE: n1 through an opaque copy, so the R row compares are made here (once per
+        // lane) rather than hoisted out of the column loop as R live lane masks
+        int nr = n1;
+        if (PERLANE) asm volatile("" : "+v"(nr));
 #pragma unroll
-        for (int row = R - TAIL + 1; row <= R; ++row)
-          if (row == n1) r = row <= H ? (Pout[row] & 0xFFFFu) : (Pout[row - H] >> 16);
+        for (int row = PERLANE ? 1 : R - TAIL + 1; row <= R; ++row)
+          if (row == nr) r = row <= H ? (Pout[row] & 0xFFFFu) : (Pout[row - H] >> 16);
         result = (int)(r - B);
         live = false;
       }
@@ -270,9 +276,11 @@ __device__ __forceinline__ int compact_distance_pp(const uint64_t* peq, int n1, 
 // [Duke 1.2] comparators.Levenshtein.compare.  RMAX: the largest row bucket this kernel
 // variant instantiates (the host picks the variant from the longest Levenshtein value),
 // which bounds the VGPRs of the whole fused kernel and so its occupancy.
-template <int RMAX, typename CT>
+// PERLANE: n1 per lane (k_score_sym2), `nsel` (wave-uniform, >= every lane's n1) picks the
+// row bucket
+template <int RMAX, typename CT, bool PERLANE = false>
 __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str<CT>& s1, int n1,
-                                                  const Str<CT>& s2, int n2, bool act) {
+                                                  const Str<CT>& s2, int n2, bool act, int nsel = 0) {
   const int len = min(n1, n2);
   const int maxlen = max(n1, n2);
   double r = 0.0;
@@ -286,31 +294,34 @@ __device__ __forceinline__ double levenshtein_peq(const uint64_t* peq, const Str
   // row buckets of 2 up to 16 rows (a date "YYYY-MM-DD" takes 10 rows, not 12), of 4 up to
   // 32, of 8 above (n1 is wave-uniform: a scalar switch)
   int d;
-  if (n1 <= 16) {
-    switch ((n1 + 1) >> 1) {
-      case 1: case 2: d = compact_distance_pp<4>(peq, n1, s2, n2, run); break;
-      case 3: d = compact_distance_pp<6>(peq, n1, s2, n2, run); break;
-      case 4: d = compact_distance_pp<8>(peq, n1, s2, n2, run); break;
-      case 5: d = compact_distance_pp<10>(peq, n1, s2, n2, run); break;
-      case 6: d = compact_distance_pp<12>(peq, n1, s2, n2, run); break;
-      case 7: d = compact_distance_pp<14>(peq, n1, s2, n2, run); break;
-      default: d = compact_distance_pp<16>(peq, n1, s2, n2, run); break;
+  const int ns = PERLANE ? nsel : n1;
+#define DK_CD(R_) compact_distance_pp<R_, CT, PERLANE>(peq, n1, s2, n2, run)
+  if (ns <= 16) {
+    switch ((ns + 1) >> 1) {
+      case 1: case 2: d = DK_CD(4); break;
+      case 3: d = DK_CD(6); break;
+      case 4: d = DK_CD(8); break;
+      case 5: d = DK_CD(10); break;
+      case 6: d = DK_CD(12); break;
+      case 7: d = DK_CD(14); break;
+      default: d = DK_CD(16); break;
     }
   } else
-  switch ((n1 + 3) >> 2) {
-    case 1: d = compact_distance_pp<4>(peq, n1, s2, n2, run); break;
-    case 2: d = compact_distance_pp<8>(peq, n1, s2, n2, run); break;
-    case 3: d = compact_distance_pp<12>(peq, n1, s2, n2, run); break;
-    case 4: d = compact_distance_pp<16>(peq, n1, s2, n2, run); break;
-    case 5: d = compact_distance_pp<20>(peq, n1, s2, n2, run); break;
-    case 6: d = compact_distance_pp<24>(peq, n1, s2, n2, run); break;
-    case 7: d = compact_distance_pp<28>(peq, n1, s2, n2, run); break;
-    case 8: d = compact_distance_pp<32>(peq, n1, s2, n2, run); break;
-    case 9: case 10: d = compact_distance_pp<(RMAX < 40 ? 4 : 40)>(peq, n1, s2, n2, run); break;
-    case 11: case 12: d = compact_distance_pp<(RMAX < 48 ? 4 : 48)>(peq, n1, s2, n2, run); break;
-    case 13: case 14: d = compact_distance_pp<(RMAX < 56 ? 4 : 56)>(peq, n1, s2, n2, run); break;
-    default: d = compact_distance_pp<(RMAX < 64 ? 4 : 64)>(peq, n1, s2, n2, run); break;
+  switch ((ns + 3) >> 2) {
+    case 1: d = DK_CD(4); break;
+    case 2: d = DK_CD(8); break;
+    case 3: d = DK_CD(12); break;
+    case 4: d = DK_CD(16); break;
+    case 5: d = DK_CD(20); break;
+    case 6: d = DK_CD(24); break;
+    case 7: d = DK_CD(28); break;
+    case 8: d = DK_CD(32); break;
+    case 9: case 10: d = DK_CD((RMAX < 40 ? 4 : 40)); break;
+    case 11: case 12: d = DK_CD((RMAX < 48 ? 4 : 48)); break;
+    case 13: case 14: d = DK_CD((RMAX < 56 ? 4 : 56)); break;
+    default: d = DK_CD((RMAX < 64 ? 4 : 64)); break;
   }
+#undef DK_CD
   if (run) {
     const int dist = min(d, len);
     r = 1.0 - ((double)dist / (double)len);
@@ -1409,6 +1420,194 @@ void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t n
   score_body<RMAX, 0, SYM, true, GR>(P, S, slot0, nslots, out);
 }
 
+// The symmetric owner schedule with TWO queries per wave (PairSource::two): every query's
+// owner slots are padded to 32, not 64, so each half-wave holds one query and a wave at most
+// two -- configs[1]'s owned lists waste 6.7 % of their slots on padding instead of 13.3 %.
+// Schemas of Latin-1 Levenshtein / JaroWinkler, Exact and Numeric properties in one HashMap
+// order class (the host checks: dk_api.cpp sym2_ok): the wave's two Peq tables fit its LDS
+// slice (256 entries each), the row bucket covers the longer query value, and the query side
+// of every comparator is per lane (its half's query); the rest is score_body's SYM path.
+template <int RMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? DK_WAVES_SHORT : 4, 8)))
+void k_score_sym2(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
+  uint64_t* tab = g_wave_tables[threadIdx.x >> 6];
+  for (int e = (int)lane_id(); e < kPeqEntries; e += 64) tab[e] = 0;
+  const int lane = (int)lane_id();
+  const bool hi = lane >= 32;
+  const uint64_t bid = blockIdx.x;
+  const uint64_t idx = bid * blockDim.x + threadIdx.x;
+  const bool in_launch = idx < nslots;
+  bool valid = in_launch;
+  const uint64_t s = slot0 + min(idx, nslots - 1);
+  // the two half-waves' queries (scalar loads; equal when one query fills the wave)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t w0 = bid * blockDim.x + (uint64_t)wave * 64u;
+  const uint32_t qiA = __builtin_amdgcn_readfirstlane(S.wq[(slot0 + min(w0, nslots - 1)) >> 5]);
+  const uint32_t qiB = __builtin_amdgcn_readfirstlane(S.wq[(slot0 + min(w0 + 32u, nslots - 1)) >> 5]);
+  const bool two = qiA != qiB;  // wave-uniform
+  const uint32_t qA = __builtin_amdgcn_readfirstlane(S.queries[qiA]);
+  const uint32_t qB = __builtin_amdgcn_readfirstlane(S.queries[qiB]);
+  const uint32_t q = hi ? qB : qA;
+  uint64_t* peq = tab + (two && hi ? 256 : 0);  // this lane's query's Peq table
+  uint32_t g = 0;
+  bool mirror = false;
+  int ksel = 0;
+  uint32_t moff = 0;
+  {
+    // owner slot t of the lane's query: key function k's owned range [lo, qa) then (pq, hi)
+    uint64_t t = s - (hi ? S.qoff[qiB] : S.qoff[qiA]);
+    int k = -1;
+    constexpr int kPre = 2;  // the two queries' first ranges as scalars (SGPR budget)
+    uint4 pa[kPre], pb[kPre];
+#pragma unroll
+    for (int kk = 0; kk < kPre; ++kk) {
+      const uint64_t at = (uint64_t)min(kk, S.nseg - 1) * S.nq;
+      pa[kk] = S.sranges[at + qiA];
+      pb[kk] = S.sranges[at + qiB];
+    }
+#pragma unroll
+    for (int kk = 0; kk < kMaxSegs; ++kk) {
+      if (kk >= S.nseg) break;  // wave-uniform
+      const uint4 ra = kk < kPre ? pa[kk < kPre ? kk : 0] : S.sranges[(uint64_t)kk * S.nq + qiA];
+      const uint4 rb = kk < kPre ? pb[kk < kPre ? kk : 0] : S.sranges[(uint64_t)kk * S.nq + qiB];
+      const uint4 r = hi ? rb : ra;
+      const bool in_t = r.w != kNoPos;
+      const uint64_t nlow = r.z - r.x;
+      const uint64_t len = nlow + (in_t ? (uint64_t)(r.y - r.w - 1) : 0);
+      if (k < 0) {
+        if (t < len) {
+          k = kk;
+          const uint64_t x = t < nlow ? r.x + t : r.w + 1 + (t - nlow);
+          g = (uint32_t)(S.segoff[kk] + x);
+          mirror = in_t;
+          ksel = kk;
+          moff = r.w - r.z;
+        } else {
+          t -= len;
+        }
+      }
+    }
+    valid = valid && k >= 0;
+    if (!valid) g = 0u;
+    const uint64_t rid = S.rident[g];
+    const uint64_t ida = P.ident[qA], idb = P.ident[qB];
+    bool ok = rid != (hi ? idb : ida) && rid != kDeadIdent;
+    const int kf = k >> S.seg_shift;
+    for (int j = 0; j < S.nkeys - 1; ++j) {
+      const uint64_t ka = S.qkeys[j][qA], kb = S.qkeys[j][qB];
+      if (j < kf) ok = ok && S.rkeys[j][g] != (hi ? kb : ka);
+    }
+    valid = valid && ok;
+  }
+  const uint32_t crow = P.rowof[g];
+  mirror = mirror && valid && crow >= S.r0 && crow < S.r1;
+  wave_lds_sync();
+
+  double prob = 0.5, prob2 = 0.5;
+  bool asym = false;
+  uint32_t bytes = valid ? 9u : 0u;
+  // the next property's query lengths, this lane's unit of each query (Peq bits) and the
+  // candidate's length, loaded while the current property computes
+  auto prefetch = [&](int pp, int& la, int& lb, uint32_t& ca, uint32_t& cb, int& lc_) {
+    const DevProp& E = P.props[pp];
+    la = (int)__builtin_amdgcn_readfirstlane((uint32_t)E.len[qA]);
+    lb = (int)__builtin_amdgcn_readfirstlane((uint32_t)E.len[qB]);
+    ca = cb = 0u;
+    if (E.op == DK_CMP_LEVENSHTEIN || E.op == DK_CMP_JAROWINKLER) {
+      const uint8_t* u = reinterpret_cast<const uint8_t*>(E.units);
+      if (la != (int)kMissing && lane < la && lane < 64)
+        ca = u[__builtin_amdgcn_readfirstlane(E.off[qA]) + lane];
+      if (two && lb != (int)kMissing && lane < lb && lane < 64)
+        cb = u[__builtin_amdgcn_readfirstlane(E.off[qB]) + lane];
+    }
+    lc_ = valid ? (int)__hip_atomic_load(E.rlen + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (int)kMissing;
+  };
+  // the wave's Peq tables: query A's in [0, 256), query B's in [256, 512) (two queries) --
+  // set (on) or cleared
+  auto tables = [&](int la, int lb, uint32_t ca, uint32_t cb, bool on) {
+    const uint64_t bit = 1ull << lane;
+    if (lane < la) {
+      if (on) atomicOr((unsigned long long*)&tab[ca], (unsigned long long)bit);
+      else tab[ca] = 0;
+    }
+    if (two && lane < lb) {
+      if (on) atomicOr((unsigned long long*)&tab[256 + cb], (unsigned long long)bit);
+      else tab[256 + cb] = 0;
+    }
+    wave_lds_sync();
+  };
+  const uint64_t ow = P.order[0];
+  int la_n = 0, lb_n = 0, lc_n = (int)kMissing;
+  uint32_t ca_n = 0u, cb_n = 0u;
+  if (P.nprops > 0) prefetch(order_at(ow, 0), la_n, lb_n, ca_n, cb_n, lc_n);
+  for (int p = 0; p < P.nprops; ++p) {
+    const int pp = order_at(ow, p);
+    const DevProp& D = P.props[pp];
+    const int la = la_n, lb = lb_n, lc = lc_n;
+    const uint32_t ca = ca_n, cb = cb_n;
+    if (p + 1 < P.nprops) prefetch(order_at(ow, p + 1), la_n, lb_n, ca_n, cb_n, lc_n);
+    const bool ma = la == (int)kMissing, mb = !two || lb == (int)kMissing;
+    if (ma && (mb || !two)) continue;  // no query of the wave has a value: skipped
+    const int lq = hi ? lb : la;
+    const bool qmiss = lq == (int)kMissing;  // r1 has no value: the property is skipped
+    const bool present = !qmiss && lc != (int)kMissing;
+    const bool cmp = present && lq > 0 && lc > 0;
+    double sim = 0.0, rev = __builtin_nan("");
+    if (present) bytes += 2u;
+    const Str<uint8_t> s1{reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(D.units) + D.off[q]),
+                          1, 1 << 30};
+    const Str<uint8_t> s2 = D.rlmax ? Str<uint8_t>{reinterpret_cast<const uint32_t*>(D.runits) + g, P.rstride,
+                                                   D.rlmax / 4 - 1}
+                                    : Str<uint8_t>{reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(D.units) + D.off[crow]),
+                                                   1, 1 << 30};
+    if (D.op == DK_CMP_NUMERIC) {
+      if (cmp) sim = numeric(D.num[q], D.numok[q] != 0, D.rnum[g], D.rnumok[g] != 0, D.min_ratio);
+      if (cmp) bytes += 9u;
+    } else if (D.op == DK_CMP_EXACT) {
+      if (cmp) sim = str_equal(s1, lq, s2, lc) ? 1.0 : 0.0;
+      if (cmp) bytes += (uint32_t)lc;
+    } else if (D.op == DK_CMP_LEVENSHTEIN || D.op == DK_CMP_JAROWINKLER) {
+      const int nmax = max(ma ? 0 : la, mb ? 0 : lb);  // wave-uniform: the row bucket / mask width
+      const int n1 = qmiss ? 0 : lq;
+      const bool table = nmax <= 64 && (D.op == DK_CMP_LEVENSHTEIN || __ballot(cmp && lc > 64) == 0);
+      if (table) {
+        tables(ma ? 0 : la, mb ? 0 : lb, ca, cb, true);
+        if (D.op == DK_CMP_LEVENSHTEIN) {
+          sim = levenshtein_peq<RMAX, uint8_t, true>(peq, s1, n1, s2, lc, cmp, nmax);
+        } else {
+          double r = 0.0;
+          sim = nmax <= DK_JW_NARROW ? jarowinkler_peq<uint32_t, uint8_t, true>(peq, s1, n1, s2, lc, cmp, &r)
+                                     : jarowinkler_peq<uint64_t, uint8_t, true>(peq, s1, n1, s2, lc, cmp, &r);
+          rev = r;
+        }
+        tables(ma ? 0 : la, mb ? 0 : lb, ca, cb, false);
+      } else if (cmp) {
+        sim = jarowinkler(s1, lq, s2, lc);
+        rev = lq == lc ? jarowinkler(s2, lc, s1, lq) : sim;
+      }
+      if (cmp) bytes += (uint32_t)lc;
+    }
+    if (rev != rev) rev = sim;
+    if (D.op == DK_CMP_JAROWINKLER) asym = true;  // wave-uniform
+    if (present) {
+      prob = compute_bayes(prob, cmp ? property_prob(D, sim) : 0.0);
+      prob2 = asym ? compute_bayes(prob2, cmp ? property_prob(D, rev) : 0.0) : prob;
+    }
+  }
+  const uint32_t kind = valid ? decide(prob, P.threshold, P.maybe) : 0u;
+  if (in_launch) {
+    S.okind[s] = (uint8_t)kind;
+    if (kind != 0u) S.ores[s] = prob;
+  }
+  const uint32_t kind2 = mirror ? decide(prob2, P.threshold, P.maybe) : 0u;
+  if (kind2 != 0u) {
+    const uint64_t m = S.mbase[(uint64_t)ksel * S.nq + (crow - S.r0)] + moff;
+    S.mkind[m] = (uint8_t)kind2;
+    S.mres[m] = prob2;
+  }
+  block_emit_at(out, bid, 0u, 0.0, 0u, 0u, valid ? (mirror ? 2u : 1u) : 0u, bytes);
+}
+
 // Schemas without a DP comparator (QGram / Numeric / Exact / token comparators: configs[2]'s
 // linkage): none of the DP code, its registers or its spills; the kernel is memory-latency
 // bound, so it takes the occupancy instead.
@@ -1928,7 +2127,8 @@ __global__ void k_count(const uint32_t* __restrict__ queries, uint64_t nq, const
 
 // Symmetric dedup schedule (PairSource::sym): per query and key function its bucket
 // [lo, hi), the first position qa of a query row (rows >= r0; the bucket is sorted by row)
-// and its own position pq, by binary search; full and owner slot counts padded to 64.
+// and its own position pq, by binary search; full slot counts padded to 64, owner slot
+// counts to opad (64, or 32 for k_score_sym2's half-wave queries).
 __device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* a, uint64_t lo, uint64_t hi,
                                                     uint32_t v) {
   while (lo < hi) {
@@ -1941,7 +2141,7 @@ __device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* a, uint64_t 
 __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, const BlockTables T,
                             uint32_t r0, uint4* __restrict__ sranges, uint64_t* __restrict__ counts,
                             uint64_t* __restrict__ ocounts, uint64_t* __restrict__ mcounts,
-                            uint64_t* __restrict__ real) {
+                            uint64_t* __restrict__ real, uint32_t opad) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t total = 0, own = 0, mir = 0;
   if (i < nq) {
@@ -1964,7 +2164,7 @@ __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, c
       mir += in_t ? p - qa : 0;
     }
     counts[i] = (total + 63) & ~(uint64_t)63;
-    ocounts[i] = (own + 63) & ~(uint64_t)63;
+    ocounts[i] = (own + opad - 1) / opad * opad;
     mcounts[i] = mir;
   }
   uint64_t w = total;
@@ -2006,10 +2206,10 @@ __global__ void k_iota_u32(uint32_t* __restrict__ out, uint64_t n, uint32_t star
 
 // wq[w] = qi for every wave w of query qi's slots (one thread per query, its waves in a
 // short loop: a query spans a few waves on average)
-__global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32_t* __restrict__ wq) {
+__global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32_t* __restrict__ wq, int shift) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
-  for (uint64_t w = qoff[i] >> 6, e = qoff[i + 1] >> 6; w < e; ++w) wq[w] = (uint32_t)i;
+  for (uint64_t w = qoff[i] >> shift, e = qoff[i + 1] >> shift; w < e; ++w) wq[w] = (uint32_t)i;
 }
 
 // replica-ordered identity and keys (the score kernel's candidate filters read them
@@ -2376,9 +2576,9 @@ hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockT
   return hipGetLastError();
 }
 
-hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s) {
+hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s, int shift) {
   DK_LAUNCH_GUARD(nq);
-  k_wavemap<<<grid1d(nq), 256, 0, s>>>(qoff, nq, wq);
+  k_wavemap<<<grid1d(nq), 256, 0, s>>>(qoff, nq, wq, shift);
   return hipGetLastError();
 }
 
@@ -2394,9 +2594,9 @@ hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t pos0, uint64_t 
 
 hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
                             uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* mcounts,
-                            uint64_t* real, hipStream_t s) {
+                            uint64_t* real, uint32_t opad, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_count_sym<<<grid1d(nq), 256, 0, s>>>(queries, nq, T, r0, sranges, counts, ocounts, mcounts, real);
+  k_count_sym<<<grid1d(nq), 256, 0, s>>>(queries, nq, T, r0, sranges, counts, ocounts, mcounts, real, opad);
   return hipGetLastError();
 }
 
@@ -2480,6 +2680,12 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
     if (P.long_rows <= 64) { if (lev64) DK_LONG(64, 4); else DK_LONG(16, 4); }
     else if (P.long_rows <= 128) { if (lev64) DK_LONG(64, 8); else DK_LONG(16, 8); }
     else { if (lev64) DK_LONG(64, 16); else DK_LONG(16, 16); }
+  } else if (src.sym && src.two) {
+    if (P.lev_rows <= 16) k_score_sym2<16><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+    else if (P.lev_rows <= 32) k_score_sym2<32><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+    else if (P.lev_rows <= 40) k_score_sym2<40><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+    else if (P.lev_rows <= 48) k_score_sym2<48><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
+    else k_score_sym2<64><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
   } else if (P.lev_rows <= 16) DK_SHORT(16);
   else if (P.lev_rows <= 32) DK_SHORT(32);
   else if (P.lev_rows <= 40) DK_SHORT(40);

@@ -26,7 +26,7 @@ KIND_MATCH, KIND_MAYBE = 1, 2
 
 MATCH_HOST, MATCH_DEVICE = 0, 1
 LUCENE_STATS_MERGED, LUCENE_STATS_UNMERGED = 0, 1
-ABI_VERSION = 8   # include/dukehip.h DK_ABI_VERSION
+ABI_VERSION = 9   # include/dukehip.h DK_ABI_VERSION
 
 EXPORTS = ("dk_create", "dk_create_multi", "dk_num_devices", "dk_destroy", "dk_upsert", "dk_upsert_transient", "dk_drop_transient",
            "dk_lucene_set_stats", "dk_lucene_merge",
@@ -118,7 +118,8 @@ class dk_profile(C.Structure):
                 ("pairs_generated", C.c_uint64), ("score_bytes", C.c_uint64),
                 ("ms_copy", C.c_double), ("ms_emit", C.c_double), ("sym_matches", C.c_uint64),
                 ("full_builds", C.c_uint64), ("delta_builds", C.c_uint64),
-                ("replica_positions", C.c_uint64), ("gram_row_bytes", C.c_uint64)]
+                ("replica_positions", C.c_uint64), ("gram_row_bytes", C.c_uint64),
+                ("sym2_matches", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

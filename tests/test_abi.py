@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
 
 def test_abi_version_and_error_text():
     lib = A.load()
-    assert lib.dk_abi_version() == A.ABI_VERSION == 8
+    assert lib.dk_abi_version() == A.ABI_VERSION == 9
     assert isinstance(lib.dk_last_error(), bytes)
 
 
@@ -61,7 +61,7 @@ int main(void) {
   F(dk_profile, pairs_scored) F(dk_profile, pairs_generated) F(dk_profile, score_bytes)
   F(dk_profile, ms_copy) F(dk_profile, ms_emit) F(dk_profile, sym_matches)
   F(dk_profile, full_builds) F(dk_profile, delta_builds) F(dk_profile, replica_positions)
-  F(dk_profile, gram_row_bytes)
+  F(dk_profile, gram_row_bytes) F(dk_profile, sym2_matches)
   S(dk_region_layout) F(dk_region_layout, capacity) F(dk_region_layout, first_offset)
   F(dk_region_layout, prob_offset) F(dk_region_layout, candidate_offset)
   F(dk_region_layout, kind_offset)

@@ -634,6 +634,68 @@ def test_symmetric_schedule_equals_direct(seed, monkeypatch):
     eng.close()
 
 
+def sym2_case(seed, n=3000):
+    """Latin-1 JaroWinkler / Levenshtein / Exact / Numeric values for k_score_sym2: lengths
+    from 1 to 40 units (the two half-waves' queries pick different row buckets), missing
+    values on both sides, small key buckets (most owned lists under 32: many waves hold two
+    queries)."""
+    rng = random.Random(seed)
+    alpha = "abcdeé"
+    def word(lo, hi):
+        return "".join(rng.choice(alpha) for _ in range(rng.randint(lo, hi)))
+    name = [word(1, 14) if rng.random() > 0.05 else None for _ in range(n)]
+    addr = [word(3, 40) if rng.random() > 0.08 else None for _ in range(n)]
+    code = [word(2, 3) if rng.random() > 0.1 else None for _ in range(n)]
+    num = [str(rng.randint(1, 9)) if rng.random() > 0.1 else None for _ in range(n)]
+    props = [{"comparator": JW, "low": 0.2, "high": 0.9},
+             {"comparator": LEV, "low": 0.1, "high": 0.8},
+             {"comparator": LEV, "low": 0.15, "high": 0.85},
+             {"comparator": NUM, "low": 0.3, "high": 0.7, "min_ratio": 0.5},
+             {"comparator": EX, "low": 0.4, "high": 0.6}]
+    vals = [name, addr, code, num, code]
+    keys = [[(v or "")[:2] for v in name], [(v or "")[:2] for v in addr]]
+    return props, vals, keys
+
+
+@pytest.mark.parametrize("seed", [43, 44])
+def test_sym2_two_queries_per_wave(seed, monkeypatch):
+    """k_score_sym2 (owner slots padded to 32, a query per half-wave) bit-exact against the
+    oracle, against one query per wave (DK_SYM2=0) and against the direct schedule
+    (DK_SYM=0), with superseded and deleted rows, a delta segment, one chunk and many."""
+    props, vals, keys = sym2_case(seed)
+    n = len(vals[0])
+    rng = np.random.default_rng(seed)
+    ident = np.arange(n, dtype=np.uint64)
+    ident[2500:2600] = ident[100:200]
+    deleted = (rng.random(n) < 0.03).astype(np.uint8)
+    eng = dh.GpuEngine(schema_of(props, 0.75, 0.55, "dedup", 2))
+    upsert_slice(eng, vals, keys, ident, 0, 2000, deleted)
+    upsert_slice(eng, vals, keys, ident, 2000, n, deleted)
+    ot = O.OracleTable(props, vals, keys=keys, ident=ident, deleted=deleted,
+                       alive=alive_after(list(ident), n), threshold=0.75, maybe=0.55)
+    for q in (np.arange(n, dtype=np.uint32), np.arange(900, 2700, dtype=np.uint32)):
+        ref = ot.match(q)
+        assert len(ref["query"]) > 100
+        for chunk in (None, "640"):
+            if chunk:
+                monkeypatch.setenv("DK_CHUNK_SLOTS", chunk)
+            else:
+                monkeypatch.delenv("DK_CHUNK_SLOTS", raising=False)
+            for env in ({}, {"DK_SYM2": "0"}, {"DK_SYM": "0"}):
+                for k, v in env.items():
+                    monkeypatch.setenv(k, v)
+                eng.reset_profile()
+                res = eng.match(q)
+                prof = eng.profile()
+                assert prof["sym_matches"] == (0 if env.get("DK_SYM") == "0" else 1)
+                assert prof["sym2_matches"] == (1 if not env else 0)
+                assert_same(res, ref)
+                res.close()
+                for k in env:
+                    monkeypatch.delenv(k)
+    eng.close()
+
+
 def test_symmetric_schedule_overwrite_duplicates():
     """overwrite: several alive rows of one ID; isSameAs filters them from each other."""
     props, vals, keys = sym_case(43, n=900)
