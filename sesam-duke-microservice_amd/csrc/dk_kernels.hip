@@ -1785,16 +1785,16 @@ __global__ __launch_bounds__(256) void k_sym_emit(const EmitSource S, uint64_t q
       kind[u] = t < L ? (uint32_t)(m ? S.mkind[idx[u]] : S.okind[idx[u]]) : 0u;
     }
     if (WRITE) {
+      // every in-range candidate's probability and row loaded with its decision byte (one
+      // memory round trip, not two: at ~1 entry in 4 candidates an entry-only load touches
+      // the same cache lines)
       double pr[kEmitBatch];
       uint32_t crow[kEmitBatch];
 #pragma unroll
       for (int u = 0; u < kEmitBatch; ++u) {
-        pr[u] = 0.0;
-        crow[u] = 0u;
-        if (kind[u] != 0u) {
-          pr[u] = mir[u] ? S.mres[idx[u]] : S.ores[idx[u]];
-          crow[u] = S.rowof[pos[u]];
-        }
+        const bool in = t0 + (uint64_t)u * 64 + lane < L;
+        pr[u] = in ? (mir[u] ? S.mres[idx[u]] : S.ores[idx[u]]) : 0.0;
+        crow[u] = in ? S.rowof[pos[u]] : 0u;
       }
 #pragma unroll
       for (int u = 0; u < kEmitBatch; ++u) {
