@@ -200,6 +200,8 @@ typedef struct dk_profile {
                                  them through head / tail buffer resources) */
   uint64_t sym2_matches;  /* symmetric dedup calls with two queries per wave (k_score_sym2:
                              owner slots padded to 32; ABI 9) */
+  uint64_t pairs_exact;   /* scored pairs that took k_score_gq's exact double-precision pass
+                             (the rest were decided by its single-precision screen; ABI 9) */
 } dk_profile;
 
 typedef struct dk_ctx dk_ctx;

@@ -557,12 +557,11 @@ struct dk_ctx {
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
   DevBuf ocounts, oqoff, owq, obase, okind, ores, mcounts, mqoff, mbase, mkind, mres, ecount, eincl, bidx, bval;
-  DevBuf lsim;             // the long-value DP pre-pass's similarities (k_long_pre)
   DevBuf raised;           // k_score_geo: a compared GeopositionComparator value without ','
   PinnedBuf h_raised;
   PinnedBuf h_bounds;
   DevBuf counters;
-  struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx; };
+  struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx, bexact; };
   StageBufs stage[2];                          // double-buffered per-chunk staging
   StageBufs owner_stage;  // block counters of the owner phase (it emits no entries)
   hipEvent_t count_ready[2] = {nullptr, nullptr};  // a chunk's entry count reached hs[]
@@ -849,6 +848,7 @@ int dk_get_profile(const dk_ctx* c, dk_profile* out) {
       t.score_bytes += p.score_bytes;
       t.sym_matches += p.sym_matches;
       t.sym2_matches += p.sym2_matches;
+      t.pairs_exact += p.pairs_exact;
       t.full_builds += p.full_builds;
       t.delta_builds += p.delta_builds;
       t.replica_positions = std::max(t.replica_positions, p.replica_positions);
@@ -1759,19 +1759,7 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
       P.order[o] |= (uint64_t)(c->orders.empty() ? k : c->orders[(size_t)o * P.nprops + k]) << (4 * k);
   }
   P.oclass = c->oclass.as<uint8_t>();
-  // the long-value DP's properties (k_long_pre): WeightedLevenshtein, and Levenshtein (its
-  // queries over 64 units); the buffer is set per launch (long_sim_buffer)
   P.raised = c->raised.as<uint32_t>();
-  P.lsim = nullptr;
-  P.lstride = 0;
-  P.long_word = ~0ull;
-  for (int p = 0, j = 0; p < P.nprops; ++p) {
-    const int op = c->P[p].cfg.comparator;
-    if (op == DK_CMP_WEIGHTED_LEVENSHTEIN || op == DK_CMP_LEVENSHTEIN) {
-      P.long_word &= ~(15ull << (4 * p));
-      P.long_word |= (uint64_t)j++ << (4 * p);
-    }
-  }
   for (const auto& S : c->P) {
     const int op = S.cfg.comparator;
     if (op == DK_CMP_LEVENSHTEIN || op == DK_CMP_JAROWINKLER || op == DK_CMP_WEIGHTED_LEVENSHTEIN) P.has_dp = 1;
@@ -1819,20 +1807,6 @@ static ScoreParams make_params(const dk_ctx* c, const std::vector<Replica>& rep,
     D.gseed = S.gseed.as<uint16_t>();
   }
   return P;
-}
-
-// The long-value DP pre-pass's similarity buffer for launches of up to `maxslots` slots
-// (k_long_pre -> k_score_long): 8 B per slot and property on that DP.  Returns false on an
-// allocation failure.
-static bool long_sim_buffer(dk_ctx* c, ScoreParams& P, uint64_t maxslots) {
-  if (P.long_rows <= 0 || P.has_geo || !long_dp_split()) return true;
-  int nlong = 0;
-  for (int p = 0; p < P.nprops; ++p) nlong += ((P.long_word >> (4 * p)) & 15u) != 15u;
-  const uint64_t stride = std::max<uint64_t>(kScoreBlock, (maxslots + kScoreBlock - 1) / kScoreBlock * kScoreBlock);
-  if (c->lsim.reserve((uint64_t)std::max(nlong, 1) * stride * 8, 0, c->stream) != hipSuccess) return false;
-  P.lsim = c->lsim.as<double>();
-  P.lstride = stride;
-  return true;
 }
 
 // Candidate replica: every property's candidate-side values in replica order, units
@@ -2733,7 +2707,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     so = StageOut{c->counters.as<uint64_t>(), G.bcnt.as<uint32_t>(), G.bscored.as<uint32_t>(),
                   G.bbytes.as<uint32_t>(), nullptr, nullptr, nullptr};
   }
-  HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * sizeof(uint64_t), s));
+  HIPCHK(hipMemsetAsync(c->counters.p, 0, 4 * sizeof(uint64_t), s));
   ResultBufs& B = *R->bufs;
   uint64_t nm = 0;  // entries so far
   PairSource src{};
@@ -2793,6 +2767,13 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   int gq_nq = 0, gq_nn = 0;
   const bool gq = grouped && gq_args(P, &gqa, &gq_nq, &gq_nn);
   if (gq) {
+    // per staging block: the pairs that reached the exact pass (dk_profile.pairs_exact)
+    uint64_t nbx = 1;
+    for (size_t i = 0; i + 1 < bounds.size(); ++i) nbx = std::max(nbx, (bounds[i + 1] - bounds[i] + kScoreBlock - 1) / kScoreBlock);
+    for (int b = 0; b < 2; ++b) {
+      HIPCHK(c->stage[b].bexact.reserve(nbx * 4 + 4, 0, s));
+      st[b].bexact = c->stage[b].bexact.as<uint32_t>();
+    }
     // one copy per staging set (the launch's output buffers are part of it)
     GQArgs two[2] = {gqa, gqa};
     for (int b = 0; b < 2; ++b) {
@@ -2937,12 +2918,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     return DK_OK;
   };
   const size_t nchunks = bounds.size() - 1;
-  ScoreParams PL = P;  // + the long-value DP's buffer (k_long_pre)
-  {
-    uint64_t maxc = 0;
-    for (size_t ci = 0; ci < nchunks; ++ci) maxc = std::max(maxc, bounds[ci + 1] - bounds[ci]);
-    if (!sym && !long_sim_buffer(c, PL, maxc)) return fail(DK_E_DEVICE, "long-value DP buffer");
-  }
   // SYM: chunk ci's owner scoring, its emission's count pass and the scan of the counts run
   // on the ctx stream; its write pass on the copy stream (compact_chunk) beside chunk ci+1's
   // scoring.  Emission of chunk ci reads owner results of chunk ci and mirror results of
@@ -2988,7 +2963,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
           HIPCHK(launch_score_gq(P, src, s0, s1 - s0, perm, c->gqargs.as<GQArgs>() + b, gq_nq, gq_nn, gqa.defer, st[b], s));
         else if (grouped)
           HIPCHK(launch_score_grouped(P, src, s0, s1 - s0, perm, c->gprops.as<GroupedProp>(), gmode, st[b], s));
-        else HIPCHK(launch_score(PL, src, s0, s1 - s0, st[b], s));
+        else HIPCHK(launch_score(P, src, s0, s1 - s0, st[b], s));
         t_score.stop();
       }
       HIPCHK(launch_reduce_blocks(st[b], nblk, s));
@@ -3015,7 +2990,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     if (rc2) return rc2;
     HIPCHK(hipStreamWaitEvent(s, c->compact_done[(nchunks - 1) & 1], 0));  // list complete
   }
-  HIPCHK(hipMemcpyAsync(c->h_small.p, c->counters.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_small.p, c->counters.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   {
     const int rg = geo_raise_check(c, P);
@@ -3024,6 +2999,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   lap("score+emit");
   const uint64_t scored = c->h_small.as<uint64_t>()[0];
   const uint64_t sbytes = c->h_small.as<uint64_t>()[1];
+  c->prof.pairs_exact += c->h_small.as<uint64_t>()[3];
   if (sym) c->prof.sym_matches += 1;
   if (sym && two) c->prof.sym2_matches += 1;
   R->r.pairs_scored = scored;
@@ -3280,7 +3256,6 @@ static int compare_one(dk_ctx* c, uint32_t r1, uint32_t r2, int raw_prop, double
   src.m = 1;
   src.mpad = 64;
   src.same_ok = 1;  // Processor.compare scores a record against itself too
-  if (!long_sim_buffer(c, P, 1)) return fail(DK_E_DEVICE, "long-value DP buffer");
   rc = geo_raise_clear(c, P);
   if (rc) return rc;
   HIPCHK(launch_score(P, src, 0, 1, st, s));

@@ -133,12 +133,6 @@ struct ScoreParams {
   int32_t norders;
   uint64_t order[kMaxOrders];
   const uint8_t* oclass;  // per row: its order class (norders > 1)
-  // the long-value DP pre-pass (k_long_pre -> k_score_long): property p's similarity of the
-  // launch's slot i at lsim[j * lstride + i], j = bits [4p, 4p + 4) of long_word (15: p is
-  // not on the long-value DP)
-  double* lsim;
-  uint64_t lstride;
-  uint64_t long_word;
   // GeopositionComparator: set (non-zero) by a kernel that compared a value without ','
   // (numok 2) -- stock Duke raises there; the host then fails the call
   uint32_t* raised;
@@ -312,13 +306,15 @@ struct EmitSource {
 constexpr int kScoreBlock = 256;
 constexpr int kKindShift = 30;  // staged candidate word = row | kind << 30
 struct StageOut {
-  uint64_t* counters;  // [0] pairs scored, [1] operand bytes (summed by k_reduce_blocks)
+  uint64_t* counters;  // [0] pairs scored, [1] operand bytes, [3] pairs that took k_score_gq's
+                       // exact pass (summed by k_reduce_blocks)
   uint32_t* bcnt;      // per block: emitted entries
   uint32_t* bscored;   // per block: pairs scored
   uint32_t* bbytes;    // per block: algorithmic operand bytes
   double* prob;
   uint32_t* cand;
   uint32_t* qidx;
+  uint32_t* bexact;    // per block: pairs through the exact pass (k_score_gq; null: none)
 };
 
 // Device-resident match list of one dk_match call.
@@ -513,7 +509,6 @@ hipError_t launch_gather_u64(const uint64_t* src, const uint64_t* idx, uint64_t 
 // out[i] = start + i (a contiguous batch's query rows, written on the device)
 hipError_t launch_iota_u32(uint32_t* out, uint64_t n, uint32_t start, hipStream_t s);
 hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s);
-bool long_dp_split();  // dk_kernels.hip built with DK_LONG_SPLIT (k_long_pre + P.lsim)
 hipError_t launch_compact(const StageOut& st, const uint64_t* boff, uint64_t nblocks,
                           uint64_t base, const MatchList& out, hipStream_t s);
 hipError_t launch_first(const uint32_t* qidx, uint64_t n, uint64_t nq, uint64_t* first,

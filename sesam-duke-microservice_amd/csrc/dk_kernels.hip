@@ -29,16 +29,10 @@
 #define DK_WAVES_NODP 8   // k_score_nodp waves per SIMD (no DP comparator: latency bound)
 #endif
 #ifndef DK_WAVES_LONG8
-#define DK_WAVES_LONG8 5  // k_score_long waves per SIMD (the long DP is in k_long_pre)
+#define DK_WAVES_LONG8 5  // k_score_long waves per SIMD (the DP an out-of-line call)
 #endif
 #ifndef DK_WAVES_LONG16
 #define DK_WAVES_LONG16 5  // k_score_long_geo waves per SIMD (the DP in the fused kernel)
-#endif
-#ifndef DK_WAVES_LONGPRE
-#define DK_WAVES_LONGPRE 4  // k_long_pre waves per SIMD, DP variants of <= 4 rows per lane
-#endif
-#ifndef DK_WAVES_LONGPRE_HI
-#define DK_WAVES_LONGPRE_HI 4  // the same, 5-8 rows per lane (f64 columns of 6-9 values)
 #endif
 
 namespace dk {
@@ -450,8 +444,10 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// long_dp_body is inlined into the pre-pass kernel k_long_pre (its own registers, no call
-// frame); long_dp, its out-of-line form, serves the fused geo variant
+// long_dp_body runs as long_dp, an out-of-line call: the call saves the fused kernel's live
+// state to its scratch frame, so the DP's column, weights and units get the registers, at 5
+// waves per SIMD.  Inlined (one variant per kernel, zero scratch at 3-4 waves, or 4-5 waves
+// with spills inside the DP) it ran 1.5-1.6x slower.
 template <int G, int R, bool WL, typename CT>
 __device__ __forceinline__ void long_dp_body(uint64_t wstride, const CT* s1p, int n1, int nneed) {
   uint64_t* lds = g_wave_tables[threadIdx.x >> 6];
@@ -636,12 +632,10 @@ __host__ __device__ constexpr int long_variant(int n1) {
        : n1 <= 96 ? 5 : n1 <= 112 ? 6 : (n1 <= 128 || LR <= 8) ? 7 : n1 <= 160 ? 8 : n1 <= 192 ? 9
        : n1 <= 224 ? 10 : 11;
 }
-template <int LR>
-__host__ __device__ constexpr int long_nvariants() { return LR <= 4 ? 4 : LR <= 8 ? 8 : 12; }
 
-// Similarity of every lane with `need` set (the others keep `sim`) through long_dp (INL:
-// the inlined body; VI >= 0: only DP variant VI).  Wave-uniform call: all 64 lanes enter.
-template <int LR, bool WL, typename CT, bool INL = false, int VI = -1>
+// Similarity of every lane with `need` set (the others keep `sim`) through long_dp.
+// Wave-uniform call: all 64 lanes enter.
+template <int LR, bool WL, typename CT>
 __device__ __forceinline__ double long_sims(const DevProp& D, uint64_t rstride, uint64_t* lds, uint32_t q,
                                             int n1, uint32_t g, uint32_t crow, int lc, bool need,
                                             double sim) {
@@ -676,15 +670,9 @@ __device__ __forceinline__ double long_sims(const DevProp& D, uint64_t rstride, 
   // DPP row_shr) up to 128 rows, 32-lane groups (2 streams, wave_shr) beyond; R = rows /
   // lanes rounded up, so most of a group's lanes hold rows, and R <= 8 keeps the column,
   // weights and units in VGPRs.  LR caps the variants a kernel carries.
-  // VI >= 0 (the pre-pass kernels): only variant VI is compiled in
   const int vi = long_variant<LR>(n1);
-#define DK_LDP(V_, G_, R_)                                                                  \
-  if constexpr (VI < 0 || VI == (V_)) {                                                     \
-    if (vi == (V_)) {                                                                       \
-      if constexpr (INL) long_dp_body<G_, R_, WL, CT>(wstride, s1p, n1, nneed);             \
-      else long_dp<G_, R_, WL, CT>(wstride, s1p, n1, nneed);                                \
-    }                                                                                       \
-  }
+#define DK_LDP(V_, G_, R_) \
+  if (vi == (V_)) long_dp<G_, R_, WL, CT>(wstride, s1p, n1, nneed);
   DK_LDP(0, 16, 1)
   DK_LDP(1, 16, 2)
   DK_LDP(2, 16, 3)
@@ -1004,13 +992,10 @@ __device__ __forceinline__ int qgram_common_perfect(uint32_t* tab, const uint64_
 // ------------------------------------------------------------------------------------
 // SYM: `rev` receives Comparator.compare(candidate, query) where it can differ from
 // compare(query, candidate) (JaroWinkler on equal lengths); it is left alone otherwise.
-// LB: the long-value DP's similarities computed here (0), inlined for the pre-pass (1), or
-// taken from it (2: lbuf)
-template <int RMAX, int LR, typename CT, bool SYM, bool DP, bool GR, int LB = 0, int VI = -1>
+template <int RMAX, int LR, typename CT, bool SYM, bool DP, bool GR>
 __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride, uint64_t* peq,
                                              uint32_t q, uint32_t g, uint32_t crow, int lq,
-                                             int lc, bool cmp, double& rev, uint32_t qch,
-                                             double lbuf = 0.0) {
+                                             int lc, bool cmp, double& rev, uint32_t qch) {
   const CT* base = reinterpret_cast<const CT*>(D.units);
   const Str<CT> s1{reinterpret_cast<const uint32_t*>(base + D.off[q]), 1, 1 << 30};
   const Str<CT> s2 = D.rlmax ? Str<CT>{reinterpret_cast<const uint32_t*>(D.runits) + g, rstride,
@@ -1020,22 +1005,14 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
   switch (D.op) {
     case DK_CMP_WEIGHTED_LEVENSHTEIN:
       if (DP && LR > 0) {  // the host only schedules WeightedLevenshtein on LR > 0 variants
-        if (LB == 2) {
-          sim = lbuf;
-          break;
-        }
         const bool same = cmp && str_equal(s1, lq, s2, lc);
         sim = same ? 1.0 : 0.0;
-        sim = long_sims<LR, true, CT, LB == 1, VI>(D, rstride, peq, q, lq, g, crow, lc, cmp && !same, sim);
+        sim = long_sims<LR, true, CT>(D, rstride, peq, q, lq, g, crow, lc, cmp && !same, sim);
       }
       break;
     case DK_CMP_LEVENSHTEIN:
       if (!DP) break;  // the DP-free variant is only launched without DP comparators
       if (LR > 0 && lq > kMaxUnits) {  // query over 64 units: long-value DP
-        if (LB == 2) {
-          sim = lbuf;
-          break;
-        }
         bool need = false;
         if (cmp) {
           const int len = min(lq, lc), maxlen = max(lq, lc);
@@ -1043,7 +1020,7 @@ __device__ __forceinline__ double string_sim(const DevProp& D, uint64_t rstride,
           else if (len == maxlen && str_equal(s1, lq, s2, lc)) sim = 1.0;
           else need = true;
         }
-        sim = long_sims<LR, false, CT, LB == 1, VI>(D, rstride, peq, q, lq, g, crow, lc, need, sim);
+        sim = long_sims<LR, false, CT>(D, rstride, peq, q, lq, g, crow, lc, need, sim);
         break;
       }
       [[fallthrough]];
@@ -1189,9 +1166,7 @@ __device__ __forceinline__ void block_emit(const StageOut& out, uint32_t kind, d
 // SYM: the owner slots of the symmetric dedup schedule (PairSource::sym): every owned pair
 // is scored in both directions in one pass and the two probabilities go to S.ores; the
 // emission pass (k_sym_emit) turns them into the match list.
-// LB (long-value DP properties): 0 computed in place; 1 the pre-pass (k_long_pre: only those
-// properties, their similarities to P.lsim, no decisions); 2 read from P.lsim (k_score_long)
-template <int RMAX, int LR, bool SYM, bool DP, bool GR = true, bool GEO = false, int LB = 0, int VI = -1>
+template <int RMAX, int LR, bool SYM, bool DP, bool GR = true, bool GEO = false>
 __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSource& S, uint64_t slot0,
                                            uint64_t nslots, const StageOut& out) {
   uint64_t* peq = g_wave_tables[threadIdx.x >> 6];
@@ -1323,7 +1298,6 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     const uint32_t qch = qch_n;
     if (p + 1 < P.nprops) prefetch(order_at(ow, p + 1), lq_n, qch_n, lc_n);
     if (lq == (int)kMissing) continue;  // r1 has no value: property skipped for the wave
-    if (LB == 1 && D.op != DK_CMP_WEIGHTED_LEVENSHTEIN && D.op != DK_CMP_LEVENSHTEIN) continue;
     const bool present = lc != (int)kMissing;
     const bool cmp = present && lq > 0 && lc > 0;
     double sim = 0.0, rev = 0.0;
@@ -1347,17 +1321,8 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     } else if (D.op != DK_CMP_NONE) {
       rev = __builtin_nan("");  // marks "same as sim" unless the comparator sets it
       // a property on the long-value DP for this wave (wave-uniform): the pre-pass's slot
-      const bool on_long = LR > 0 && (D.op == DK_CMP_WEIGHTED_LEVENSHTEIN ||
-                                      (D.op == DK_CMP_LEVENSHTEIN && lq > kMaxUnits));
-      const uint64_t lat = ((P.long_word >> (4 * pp)) & 15u) * P.lstride + min(idx, nslots - 1);
-      if (LB == 1 && (!on_long || long_variant<LR>(lq) != VI)) continue;  // another pre-pass kernel's
-      const double lbuf = LB == 2 && on_long ? P.lsim[lat] : 0.0;
-      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM, DP, GR, LB, VI>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch, lbuf)
-                         : string_sim<RMAX, LR, uint16_t, SYM, DP, GR, LB, VI>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch, lbuf);
-      if (LB == 1) {
-        if (in_launch) P.lsim[lat] = sim;
-        continue;
-      }
+      sim = D.width == 1 ? string_sim<RMAX, LR, uint8_t, SYM, DP, GR>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch)
+                         : string_sim<RMAX, LR, uint16_t, SYM, DP, GR>(D, P.rstride, peq, q, g, crow, lq, lc, cmp, rev, qch);
       if (!SYM || rev != rev) rev = sim;
       if (cmp) {
         if (D.op == DK_CMP_QGRAM)  // the candidate's gram codes (u32 replica codes for q <= 2,
@@ -1385,7 +1350,6 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
     }
   }
 
-  if (LB == 1) return;  // the pre-pass: similarities only
   if (SYM) {
     // the owner decision byte for this query's list (its probability only for an entry); the
     // reverse direction into the candidate's mirror segment (scattered stores while the
@@ -1617,40 +1581,12 @@ void k_score_nodp(const ScoreParams P, const PairSource S, uint64_t slot0, uint6
   score_body<16, 0, SYM, false>(P, S, slot0, nslots, out);
 }
 
-// Long values (WeightedLevenshtein, Levenshtein over 64 units): the systolic DP runs in its
-// own pass first -- k_long_pre, the DP inlined (its registers alone, no call frame) -- and
-// leaves each slot's similarity in P.lsim (8 B per slot and long property); k_score_long then
-// scores with every other comparator and reads those.  With the DP as an out-of-line call
-// inside the fused kernel, the call frame and the callee-saved registers of the DP cost a
-// 120-280 B/lane scratch frame.
-#ifndef DK_LONG_SPLIT
-#define DK_LONG_SPLIT 0  // 1: the DP in its own pass (k_long_pre, no scratch) -- measured 1.6x
-                         // slower on configs[4], so the fused call stays the build
-#endif
-#if DK_LONG_SPLIT
-// One pre-pass kernel per DP variant VI (rows per lane, long_variant): each carries that
-// variant alone, so its registers are that variant's; the waves of queries of other lengths
-// leave after the slot mapping.
-template <int LR, int VI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VI >= 4 ? DK_WAVES_LONGPRE_HI : DK_WAVES_LONGPRE, 8)))
-void k_long_pre(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
-  score_body<16, LR, false, true, true, false, 1, VI>(P, S, slot0, nslots, out);
-}
-
-template <int LR, int VI = 0>
-static void launch_long_pre(const ScoreParams& P, const PairSource& src, uint64_t slot0, uint64_t nslots,
-                            const StageOut& out, unsigned grid, hipStream_t s) {
-  k_long_pre<LR, VI><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);
-  if constexpr (VI + 1 < long_nvariants<LR>()) launch_long_pre<LR, VI + 1>(P, src, slot0, nslots, out, grid, s);
-}
-#endif
-
-
+// Long values (WeightedLevenshtein, Levenshtein over 64 units): the fused kernel with the DP
+// as an out-of-line call (long_dp).
 template <int RMAX, int LR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_LONG8, 8)))
-void k_score_long(const ScoreParams P, const PairSource S,
-                                                    uint64_t slot0, uint64_t nslots, StageOut out) {
-  score_body<RMAX, LR, false, true, true, false, DK_LONG_SPLIT ? 2 : 0>(P, S, slot0, nslots, out);
+void k_score_long(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
+  score_body<RMAX, LR, false, true, true, false>(P, S, slot0, nslots, out);
 }
 
 // Schemas with a GeopositionComparator (P.has_geo; never the symmetric schedule): the direct
@@ -1825,27 +1761,32 @@ __global__ __launch_bounds__(256) void k_sym_emit(const EmitSource S, uint64_t q
 // Sum the per-block counters of a chunk into counters[0..1]: one atomic pair per block
 // of this kernel (a same-address atomic per score wave serialises at the memory side).
 __global__ __launch_bounds__(256) void k_reduce_blocks(const StageOut st, uint64_t nblocks) {
-  uint64_t a = 0, b = 0;
+  uint64_t a = 0, b = 0, x = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nblocks;
        i += (uint64_t)gridDim.x * blockDim.x) {
     a += st.bscored[i];
     b += st.bbytes[i];
+    if (st.bexact) x += st.bexact[i];
   }
   for (int o = 32; o > 0; o >>= 1) {
     a += __shfl_xor(a, o);
     b += __shfl_xor(b, o);
+    x += __shfl_xor(x, o);
   }
-  __shared__ uint64_t sa[4], sbb[4];
+  __shared__ uint64_t sa[4], sbb[4], sx[4];
   if (lane_id() == 0) {
     sa[threadIdx.x >> 6] = a;
     sbb[threadIdx.x >> 6] = b;
+    sx[threadIdx.x >> 6] = x;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     a = sa[0] + sa[1] + sa[2] + sa[3];
     b = sbb[0] + sbb[1] + sbb[2] + sbb[3];
+    x = sx[0] + sx[1] + sx[2] + sx[3];
     if (a) atomicAdd((unsigned long long*)&st.counters[0], (unsigned long long)a);
     if (b) atomicAdd((unsigned long long*)&st.counters[1], (unsigned long long)b);
+    if (x) atomicAdd((unsigned long long*)&st.counters[3], (unsigned long long)x);
   }
 }
 
@@ -2655,17 +2596,7 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
       else k_score<RM, false, false><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);        \
     }                                                                                         \
   } while (0)
-#if DK_LONG_SPLIT
-#define DK_LONG(RM, L)                                                                   \
-  do {                                                                                   \
-    if (!P.lsim || P.lstride < (nslots + kScoreBlock - 1) / kScoreBlock * kScoreBlock)   \
-      return hipErrorInvalidValue;                                                       \
-    launch_long_pre<L>(P, src, slot0, nslots, out, grid, s);                             \
-    k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out);        \
-  } while (0)
-#else
 #define DK_LONG(RM, L) k_score_long<RM, L><<<grid, kScoreBlock, 0, s>>>(P, src, slot0, nslots, out)
-#endif
   if (src.sym && P.long_rows > 0) return hipErrorInvalidValue;  // the host never schedules it
   if (P.has_geo) {
     if (src.sym) return hipErrorInvalidValue;  // the host never schedules it (sym_schema_ok)
@@ -2696,7 +2627,6 @@ hipError_t launch_score(const ScoreParams& P, const PairSource& src, uint64_t sl
   return hipGetLastError();
 }
 
-bool long_dp_split() { return DK_LONG_SPLIT != 0; }
 
 hipError_t launch_reduce_blocks(const StageOut& st, uint64_t nblocks, hipStream_t s) {
   DK_LAUNCH_GUARD(nblocks);

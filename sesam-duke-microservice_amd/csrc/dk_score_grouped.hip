@@ -677,7 +677,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
   }
   wave_lds_sync();
 
-  uint32_t cnt = 0, scored = 0, bytes = 0;
+  uint32_t cnt = 0, scored = 0, bytes = 0, nexact = 0;
   const uint64_t blk = task;  // staging block of the task (k_compact: block order = slot order)
 
   // the query's role constants (LDS, uniform)
@@ -744,6 +744,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
   auto exact = [&](uint32_t head, uint32_t n) {
     GQLds* const H = gq_hdr(hdr0);
     const bool act = lane < n;
+    nexact += n;
     const uint64_t ent = act ? queue[(head + lane) & (kGQQueue - 1)] : 0ull;
     const uint32_t g = (uint32_t)ent;
     uint32_t qlen[NR1], m1[NQ1], sd[NQ1];
@@ -772,6 +773,11 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
     }
     if constexpr (DEF >= 0)
       if (perfect[DEF < 0 ? 0 : DEF]) common[DEF < 0 ? 0 : DEF] = role_common(H, std::integral_constant<int, DEF < 0 ? 0 : DEF>{}, g, nwd, sd[DEF < 0 ? 0 : DEF], wd);
+    // algorithmic bytes: the deferred role's candidate keys, read by this pass only
+    if constexpr (DEF >= 0)
+      if (act && lq[DEF < 0 ? 0 : DEF] != kMissing && lq[DEF < 0 ? 0 : DEF] > 0 && qlen[DEF < 0 ? 0 : DEF] > 0 &&
+          qlen[DEF < 0 ? 0 : DEF] != kMissing)
+        bytes += 2u * cq[DEF < 0 ? 0 : DEF];
     double pp[NR1];
     bool ap[NR1];
 #pragma unroll
@@ -901,7 +907,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
       const bool present = valid && lq[a] != kMissing;
       const bool cmp = present && lq[a] > 0 && qlen[a] > 0;
       if (present) by += 2u;
-      if (cmp) by += 6u + 2u * cq[a];
+      if (cmp) by += 6u + (a == DEF ? 0u : 2u * cq[a]);  // the deferred role's keys: the exact pass
       if constexpr (a != DEF)
         if (perfect[a]) common[a] = role_common(H, ic, g, nw[a], sd[a], w);
       if (!present) return;
@@ -971,6 +977,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
     out.bcnt[blk] = cnt;
     out.bscored[blk] = ss;
     out.bbytes[blk] = sbytes;
+    if (out.bexact) out.bexact[blk] = nexact;
   }
 }
 

@@ -119,7 +119,7 @@ class dk_profile(C.Structure):
                 ("ms_copy", C.c_double), ("ms_emit", C.c_double), ("sym_matches", C.c_uint64),
                 ("full_builds", C.c_uint64), ("delta_builds", C.c_uint64),
                 ("replica_positions", C.c_uint64), ("gram_row_bytes", C.c_uint64),
-                ("sym2_matches", C.c_uint64)]
+                ("sym2_matches", C.c_uint64), ("pairs_exact", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

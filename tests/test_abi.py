@@ -61,7 +61,7 @@ int main(void) {
   F(dk_profile, pairs_scored) F(dk_profile, pairs_generated) F(dk_profile, score_bytes)
   F(dk_profile, ms_copy) F(dk_profile, ms_emit) F(dk_profile, sym_matches)
   F(dk_profile, full_builds) F(dk_profile, delta_builds) F(dk_profile, replica_positions)
-  F(dk_profile, gram_row_bytes) F(dk_profile, sym2_matches)
+  F(dk_profile, gram_row_bytes) F(dk_profile, sym2_matches) F(dk_profile, pairs_exact)
   S(dk_region_layout) F(dk_region_layout, capacity) F(dk_region_layout, first_offset)
   F(dk_region_layout, prob_offset) F(dk_region_layout, candidate_offset)
   F(dk_region_layout, kind_offset)

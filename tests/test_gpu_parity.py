@@ -324,6 +324,27 @@ def test_long_and_short_properties_fused():
     assert_same(res, ref)
 
 
+@pytest.mark.parametrize("long_cmp", [WL, LEV])
+def test_long_dp_variants_blocked(long_cmp):
+    """One long-DP property under blocking, query values of 1 to 256 units (every one of the
+    twelve DP variants), with missing values, beside a short Levenshtein / JaroWinkler / QGram
+    property; bit-exact against the oracle."""
+    rng = random.Random(long_cmp * 7 + 3)
+    n = 900
+    lo = 1 if long_cmp == WL else 40
+    text = families(rng, 90, 9, WL_ALPHA if long_cmp == WL else "abcd", lo, 256, 14, 256)[:n]
+    short = families(rng, 90, 9, "abcdefg", 3, 30, 3, 64)[:n]
+    for i in range(0, n, 19):
+        text[i] = None
+    keys = [[("k%d" % (i % 45)) for i in range(n)]]
+    props = [{"comparator": long_cmp, "low": 0.2, "high": 0.9},
+             {"comparator": LEV if long_cmp == WL else JW, "low": 0.3, "high": 0.7},
+             {"comparator": QG, "low": 0.4, "high": 0.6, "q": 3, "formula": 1}]
+    res, ref = run_both(props, [text, short, text], keys, threshold=0.6, maybe=0.3)
+    assert res.n > 0
+    assert_same(res, ref)
+
+
 @pytest.mark.parametrize("cmp", [DICE_T, JACC_T])
 def test_token_comparators_allpairs(cmp):
     rng = random.Random(cmp)
