@@ -557,6 +557,9 @@ struct dk_ctx {
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
   DevBuf ocounts, oqoff, owq, obase, okind, ores, mcounts, mqoff, mbase, mkind, mres, ecount, eincl, bidx, bval;
+  // k_count_sym's bucket lookup for large batches (SymIndex), built once per table build
+  DevBuf sx_posof, sx_hflag, sx_bstart, sx_bend, sx_tmp;
+  uint64_t sx_gen = 0;
   DevBuf raised;           // k_score_geo: a compared GeopositionComparator value without ','
   PinnedBuf h_raised;
   PinnedBuf h_bounds;
@@ -2529,6 +2532,28 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   bool grouped = false;  // k_score_grouped: query slots padded to kScoreBlock
   const uint32_t r0 = nq ? query_rows[0] : 0;
   uint64_t* hs = c->h_small.as<uint64_t>();
+  SymIndex sx{};
+  // a large batch looks its queries' buckets up in SymIndex (built once per table build: one
+  // pass over the replica positions); a small one (an incremental batch) searches the tables
+  const char* sxe = getenv("DK_SYMIDX");  // 1: always, 0: never (tests, A/B)
+  if (sym && (sxe ? sxe[0] == '1' : nq * 8 >= P.rstride)) {
+    if (c->sx_gen != c->tables_gen) {
+      uint64_t maxlen = 1;
+      for (int k = 0; k < T.nseg; ++k) maxlen = std::max<uint64_t>(maxlen, T.seg_len[k]);
+      size_t tb = 0;
+      HIPCHK(symidx_scan_bytes(maxlen, &tb));
+      HIPCHK(c->sx_posof.reserve((uint64_t)T.nseg * c->nrows * 4 + 4, 0, s));
+      HIPCHK(c->sx_hflag.reserve(P.rstride * 4 + 4, 0, s));
+      HIPCHK(c->sx_bstart.reserve(P.rstride * 4 + 4, 0, s));
+      HIPCHK(c->sx_bend.reserve(P.rstride * 4 + 4, 0, s));
+      HIPCHK(c->sx_tmp.reserve(tb + 16, 0, s));
+      HIPCHK(hipMemsetAsync(c->sx_posof.p, 0xFF, (uint64_t)T.nseg * c->nrows * 4, s));
+      HIPCHK(launch_symidx(T, c->nrows, c->sx_posof.as<uint32_t>(), c->sx_hflag.as<uint32_t>(),
+                           c->sx_bstart.as<uint32_t>(), c->sx_bend.as<uint32_t>(), c->sx_tmp.p, tb, s));
+      c->sx_gen = c->tables_gen;
+    }
+    sx = SymIndex{c->sx_posof.as<uint32_t>(), c->sx_bstart.as<uint32_t>(), c->sx_bend.as<uint32_t>(), c->nrows};
+  }
   if (sym) {
     HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 16 + 16, 0, s));
     HIPCHK(c->counts.reserve((nq + 1) * 8, 0, s));
@@ -2540,7 +2565,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
     HIPCHK(launch_count_sym(c->d_queries.as<uint32_t>(), nq, T, r0, c->ranges.as<uint4>(),
                             c->counts.as<uint64_t>(), c->ocounts.as<uint64_t>(),
-                            c->mcounts.as<uint64_t>(), c->counters.as<uint64_t>() + 2, two ? 32u : 64u, s));
+                            c->mcounts.as<uint64_t>(), c->counters.as<uint64_t>() + 2, two ? 32u : 64u, sx, s));
     HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->ocounts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->mcounts.as<uint64_t>() + nq, 0, 8, s));

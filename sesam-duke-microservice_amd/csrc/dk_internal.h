@@ -494,9 +494,21 @@ hipError_t launch_task_keys(const PairSource& src, uint64_t ntask, const uint64_
                             uint64_t* key, uint32_t* val, hipStream_t s);
 // symmetric dedup schedule: per query its bucket positions (sranges), full and owner slot
 // counts (each padded to 64), real[0] += the unpadded full total
+// the symmetric schedule's bucket lookup (k_count_sym's fast path; posof null: binary searches)
+struct SymIndex {
+  const uint32_t* posof;   // [segment * nrows + row]: position in the segment, kNoPos: none
+  const uint32_t* bstart;  // [replica position]: its bucket's first position (segment-relative)
+  const uint32_t* bend;    // [replica position of a bucket's first entry]: the bucket's end
+  uint64_t nrows;
+};
 hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
                             uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* mcounts,
-                            uint64_t* real, uint32_t opad, hipStream_t s);
+                            uint64_t* real, uint32_t opad, const SymIndex& X, hipStream_t s);
+// builds SymIndex over every segment of T (hflag: scratch of one u32 per replica position;
+// tmp: symidx_scan_bytes of the longest segment)
+hipError_t launch_symidx(const BlockTables& T, uint64_t nrows, uint32_t* posof, uint32_t* hflag,
+                         uint32_t* bstart, uint32_t* bend, void* tmp, size_t tmp_bytes, hipStream_t s);
+hipError_t symidx_scan_bytes(uint64_t n, size_t* bytes);
 hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint64_t* mqoff,
                         uint64_t nq, int nseg, uint64_t* obase, uint64_t* mbase, hipStream_t s);
 // k_sym_emit over the chunk's queries [q0, q0 + nqc): write = false counts each query's

@@ -614,6 +614,8 @@ def test_symmetric_schedule_equals_direct(seed, monkeypatch):
                 monkeypatch.setenv("DK_CHUNK_SLOTS", chunk)
             else:
                 monkeypatch.delenv("DK_CHUNK_SLOTS", raising=False)
+            # the bucket lookup index (SymIndex) on the 3000-slot chunks, binary searches else
+            monkeypatch.setenv("DK_SYMIDX", "1" if chunk == "3000" else "0")
             eng.reset_profile()
             eng.set_profiling(True)
             res = eng.match(q)
@@ -660,8 +662,9 @@ def sym2_case(seed, n=3000):
 @pytest.mark.parametrize("seed", [43, 44])
 def test_sym2_two_queries_per_wave(seed, monkeypatch):
     """k_score_sym2 (owner slots padded to 32, a query per half-wave) bit-exact against the
-    oracle, against one query per wave (DK_SYM2=0) and against the direct schedule
-    (DK_SYM=0), with superseded and deleted rows, a delta segment, one chunk and many."""
+    oracle, against one query per wave (DK_SYM2=0), against the direct schedule (DK_SYM=0) and
+    with the bucket lookup index of large batches (DK_SYMIDX=1: SymIndex instead of binary
+    searches), with superseded and deleted rows, a delta segment, one chunk and many."""
     props, vals, keys = sym2_case(seed)
     n = len(vals[0])
     rng = np.random.default_rng(seed)
@@ -681,14 +684,14 @@ def test_sym2_two_queries_per_wave(seed, monkeypatch):
                 monkeypatch.setenv("DK_CHUNK_SLOTS", chunk)
             else:
                 monkeypatch.delenv("DK_CHUNK_SLOTS", raising=False)
-            for env in ({}, {"DK_SYM2": "0"}, {"DK_SYM": "0"}):
+            for env in ({}, {"DK_SYM2": "0"}, {"DK_SYM": "0"}, {"DK_SYMIDX": "1"}):
                 for k, v in env.items():
                     monkeypatch.setenv(k, v)
                 eng.reset_profile()
                 res = eng.match(q)
                 prof = eng.profile()
                 assert prof["sym_matches"] == (0 if env.get("DK_SYM") == "0" else 1)
-                assert prof["sym2_matches"] == (1 if not env else 0)
+                assert prof["sym2_matches"] == (0 if env.get("DK_SYM") == "0" or env.get("DK_SYM2") == "0" else 1)
                 assert_same(res, ref)
                 res.close()
                 for k in env:
