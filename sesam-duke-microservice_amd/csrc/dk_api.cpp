@@ -2565,7 +2565,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(hipMemsetAsync(c->counters.as<uint64_t>() + 2, 0, 8, s));
     HIPCHK(launch_count_sym(c->d_queries.as<uint32_t>(), nq, T, r0, c->ranges.as<uint4>(),
                             c->counts.as<uint64_t>(), c->ocounts.as<uint64_t>(),
-                            c->mcounts.as<uint64_t>(), c->counters.as<uint64_t>() + 2, two ? 32u : 64u, sx, s));
+                            c->mcounts.as<uint64_t>(), c->counters.as<uint64_t>() + 2, two ? 1u : 64u, sx, s));
+    if (two) HIPCHK(launch_opack(c->ocounts.as<uint64_t>(), nq, s));  // waves of at most two queries
     HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->ocounts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->mcounts.as<uint64_t>() + nq, 0, 8, s));
@@ -2627,7 +2628,12 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(hipMemcpyAsync(hb, c->bval.p, nb * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     obounds.assign(hb, hb + nb);
-    for (size_t i = 0; i + 1 < obounds.size(); ++i) ochunk = std::max(ochunk, obounds[i + 1] - obounds[i]);
+    // a half holds the chunk's slots from the wave of its first one (k_score_sym2's chunks
+    // start inside a wave), plus 64 B the count pass's 16-B reads may touch past the end:
+    // slot s of chunk ci at half + s - (obounds[ci] & ~63), 16-B aligned like s
+    for (size_t i = 0; i + 1 < obounds.size(); ++i)
+      ochunk = std::max(ochunk, obounds[i + 1] - (obounds[i] & ~(uint64_t)63));
+    ochunk = (ochunk + 127) & ~(uint64_t)63;
     // mirror results live for the whole call (a query's emission reads what earlier
     // queries pushed): a decision byte + 8 B per mirror slot; owner results for one chunk
     // (its emission reads only its own queries' owner slots): two chunk-sized halves of a
@@ -2649,9 +2655,10 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(c->eincl.reserve(nq * 8 + 8, 0, s));
     HIPCHK(c->mbase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
     HIPCHK(hipMemsetAsync(c->mkind.p, 0, mtot, s));  // no entry unless an owner pushes one
-    HIPCHK(c->owq.reserve(otot / 32 * 4 + 4, 0, s));
+    HIPCHK(c->owq.reserve(otot / 64 * 8 + 8, 0, s));
     HIPCHK(c->obase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
-    HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s, two ? 5 : 6));
+    if (two) HIPCHK(launch_wavemap2(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint2>(), s));
+    else HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s));
     HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), c->mqoff.as<uint64_t>(),
                         nq, T.nseg, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
   } else if (!allpairs && !lucene) {
@@ -2762,6 +2769,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     src.sym = 1;
     src.two = two ? 1 : 0;
     src.wq = c->owq.as<uint32_t>();
+    src.wq2 = two ? c->owq.as<uint2>() : nullptr;
     src.qoff = c->oqoff.as<uint64_t>();
     src.sranges = c->ranges.as<uint4>();
     src.mkind = c->mkind.as<uint8_t>();
@@ -2892,9 +2900,9 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
         Timer t_gather(c, &c->prof.ms_gather, s);
         EmitSource e = esrc;  // chunk ci's owner results: half b, indexed by absolute owner slot
         const uint64_t o0 = obounds[ci];
-        e.okind = c->okind.as<uint8_t>() + (uint64_t)b * ochunk - o0;
+        e.okind = c->okind.as<uint8_t>() + (uint64_t)b * ochunk - (o0 & ~(uint64_t)63);
         e.ores = reinterpret_cast<const double*>(
-            reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - o0 * sizeof(double));
+            reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - (o0 & ~(uint64_t)63) * sizeof(double));
         HIPCHK(launch_sym_emit(e, bounds[ci], bounds[ci + 1] - bounds[ci], true, nm, ml,
                                B.d_first.as<uint64_t>(), s));
         t_gather.stop();
@@ -2958,15 +2966,19 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       // (half b, indexed by the absolute owner slot o0..o1-1) and the mirror results
       const uint64_t o0 = obounds[ci], o1 = obounds[ci + 1];
       PairSource osrc = src;
-      osrc.okind = c->okind.as<uint8_t>() + (uint64_t)b * ochunk - o0;
+      osrc.okind = c->okind.as<uint8_t>() + (uint64_t)b * ochunk - (o0 & ~(uint64_t)63);
       osrc.ores = reinterpret_cast<double*>(
-          reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - o0 * sizeof(double));
+          reinterpret_cast<uintptr_t>(c->ores.as<double>() + (uint64_t)b * ochunk) - (o0 & ~(uint64_t)63) * sizeof(double));
+      // k_score_sym2's chunks start inside a wave (packed owner slots): its launch starts at
+      // the wave, the slots before o0 are left to the previous chunk
+      const uint64_t w0 = o0 & ~(uint64_t)63;
+      osrc.olo = o0;
       {
         Timer t_score(c, &c->prof.ms_score, s);
-        HIPCHK(launch_score(P, osrc, o0, o1 - o0, so, s));
+        HIPCHK(launch_score(P, osrc, w0, o1 - w0, so, s));
         t_score.stop();
       }
-      HIPCHK(launch_reduce_blocks(so, (o1 - o0 + kScoreBlock - 1) / kScoreBlock, s));
+      HIPCHK(launch_reduce_blocks(so, (o1 - w0 + kScoreBlock - 1) / kScoreBlock, s));
       // phase 2: entries per query of the chunk, their inclusive scan, the chunk's total
       EmitSource e = esrc;
       e.okind = osrc.okind;

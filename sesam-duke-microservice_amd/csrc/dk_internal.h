@@ -164,7 +164,9 @@ struct PairSource {
   uint64_t mpad;            // m rounded up to a wave (64)
   int32_t same_ok;          // score pairs of one identity too (dk_compare_rows)
   int32_t sym;              // 1: owner slots of the symmetric dedup schedule (below)
-  int32_t two;              // SYM: owner slots padded to 32, wq per half-wave (k_score_sym2)
+  int32_t two;              // SYM: k_score_sym2's packed owner slots (k_opack): wq2 per wave
+  const uint2* wq2;         // {query of the wave's first slot, query of its last slot}
+  uint64_t olo;             // first owner slot of the launch's queries (slot0 is wave-aligned)
   // Symmetric dedup schedule: queries are the contiguous rows [r0, r1);
   // per (key function k, query qi) sranges[k * nq + qi] = {lo, hi, qa, pq}: the bucket
   // [lo, hi) of the query's key in sorted table k, qa = first position with row >= r0,
@@ -468,9 +470,13 @@ hipError_t launch_count(const uint32_t* queries, uint64_t nq, const BlockTables&
 // counts[i] = candidate slots of query i, unpadded (dk_candidate_counts)
 hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockTables& T,
                               uint2* ranges, uint64_t* counts, hipStream_t s);
-// wq[w] = qi for the waves of query qi's slots (qoff in slots, multiples of 64)
-// wq[w] = qi for every group w of 2^shift slots of query qi (shift 6: waves, 5: half-waves)
+// wq[w] = qi for every group w of 2^shift slots of query qi (qoff in multiples of 2^shift)
 hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s, int shift = 6);
+// k_score_sym2's owner slots: own[i] (owned candidates) -> the query's slots with the
+// padding that keeps every wave to two queries (k_opack); their scan is oqoff, and
+// wq2[w] = {query of wave w's first slot, query of its last slot}
+hipError_t launch_opack(uint64_t* own, uint64_t nq, hipStream_t s);
+hipError_t launch_wavemap2(const uint64_t* qoff, uint64_t nq, uint2* wq2, hipStream_t s);
 // replica-ordered identity and keys 0..nkeys-2 of the rows at replica positions
 hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t pos0, uint64_t npos,
                                  const uint64_t* ident, uint64_t* rident, const BlockTables& T,

@@ -1384,42 +1384,48 @@ void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t n
   score_body<RMAX, 0, SYM, true, GR>(P, S, slot0, nslots, out);
 }
 
-// The symmetric owner schedule with TWO queries per wave (PairSource::two): every query's
-// owner slots are padded to 32, not 64, so each half-wave holds one query and a wave at most
-// two -- configs[1]'s owned lists waste 6.7 % of their slots on padding instead of 13.3 %.
+// The symmetric owner schedule with TWO queries per wave (PairSource::two): the owner slots
+// are packed so that a wave holds at most two queries, the second from any lane on (k_opack)
+// -- configs[1]'s owned lists waste ~2 % of their slots on padding, against 13.3 % with every
+// query padded to a wave (6.7 % to a half-wave).
 // Schemas of Latin-1 Levenshtein / JaroWinkler, Exact and Numeric properties in one HashMap
 // order class (the host checks: dk_api.cpp sym2_ok): the wave's two Peq tables fit its LDS
 // slice (256 entries each), the row bucket covers the longer query value, and the query side
-// of every comparator is per lane (its half's query); the rest is score_body's SYM path.
+// of every comparator is per lane (its query); the rest is score_body's SYM path.
 template <int RMAX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? DK_WAVES_SHORT : 4, 8)))
 void k_score_sym2(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
   uint64_t* tab = g_wave_tables[threadIdx.x >> 6];
   for (int e = (int)lane_id(); e < kPeqEntries; e += 64) tab[e] = 0;
   const int lane = (int)lane_id();
-  const bool hi = lane >= 32;
   const uint64_t bid = blockIdx.x;
   const uint64_t idx = bid * blockDim.x + threadIdx.x;
-  const bool in_launch = idx < nslots;
-  bool valid = in_launch;
   const uint64_t s = slot0 + min(idx, nslots - 1);
-  // the two half-waves' queries (scalar loads; equal when one query fills the wave)
+  // slot0 is wave-aligned: the launch's first wave may start with the previous launch's
+  // query (slots below olo: neither scored nor written)
+  const bool in_launch = idx < nslots && s >= S.olo;
+  bool valid = in_launch;
+  // the wave's two queries (scalar loads; equal when one query fills the wave): A from lane
+  // 0, B from its first slot qoff[B] on
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t w0 = bid * blockDim.x + (uint64_t)wave * 64u;
-  const uint32_t qiA = __builtin_amdgcn_readfirstlane(S.wq[(slot0 + min(w0, nslots - 1)) >> 5]);
-  const uint32_t qiB = __builtin_amdgcn_readfirstlane(S.wq[(slot0 + min(w0 + 32u, nslots - 1)) >> 5]);
+  const uint2 wqp = S.wq2[(slot0 + min(w0, nslots - 1)) >> 6];
+  const uint32_t qiA = __builtin_amdgcn_readfirstlane(wqp.x);
+  const uint32_t qiB = __builtin_amdgcn_readfirstlane(wqp.y);
   const bool two = qiA != qiB;  // wave-uniform
+  const uint64_t offA = S.qoff[qiA], offB = S.qoff[qiB];
+  const bool hi = two && s >= offB;
   const uint32_t qA = __builtin_amdgcn_readfirstlane(S.queries[qiA]);
   const uint32_t qB = __builtin_amdgcn_readfirstlane(S.queries[qiB]);
   const uint32_t q = hi ? qB : qA;
-  uint64_t* peq = tab + (two && hi ? 256 : 0);  // this lane's query's Peq table
+  uint64_t* peq = tab + (hi ? 256 : 0);  // this lane's query's Peq table
   uint32_t g = 0;
   bool mirror = false;
   int ksel = 0;
   uint32_t moff = 0;
   {
     // owner slot t of the lane's query: key function k's owned range [lo, qa) then (pq, hi)
-    uint64_t t = s - (hi ? S.qoff[qiB] : S.qoff[qiA]);
+    uint64_t t = s - (hi ? offB : offA);
     int k = -1;
     constexpr int kPre = 2;  // the two queries' first ranges as scalars (SGPR budget)
     uint4 pa[kPre], pb[kPre];
@@ -1559,7 +1565,7 @@ void k_score_sym2(const ScoreParams P, const PairSource S, uint64_t slot0, uint6
     }
   }
   const uint32_t kind = valid ? decide(prob, P.threshold, P.maybe) : 0u;
-  if (in_launch) {
+  if (in_launch) {  // padding slots too (the count pass reads them as 0)
     S.okind[s] = (uint8_t)kind;
     if (kind != 0u) S.ores[s] = prob;
   }
@@ -2185,6 +2191,59 @@ __global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32
   for (uint64_t w = qoff[i] >> shift, e = qoff[i + 1] >> shift; w < e; ++w) wq[w] = (uint32_t)i;
 }
 
+// k_score_sym2's owner slot layout: waves hold at most two queries, each from any lane on.
+// One thread per tile of kPackTile queries places them greedily (tiles start at a wave):
+// a query starts on the next free lane unless a query already started inside that wave
+// (then the wave's rest is padding, at the end of the previous query's slots); each tile
+// ends at a wave.  own[i] (the query's owned slots) becomes its slots with trailing padding,
+// whose exclusive scan is oqoff.  Padding is ~2 % of the slots, against ~7 % when every
+// query is padded to a half-wave.
+constexpr int kPackTile = 256;
+
+__global__ void k_opack(uint64_t* __restrict__ own, uint64_t nq) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t q0 = t * kPackTile;
+  if (q0 >= nq) return;
+  const uint64_t q1 = min(nq, q0 + kPackTile);
+  uint32_t p = 0;       // next free lane of the current wave
+  bool started = false; // a query started inside the current wave (not at lane 0)
+  uint64_t last = ~0ull, lastv = 0;
+  constexpr int kBatch = 16;  // counts loaded a batch at a time (the walk is serial)
+  for (uint64_t qb = q0; qb < q1; qb += kBatch) {
+    uint64_t v[kBatch];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) v[i] = qb + i < q1 ? own[qb + i] : 0u;
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const uint64_t L = v[i];
+      if (L == 0) continue;
+      if (p > 0 && started) {  // a third query would share the wave: pad it
+        lastv += 64u - p;
+        p = 0;
+        started = false;
+      }
+      if (last != ~0ull) own[last] = lastv;
+      started = p > 0;
+      const uint64_t e = p + L;
+      if (e >= 64) started = false;  // the query reaches the next wave: it is that wave's first
+      p = (uint32_t)(e & 63u);
+      last = qb + i;
+      lastv = L;
+    }
+  }
+  if (last != ~0ull) own[last] = lastv + (p ? 64u - p : 0u);
+}
+
+// wave w of k_score_sym2's owner slots -> {query of its first slot, query of its last slot}
+// (one thread per query over the waves whose first / last slot lies in its range)
+__global__ void k_wavemap2(const uint64_t* __restrict__ qoff, uint64_t nq, uint2* __restrict__ wq2) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  const uint64_t a = qoff[i], e = qoff[i + 1];
+  for (uint64_t w = (a + 63) >> 6, we = (e + 63) >> 6; w < we; ++w) wq2[w].x = (uint32_t)i;
+  for (uint64_t w = a >> 6, we = e >> 6; w < we; ++w) wq2[w].y = (uint32_t)i;
+}
+
 // replica-ordered identity and keys (the score kernel's candidate filters read them
 // coalesced, 64 consecutive positions per wave)
 __global__ __launch_bounds__(256) void k_replicate_rows(const uint32_t* __restrict__ rowof, uint64_t pos0,
@@ -2552,6 +2611,18 @@ hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockT
 hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s, int shift) {
   DK_LAUNCH_GUARD(nq);
   k_wavemap<<<grid1d(nq), 256, 0, s>>>(qoff, nq, wq, shift);
+  return hipGetLastError();
+}
+
+hipError_t launch_opack(uint64_t* own, uint64_t nq, hipStream_t s) {
+  DK_LAUNCH_GUARD(nq);
+  k_opack<<<grid1d((nq + kPackTile - 1) / kPackTile), 256, 0, s>>>(own, nq);
+  return hipGetLastError();
+}
+
+hipError_t launch_wavemap2(const uint64_t* qoff, uint64_t nq, uint2* wq2, hipStream_t s) {
+  DK_LAUNCH_GUARD(nq);
+  k_wavemap2<<<grid1d(nq), 256, 0, s>>>(qoff, nq, wq2);
   return hipGetLastError();
 }
 
