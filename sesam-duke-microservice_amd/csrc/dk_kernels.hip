@@ -19,9 +19,7 @@
 #include "dk_internal.h"
 #include "dk_device.h"
 
-#ifndef DK_JW_NARROW
-#define DK_JW_NARROW 32  // JaroWinkler on 32-bit position masks up to this query length
-#endif
+#define DK_JW_NARROW 32  // JaroWinkler on 32-bit position masks up to this query length (kPeqNarrow)
 #ifndef DK_WAVES_SHORT
 #define DK_WAVES_SHORT 5  // k_score waves per SIMD up to 40 Levenshtein rows
 #endif
@@ -41,33 +39,36 @@ struct RowKeys {
   uint64_t* p[kMaxKeys];
 };
 
-template <typename CT>
-__device__ __forceinline__ void peq_set(uint64_t* peq, const CT* s, int n, bool on) {
-  const int lane = (int)lane_id();
-  if (lane < n) {
-    const uint32_t ch = s[lane];
-    const uint64_t bit = 1ull << lane;
-    if (sizeof(CT) == 1) {
-      if (on) atomicOr((unsigned long long*)&peq[ch], (unsigned long long)bit);
-      else peq[ch] = 0;
-    } else {
-      if (on) {
-        atomicOr((unsigned long long*)&peq[ch & 0xFF], (unsigned long long)bit);
-        atomicOr((unsigned long long*)&peq[256 + (ch >> 8)], (unsigned long long)bit);
-      } else {
-        peq[ch & 0xFF] = 0;
-        peq[256 + (ch >> 8)] = 0;
-      }
-    }
-  }
-  wave_lds_sync();
-}
+// Peq tables of a query value (bit i of entry c: unit i is c; UTF-16 units split into a low-
+// and a high-byte table whose entries are ANDed).  A query of up to kPeqNarrow units gets
+// NARROW tables of 32-bit entries (entry c at dword c): its readers take 32-bit masks
+// (JaroWinkler's, and Levenshtein's row buckets up to 32), and consecutive characters then
+// fall in distinct LDS banks -- entry c of a 64-bit table read as its low dword sits at
+// dword 2c, so characters 16 apart ('a' / 'q') share a bank (scripts/micro/lds_probe.hip).
+// Longer queries: 64-bit entries.
+constexpr int kPeqNarrow = 32;
+__device__ __forceinline__ bool peq_narrow(int n) { return n <= kPeqNarrow; }
 
-// the same with this lane's query unit already in a register (prefetched by the caller)
+// this lane's query unit (prefetched by the caller) set into / cleared from the tables
 template <typename CT>
 __device__ __forceinline__ void peq_set_unit(uint64_t* peq, uint32_t ch, int n, bool on) {
   const int lane = (int)lane_id();
-  if (lane < n) {
+  if (lane < n && peq_narrow(n)) {
+    uint32_t* p32 = reinterpret_cast<uint32_t*>(peq);
+    const uint32_t bit = 1u << lane;
+    if (sizeof(CT) == 1) {
+      if (on) atomicOr(&p32[ch], bit);
+      else p32[ch] = 0;
+    } else {
+      if (on) {
+        atomicOr(&p32[ch & 0xFF], bit);
+        atomicOr(&p32[256 + (ch >> 8)], bit);
+      } else {
+        p32[ch & 0xFF] = 0;
+        p32[256 + (ch >> 8)] = 0;
+      }
+    }
+  } else if (lane < n) {
     const uint64_t bit = 1ull << lane;
     if (sizeof(CT) == 1) {
       if (on) atomicOr((unsigned long long*)&peq[ch], (unsigned long long)bit);
@@ -92,14 +93,14 @@ __device__ __forceinline__ uint64_t peq_eq(const uint64_t* peq, uint32_t x) {
 }
 
 // Peq lookups and window masks at the width of the query's position masks: 32 bits when
-// the query value has <= 32 units (wave-uniform), which halves the mask arithmetic and
-// reads only the low half of each 64-bit Peq entry.
+// the query value has <= kPeqNarrow units (wave-uniform), which halves the mask arithmetic;
+// the tables are then narrow (peq_set_unit).
 template <typename MT, typename CT>
 __device__ __forceinline__ MT peq_eq_t(const uint64_t* peq, uint32_t x) {
   if (sizeof(MT) == 8) return (MT)peq_eq<CT>(peq, x);
-  const uint32_t* p32 = reinterpret_cast<const uint32_t*>(peq);  // little-endian low halves
-  if (sizeof(CT) == 1) return (MT)p32[2 * x];
-  return (MT)(p32[2 * (x & 0xFF)] & p32[2 * (256 + (x >> 8))]);
+  const uint32_t* p32 = reinterpret_cast<const uint32_t*>(peq);
+  if (sizeof(CT) == 1) return (MT)p32[x];
+  return (MT)(p32[x & 0xFF] & p32[256 + (x >> 8)]);
 }
 
 __device__ __forceinline__ uint64_t range_mask(int lo, int hi) {  // bits [lo, hi), 0<=lo<=hi<=64
@@ -790,7 +791,7 @@ __device__ __forceinline__ double jarowinkler_peq(const uint64_t* peq, const Str
   constexpr int UPW = Str<CT>::UPW;
   // Units past a candidate's end read as 0 (zero padded): Peq[0] is empty unless the
   // query itself holds U+0000 (wave-uniform), and only then do lanes mask past-end units.
-  const bool nul = peq_eq<CT>(peq, 0u) != 0ull;
+  const bool nul = peq_eq_t<MT, CT>(peq, 0u) != (MT)0;
   if (sizeof(MT) == 4) {
     // 32-bit masks (query <= 32 units): the window [j + lo_off, j + hi_off) slides one
     // position per unit, so it is a 64-bit register shifted left once per step whose high
@@ -1494,15 +1495,29 @@ void k_score_sym2(const ScoreParams P, const PairSource S, uint64_t slot0, uint6
   };
   // the wave's Peq tables: query A's in [0, 256), query B's in [256, 512) (two queries) --
   // set (on) or cleared
+  // (narrow: 32-bit entries, peq_set_unit, when both queries have <= kPeqNarrow units)
   auto tables = [&](int la, int lb, uint32_t ca, uint32_t cb, bool on) {
-    const uint64_t bit = 1ull << lane;
-    if (lane < la) {
-      if (on) atomicOr((unsigned long long*)&tab[ca], (unsigned long long)bit);
-      else tab[ca] = 0;
-    }
-    if (two && lane < lb) {
-      if (on) atomicOr((unsigned long long*)&tab[256 + cb], (unsigned long long)bit);
-      else tab[256 + cb] = 0;
+    if (peq_narrow(max(la, lb))) {
+      uint32_t* t32 = reinterpret_cast<uint32_t*>(tab);
+      const uint32_t bit = 1u << (lane & 31);
+      if (lane < la) {
+        if (on) atomicOr(&t32[ca], bit);
+        else t32[ca] = 0;
+      }
+      if (two && lane < lb) {
+        if (on) atomicOr(&t32[512 + cb], bit);
+        else t32[512 + cb] = 0;
+      }
+    } else {
+      const uint64_t bit = 1ull << lane;
+      if (lane < la) {
+        if (on) atomicOr((unsigned long long*)&tab[ca], (unsigned long long)bit);
+        else tab[ca] = 0;
+      }
+      if (two && lane < lb) {
+        if (on) atomicOr((unsigned long long*)&tab[256 + cb], (unsigned long long)bit);
+        else tab[256 + cb] = 0;
+      }
     }
     wave_lds_sync();
   };
