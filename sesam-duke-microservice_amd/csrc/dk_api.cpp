@@ -557,6 +557,7 @@ struct dk_ctx {
   // symmetric dedup schedule: owner slot counts / offsets / wave map,
   // per-(key, query) bucket positions, owner results, chunk boundaries
   DevBuf ocounts, oqoff, owq, obase, okind, ores, mcounts, mqoff, mbase, mkind, mres, ecount, eincl, bidx, bval;
+  DevBuf ploc, ptot, pbase;  // k_opack: first slot within the tile, tile slots, their scan
   // k_count_sym's bucket lookup for large batches (SymIndex), built once per table build
   DevBuf sx_posof, sx_hflag, sx_bstart, sx_bend, sx_tmp;
   uint64_t sx_gen = 0;
@@ -2234,6 +2235,20 @@ static bool sym2_ok(const dk_ctx* c, const ScoreParams& P) {
   return true;
 }
 
+// k_opack's order within a tile: the query's length on the schema's longest Levenshtein
+// property (the DP whose row bucket costs most), or none (DK_SYM_ORDER=0: query order)
+static const uint16_t* sym2_order_len(const dk_ctx* c, const ScoreParams& P) {
+  const char* e = getenv("DK_SYM_ORDER");
+  if (e && e[0] == '0') return nullptr;
+  int best = -1, bl = 0;
+  for (int p = 0; p < P.nprops; ++p)
+    if (P.props[p].op == DK_CMP_LEVENSHTEIN && c->P[p].maxlen > bl) {
+      best = p;
+      bl = c->P[p].maxlen;
+    }
+  return best < 0 ? nullptr : P.props[best].len;
+}
+
 static bool sym_enabled() {
   const char* e = getenv("DK_SYM");
   return !(e && e[0] == '0');
@@ -2566,7 +2581,6 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(launch_count_sym(c->d_queries.as<uint32_t>(), nq, T, r0, c->ranges.as<uint4>(),
                             c->counts.as<uint64_t>(), c->ocounts.as<uint64_t>(),
                             c->mcounts.as<uint64_t>(), c->counters.as<uint64_t>() + 2, two ? 1u : 64u, sx, s));
-    if (two) HIPCHK(launch_opack(c->ocounts.as<uint64_t>(), nq, s));  // waves of at most two queries
     HIPCHK(hipMemsetAsync(c->counts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->ocounts.as<uint64_t>() + nq, 0, 8, s));
     HIPCHK(hipMemsetAsync(c->mcounts.as<uint64_t>() + nq, 0, 8, s));
@@ -2576,9 +2590,25 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
       return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
     }));
-    HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
-      return exclusive_scan_u64(t, b, c->ocounts.as<uint64_t>(), c->oqoff.as<uint64_t>(), nq + 1, s);
-    }));
+    if (two) {
+      // waves of at most two queries, per tile of 256 queries (in the order of their length
+      // on the longest Levenshtein property; DK_SYM_ORDER=0: query order)
+      const uint64_t nt = opack_tiles(nq);
+      HIPCHK(c->ploc.reserve(nq * 4 + 4, 0, s));
+      HIPCHK(c->ptot.reserve((nt + 1) * 8, 0, s));
+      HIPCHK(c->pbase.reserve((nt + 1) * 8, 0, s));
+      HIPCHK(launch_opack(c->ocounts.as<uint64_t>(), nq, c->d_queries.as<uint32_t>(), sym2_order_len(c, P),
+                          c->ploc.as<uint32_t>(), c->ptot.as<uint64_t>(), s));
+      HIPCHK(hipMemsetAsync(c->ptot.as<uint64_t>() + nt, 0, 8, s));
+      HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+        return exclusive_scan_u64(t, b, c->ptot.as<uint64_t>(), c->pbase.as<uint64_t>(), nt + 1, s);
+      }));
+      HIPCHK(launch_opack_fin(c->ploc.as<uint32_t>(), c->pbase.as<uint64_t>(), nq, c->oqoff.as<uint64_t>(), s));
+    } else {
+      HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
+        return exclusive_scan_u64(t, b, c->ocounts.as<uint64_t>(), c->oqoff.as<uint64_t>(), nq + 1, s);
+      }));
+    }
     HIPCHK(hipMemcpyAsync(&hs[3], c->qoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&hs[2], c->counters.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&hs[1], c->oqoff.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, s));
@@ -2604,14 +2634,17 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   std::vector<uint64_t> qb, obounds;
   uint64_t ochunk = 1;
   if (sym) {
+    // k_score_sym2's chunks are whole tiles of k_opack (its queries are ordered per tile)
+    const uint64_t qg = two ? 256 : 1;
+    auto qcut = [&](uint64_t x) { return std::min(nq, (x + qg / 2) / qg * qg); };
     qb.push_back(0);
     const uint64_t nch = std::max<uint64_t>(1, (total + chunk_len(total) - 1) / chunk_len(total));
-    for (uint64_t i = 1; i < nch; ++i) qb.push_back(nq * i / nch);
+    for (uint64_t i = 1; i < nch; ++i) qb.push_back(qcut(nq * i / nch));
     qb.push_back(nq);
     if (!(flags & DK_MATCH_DEVICE)) {  // halve the last chunk twice
       for (int h = 0; h < 2; ++h) {
         const uint64_t a = qb[qb.size() - 2], e = qb.back();
-        if (e - a >= 2) qb.insert(qb.end() - 1, a + (e - a) / 2);
+        if (e - a >= 2 * qg) qb.insert(qb.end() - 1, qcut(a + (e - a) / 2));
       }
     }
     // more chunks than queries (small slot chunks): no empty chunk -- its count read-back
@@ -2622,9 +2655,10 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(c->bval.reserve(nb * 8 + 8, 0, s));
     HIPCHK(c->h_bounds.reserve(nb * 8 + 8));
     uint64_t* hb = c->h_bounds.as<uint64_t>();
-    memcpy(hb, qb.data(), nb * 8);
+    for (uint64_t i = 0; i < nb; ++i) hb[i] = two ? (qb[i] + qg - 1) / qg : qb[i];  // tile / query
     HIPCHK(hipMemcpyAsync(c->bidx.p, hb, nb * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_gather_u64(c->oqoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb, c->bval.as<uint64_t>(), s));
+    HIPCHK(launch_gather_u64(two ? c->pbase.as<uint64_t>() : c->oqoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb,
+                             c->bval.as<uint64_t>(), s));
     HIPCHK(hipMemcpyAsync(hb, c->bval.p, nb * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     obounds.assign(hb, hb + nb);
@@ -2657,7 +2691,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     HIPCHK(hipMemsetAsync(c->mkind.p, 0, mtot, s));  // no entry unless an owner pushes one
     HIPCHK(c->owq.reserve(otot / 64 * 8 + 8, 0, s));
     HIPCHK(c->obase.reserve((uint64_t)T.nseg * nq * 8 + 8, 0, s));
-    if (two) HIPCHK(launch_wavemap2(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint2>(), s));
+    if (two) HIPCHK(launch_wavemap2(c->oqoff.as<uint64_t>(), c->ocounts.as<uint64_t>(), nq, c->owq.as<uint2>(), s));
     else HIPCHK(launch_wavemap(c->oqoff.as<uint64_t>(), nq, c->owq.as<uint32_t>(), s));
     HIPCHK(launch_obase(c->ranges.as<uint4>(), c->oqoff.as<uint64_t>(), c->mqoff.as<uint64_t>(),
                         nq, T.nseg, c->obase.as<uint64_t>(), c->mbase.as<uint64_t>(), s));
@@ -2790,6 +2824,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     esrc.eincl = c->eincl.as<uint64_t>();
     esrc.oqoff = c->oqoff.as<uint64_t>();
     esrc.mqoff = c->mqoff.as<uint64_t>();
+    esrc.ocnt = two ? c->ocounts.as<uint64_t>() : nullptr;
     HIPCHK(B.d_first.reserve((nq + 1) * 8, 0, s));  // k_sym_emit writes first[] per chunk
   }
   // k_score_grouped: the tasks of each chunk in the order of their first candidate's replica

@@ -25,8 +25,10 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // filtered candidate slot
 // (u0 << 16) | u1 (16 bits per UTF-16 unit); with both units < 256 the 16-bit bigram
 // (u0 << 8) | u1 is injective, and key = bigram + 1 (mod 2^16) is never 0 except for the
 // bigram U+00FF U+00FF, whose rows get no seed -- so a zero key is padding.  A row's seed
-// s = (lt - 8) << 8 | i names the table size 2^lt (lt 8..9) and multiplier gram_mult(i)
-// under which slot(key) = low32(key * mult) >> (32 - lt) is injective on the row's keys.
+// s = (lt - kGramLtMin) << 8 | i names the table size 2^lt (lt 6..9: the smallest that has a
+// seed, k_gram_seed) and multiplier gram_mult(i) under which slot(key) = low32(key * mult)
+// >> (32 - lt) is injective on the row's keys.
+constexpr int kGramLtMin = 6;
 constexpr uint16_t kGramSeedNone = 0xFFFF;
 constexpr int kGramSeedTries = 256;
 // grams of a set that get a seed (table <= 512 u32): a property whose longest set has more
@@ -299,6 +301,7 @@ struct EmitSource {
   const uint64_t* eincl;    // per query: inclusive prefix of ecount over its chunk's queries
   const uint64_t* oqoff;    // per query: first owner slot (its owned run: up to oqoff[qi + 1])
   const uint64_t* mqoff;    // per query: first mirror slot (its mirror runs: up to mqoff[qi + 1])
+  const uint64_t* ocnt;     // non-null (k_opack's tile order): the owned run is [oqoff, + ocnt)
 };
 
 // Per-chunk staging of the score kernel.  Block b (256 slots) writes its emitted entries,
@@ -472,11 +475,17 @@ hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockT
                               uint2* ranges, uint64_t* counts, hipStream_t s);
 // wq[w] = qi for every group w of 2^shift slots of query qi (qoff in multiples of 2^shift)
 hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s, int shift = 6);
-// k_score_sym2's owner slots: own[i] (owned candidates) -> the query's slots with the
-// padding that keeps every wave to two queries (k_opack); their scan is oqoff, and
-// wq2[w] = {query of wave w's first slot, query of its last slot}
-hipError_t launch_opack(uint64_t* own, uint64_t nq, hipStream_t s);
-hipError_t launch_wavemap2(const uint64_t* qoff, uint64_t nq, uint2* wq2, hipStream_t s);
+// k_score_sym2's owner slots, per tile of 256 queries (k_opack): own[i] (owned candidates)
+// -> the query's slots with the padding that keeps every wave to two queries, loc[i] its
+// first slot within the tile (queries ordered by klen[queries[i]] when klen is given),
+// ttot[t] the tile's slots; oqoff[i] = tbase[tile] + loc[i] with tbase the exclusive scan
+// of ttot (k_opack_fin); wq2[w] = {query of wave w's first slot, query of its last slot}
+uint64_t opack_tiles(uint64_t nq);
+hipError_t launch_opack(uint64_t* own, uint64_t nq, const uint32_t* queries, const uint16_t* klen,
+                        uint32_t* loc, uint64_t* ttot, hipStream_t s);
+hipError_t launch_opack_fin(const uint32_t* loc, const uint64_t* tbase, uint64_t nq, uint64_t* oqoff,
+                            hipStream_t s);
+hipError_t launch_wavemap2(const uint64_t* qoff, const uint64_t* occ, uint64_t nq, uint2* wq2, hipStream_t s);
 // replica-ordered identity and keys 0..nkeys-2 of the rows at replica positions
 hipError_t launch_replicate_rows(const uint32_t* rowof, uint64_t pos0, uint64_t npos,
                                  const uint64_t* ident, uint64_t* rident, const BlockTables& T,

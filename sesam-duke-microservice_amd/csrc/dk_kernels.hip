@@ -937,7 +937,7 @@ __device__ __forceinline__ int count_members(const uint64_t* __restrict__ g1, in
 __device__ __forceinline__ int qgram_common_perfect(uint32_t* tab, const uint64_t* __restrict__ g1, int m1,
                                                     uint32_t seed, const uint64_t* __restrict__ rg,
                                                     uint64_t rstride, uint32_t g, int m2) {
-  const int lt = 8 + (int)(seed >> 8);
+  const int lt = kGramLtMin + (int)(seed >> 8);
   const uint32_t mult = gram_mult(seed & 0xFFu);
   const int sh = 32 - lt;
   const int lane = (int)lane_id();
@@ -1680,7 +1680,8 @@ __global__ __launch_bounds__(256) void k_sym_count(const EmitSource S, uint64_t 
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nqc) return;
   const uint64_t qi = q0 + i;
-  S.ecount[qi] = nz_run(S.okind, S.oqoff[qi], S.oqoff[qi + 1]) + nz_run(S.mkind, S.mqoff[qi], S.mqoff[qi + 1]);
+  const uint64_t oa = S.oqoff[qi], oe = S.ocnt ? oa + S.ocnt[qi] : S.oqoff[qi + 1];
+  S.ecount[qi] = nz_run(S.okind, oa, oe) + nz_run(S.mkind, S.mqoff[qi], S.mqoff[qi + 1]);
 }
 
 template <bool WRITE>
@@ -1960,24 +1961,30 @@ __global__ __launch_bounds__(256) void k_gram_seed(const uint64_t* __restrict__ 
   uint16_t out = kGramSeedNone;
   if (m > 0 && m <= kGramPerfectMax) {
     const uint64_t* g = grams + goff[row];
-    const int lt = m <= 32 ? 8 : 9;  // m <= kGramPerfectMax = 64
-    const int words = 1 << (lt - 5);
     uint32_t* bits = occ[threadIdx.x];
     bool zero = false;
     for (int k = 0; k < m; ++k) zero = zero || gram_key(g[k]) == 0u;
-    for (int t = 0; t < kGramSeedTries && !zero; ++t) {
-      const uint32_t mult = gram_mult((uint32_t)t);
-      for (int w = 0; w < words; ++w) bits[w] = 0u;
-      bool ok = true;
-      for (int k = 0; k < m && ok; ++k) {
-        const uint32_t h = (gram_key(g[k]) * mult) >> (32 - lt);
-        const uint32_t b = 1u << (h & 31u);
-        ok = (bits[h >> 5] & b) == 0u;
-        bits[h >> 5] |= b;
-      }
-      if (ok) {
-        out = (uint16_t)(((lt - 8) << 8) | t);
-        break;
+    // the smallest table first: a probe's LDS bank conflicts grow with the table's words per
+    // bank (none at 64 16-bit slots, scripts/micro/lds_probe.hip); m <= kGramPerfectMax = 64
+    const int lt_hi = m <= 32 ? 8 : 9;
+    for (int lt = lt_hi - 2; lt <= lt_hi && out == kGramSeedNone && !zero; ++lt) {
+      const int words = 1 << (lt - 5);
+      for (int t = 0; t < kGramSeedTries; ++t) {
+        const uint32_t mult = gram_mult((uint32_t)t);
+        // k_score_gq's slot-0 sentinel is a key in 1..64 whose slot is not 0
+        if (((64u * mult) >> (32 - lt)) == 0u) continue;
+        for (int w = 0; w < words; ++w) bits[w] = 0u;
+        bool ok = true;
+        for (int k = 0; k < m && ok; ++k) {
+          const uint32_t h = (gram_key(g[k]) * mult) >> (32 - lt);
+          const uint32_t b = 1u << (h & 31u);
+          ok = (bits[h >> 5] & b) == 0u;
+          bits[h >> 5] |= b;
+        }
+        if (ok) {
+          out = (uint16_t)(((lt - kGramLtMin) << 8) | t);
+          break;
+        }
       }
     }
   }
@@ -2207,54 +2214,102 @@ __global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32
 }
 
 // k_score_sym2's owner slot layout: waves hold at most two queries, each from any lane on.
-// One thread per tile of kPackTile queries places them greedily (tiles start at a wave):
-// a query starts on the next free lane unless a query already started inside that wave
-// (then the wave's rest is padding, at the end of the previous query's slots); each tile
-// ends at a wave.  own[i] (the query's owned slots) becomes its slots with trailing padding,
-// whose exclusive scan is oqoff.  Padding is ~2 % of the slots, against ~7 % when every
-// query is padded to a half-wave.
+// One workgroup per tile of kPackTile queries (tiles start at a wave and end at one): the
+// tile's queries ordered by `klen` (the query's length on the schema's longest Levenshtein
+// property, when given: a wave's DP row bucket follows its longer query, so neighbours of
+// similar length waste fewer rows), then placed greedily by one thread -- a query starts on
+// the next free lane unless a query already started inside that wave (the wave's rest is
+// then padding, at the end of the previous query's slots).  own[i] (the query's owned slots)
+// becomes its slots with trailing padding, loc[i] its first slot within the tile, ttot[t]
+// the tile's slots.  Padding is ~2 % of the slots, against ~7 % with every query padded to
+// a half-wave.
 constexpr int kPackTile = 256;
 
-__global__ void k_opack(uint64_t* __restrict__ own, uint64_t nq) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t q0 = t * kPackTile;
-  if (q0 >= nq) return;
-  const uint64_t q1 = min(nq, q0 + kPackTile);
-  uint32_t p = 0;       // next free lane of the current wave
-  bool started = false; // a query started inside the current wave (not at lane 0)
-  uint64_t last = ~0ull, lastv = 0;
-  constexpr int kBatch = 16;  // counts loaded a batch at a time (the walk is serial)
-  for (uint64_t qb = q0; qb < q1; qb += kBatch) {
-    uint64_t v[kBatch];
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) v[i] = qb + i < q1 ? own[qb + i] : 0u;
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-      const uint64_t L = v[i];
-      if (L == 0) continue;
-      if (p > 0 && started) {  // a third query would share the wave: pad it
-        lastv += 64u - p;
+__global__ __launch_bounds__(kPackTile) void k_opack(uint64_t* __restrict__ own, uint64_t nq,
+                                                     const uint32_t* __restrict__ queries,
+                                                     const uint16_t* __restrict__ klen,
+                                                     uint32_t* __restrict__ loc, uint64_t* __restrict__ ttot) {
+  __shared__ uint32_t sk[kPackTile];  // key << 8 | local index, sorted
+  __shared__ uint64_t so[kPackTile];  // owned slots -> slots with padding
+  __shared__ uint32_t sl[kPackTile];  // first slot within the tile
+  const uint32_t j = threadIdx.x;
+  const uint64_t q0 = (uint64_t)blockIdx.x * kPackTile;
+  const uint32_t n = (uint32_t)min<uint64_t>(kPackTile, nq - q0);
+  uint32_t key = 0xFFFFu;  // past the tile's queries: last
+  if (j < n) {
+    key = 0u;
+    if (klen) {
+      const uint32_t l = klen[queries[q0 + j]];
+      key = l == kMissing ? 0u : min(l, 0xFFFEu);
+    }
+    so[j] = own[q0 + j];
+  }
+  sk[j] = (key << 8) | j;
+  __syncthreads();
+  for (uint32_t k = 2; k <= kPackTile; k <<= 1) {  // bitonic sort, ascending
+    for (uint32_t h = k >> 1; h > 0; h >>= 1) {
+      const uint32_t x = j ^ h;
+      if (x > j) {
+        const uint32_t a = sk[j], b = sk[x];
+        if (((j & k) == 0) == (a > b)) {
+          sk[j] = b;
+          sk[x] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (j == 0) {
+    uint64_t cur = 0;       // next free slot of the tile
+    bool started = false;   // a query started inside the current wave (not at lane 0)
+    uint32_t last = kPackTile;
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t jj = sk[i] & 0xFFu;
+      const uint64_t L = so[jj];
+      uint32_t p = (uint32_t)(cur & 63u);
+      if (L > 0 && p > 0 && started) {  // a third query would share the wave: pad it
+        so[last] += 64u - p;
+        cur += 64u - p;
         p = 0;
         started = false;
       }
-      if (last != ~0ull) own[last] = lastv;
+      sl[jj] = (uint32_t)cur;
+      if (L == 0) continue;
       started = p > 0;
-      const uint64_t e = p + L;
-      if (e >= 64) started = false;  // the query reaches the next wave: it is that wave's first
-      p = (uint32_t)(e & 63u);
-      last = qb + i;
-      lastv = L;
+      if (p + L >= 64) started = false;  // the query reaches the next wave: it is that wave's first
+      cur += L;
+      last = jj;
     }
+    const uint32_t p = (uint32_t)(cur & 63u);
+    if (p && last < kPackTile) {
+      so[last] += 64u - p;
+      cur += 64u - p;
+    }
+    ttot[blockIdx.x] = cur;
   }
-  if (last != ~0ull) own[last] = lastv + (p ? 64u - p : 0u);
+  __syncthreads();
+  if (j < n) {
+    own[q0 + j] = so[j];
+    loc[q0 + j] = sl[j];
+  }
+}
+
+// oqoff[i] = the tile's first slot + the query's first slot within it; oqoff[nq] = the total
+__global__ void k_opack_fin(const uint32_t* __restrict__ loc, const uint64_t* __restrict__ tbase,
+                            uint64_t nq, uint64_t* __restrict__ oqoff) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nq) oqoff[i] = tbase[i / kPackTile] + loc[i];
+  if (i == 0) oqoff[nq] = tbase[(nq + kPackTile - 1) / kPackTile];
 }
 
 // wave w of k_score_sym2's owner slots -> {query of its first slot, query of its last slot}
-// (one thread per query over the waves whose first / last slot lies in its range)
-__global__ void k_wavemap2(const uint64_t* __restrict__ qoff, uint64_t nq, uint2* __restrict__ wq2) {
+// (one thread per query over the waves whose first / last slot lies in its range
+// [qoff[i], qoff[i] + occ[i]))
+__global__ void k_wavemap2(const uint64_t* __restrict__ qoff, const uint64_t* __restrict__ occ, uint64_t nq,
+                           uint2* __restrict__ wq2) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
-  const uint64_t a = qoff[i], e = qoff[i + 1];
+  const uint64_t a = qoff[i], e = a + occ[i];
   for (uint64_t w = (a + 63) >> 6, we = (e + 63) >> 6; w < we; ++w) wq2[w].x = (uint32_t)i;
   for (uint64_t w = a >> 6, we = e >> 6; w < we; ++w) wq2[w].y = (uint32_t)i;
 }
@@ -2629,15 +2684,25 @@ hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipSt
   return hipGetLastError();
 }
 
-hipError_t launch_opack(uint64_t* own, uint64_t nq, hipStream_t s) {
+uint64_t opack_tiles(uint64_t nq) { return (nq + kPackTile - 1) / kPackTile; }
+
+hipError_t launch_opack(uint64_t* own, uint64_t nq, const uint32_t* queries, const uint16_t* klen,
+                        uint32_t* loc, uint64_t* ttot, hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_opack<<<grid1d((nq + kPackTile - 1) / kPackTile), 256, 0, s>>>(own, nq);
+  k_opack<<<(unsigned)opack_tiles(nq), kPackTile, 0, s>>>(own, nq, queries, klen, loc, ttot);
   return hipGetLastError();
 }
 
-hipError_t launch_wavemap2(const uint64_t* qoff, uint64_t nq, uint2* wq2, hipStream_t s) {
+hipError_t launch_opack_fin(const uint32_t* loc, const uint64_t* tbase, uint64_t nq, uint64_t* oqoff,
+                            hipStream_t s) {
   DK_LAUNCH_GUARD(nq);
-  k_wavemap2<<<grid1d(nq), 256, 0, s>>>(qoff, nq, wq2);
+  k_opack_fin<<<grid1d(nq), 256, 0, s>>>(loc, tbase, nq, oqoff);
+  return hipGetLastError();
+}
+
+hipError_t launch_wavemap2(const uint64_t* qoff, const uint64_t* occ, uint64_t nq, uint2* wq2, hipStream_t s) {
+  DK_LAUNCH_GUARD(nq);
+  k_wavemap2<<<grid1d(nq), 256, 0, s>>>(qoff, occ, nq, wq2);
   return hipGetLastError();
 }
 

@@ -311,7 +311,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
       if (lq != kMissing && m1 > 0 && sd != kGramSeedNone) {
         uint32_t* tab = tabs + ts * kTabWords;
         const uint32_t mult = gram_mult(sd & 0xFFu);
-        const int sh = 24 - (int)(sd >> 8);  // 32 - lt
+        const int sh = 32 - kGramLtMin - (int)(sd >> 8);  // 32 - lt
         if (lane == 0) tab[0] = ~0u;  // a real key landing in slot 0 overwrites the sentinel
         if ((int)lane < m1) {
           const uint32_t key = gram_key(D.grams[D.goff[q] + lane]);
@@ -388,7 +388,7 @@ void k_score_grouped(const ScoreParams P, const PairSource S, uint64_t slot0, ui
           // formula is exactly 1.0
           const uint32_t* tab = tabs + tslot * kTabWords;
           const uint32_t mult = gram_mult(sd & 0xFFu);
-          const int sh = 24 - (int)(sd >> 8);
+          const int sh = 32 - kGramLtMin - (int)(sd >> 8);
           int common = 0;
 #pragma unroll
           for (int j = 0; j < kPreRows; ++j)
@@ -661,7 +661,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
       uint16_t* tab = tabs + a * kTabWords;
       const DevProp& D = P.props[A->q[a].prop];
       const uint32_t mult = gram_mult(sd & 0xFFu);
-      const int sh = 24 - (int)(sd >> 8);
+      const int sh = 32 - kGramLtMin - (int)(sd >> 8);
       // the sentinel: the smallest key in 1..64 whose slot is not 0
       const uint64_t off0 = __ballot(((uint32_t)__umul24(lane + 1u, mult) >> sh) != 0u);
       if (off0 == 0ull) {
@@ -711,7 +711,7 @@ void k_score_gq(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_
     constexpr int a = decltype(ic)::value;
     const uint16_t* tab = tabs + a * kTabWords;
     const uint32_t mult = gram_mult(sdv & 0xFFu);
-    const int sh = 24 - (int)(sdv >> 8);  // 32 - lt
+    const int sh = 32 - kGramLtMin - (int)(sdv >> 8);  // 32 - lt
     int common = 0;
 #pragma unroll
     for (int j = 0; j < GQRows<a>::v; ++j)

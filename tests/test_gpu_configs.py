@@ -664,7 +664,8 @@ def test_sym2_two_queries_per_wave(seed, monkeypatch):
     """k_score_sym2 (owner slots padded to 32, a query per half-wave) bit-exact against the
     oracle, against one query per wave (DK_SYM2=0), against the direct schedule (DK_SYM=0) and
     with the bucket lookup index of large batches (DK_SYMIDX=1: SymIndex instead of binary
-    searches), with superseded and deleted rows, a delta segment, one chunk and many."""
+    searches), with the owner slots in query order instead of by length within each tile
+    (DK_SYM_ORDER=0), with superseded and deleted rows, a delta segment, one chunk and many."""
     props, vals, keys = sym2_case(seed)
     n = len(vals[0])
     rng = np.random.default_rng(seed)
@@ -684,7 +685,7 @@ def test_sym2_two_queries_per_wave(seed, monkeypatch):
                 monkeypatch.setenv("DK_CHUNK_SLOTS", chunk)
             else:
                 monkeypatch.delenv("DK_CHUNK_SLOTS", raising=False)
-            for env in ({}, {"DK_SYM2": "0"}, {"DK_SYM": "0"}, {"DK_SYMIDX": "1"}):
+            for env in ({}, {"DK_SYM2": "0"}, {"DK_SYM": "0"}, {"DK_SYMIDX": "1"}, {"DK_SYM_ORDER": "0"}):
                 for k, v in env.items():
                     monkeypatch.setenv(k, v)
                 eng.reset_profile()
