@@ -564,6 +564,7 @@ struct dk_ctx {
   DevBuf raised;           // k_score_geo: a compared GeopositionComparator value without ','
   PinnedBuf h_raised;
   PinnedBuf h_bounds;
+  PinnedBuf h_pbase;  // k_opack's tile offsets, read back with the schedule's totals
   DevBuf counters;
   struct StageBufs { DevBuf bcnt, bscored, bbytes, boff, prob, cand, qidx, bexact; };
   StageBufs stage[2];                          // double-buffered per-chunk staging
@@ -2604,6 +2605,8 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
         return exclusive_scan_u64(t, b, c->ptot.as<uint64_t>(), c->pbase.as<uint64_t>(), nt + 1, s);
       }));
       HIPCHK(launch_opack_fin(c->ploc.as<uint32_t>(), c->pbase.as<uint64_t>(), nq, c->oqoff.as<uint64_t>(), s));
+      HIPCHK(c->h_pbase.reserve((nt + 1) * 8));  // the chunks' owner slots without a second round trip
+      HIPCHK(hipMemcpyAsync(c->h_pbase.p, c->pbase.p, (nt + 1) * 8, hipMemcpyDeviceToHost, s));
     } else {
       HIPCHK(with_tmp(c, [&](void* t, size_t& b) {
         return exclusive_scan_u64(t, b, c->ocounts.as<uint64_t>(), c->oqoff.as<uint64_t>(), nq + 1, s);
@@ -2651,17 +2654,21 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
     // would be the previous query's inclusive prefix
     qb.erase(std::unique(qb.begin(), qb.end()), qb.end());
     const uint64_t nb = qb.size();
-    HIPCHK(c->bidx.reserve(nb * 8 + 8, 0, s));
-    HIPCHK(c->bval.reserve(nb * 8 + 8, 0, s));
-    HIPCHK(c->h_bounds.reserve(nb * 8 + 8));
-    uint64_t* hb = c->h_bounds.as<uint64_t>();
-    for (uint64_t i = 0; i < nb; ++i) hb[i] = two ? (qb[i] + qg - 1) / qg : qb[i];  // tile / query
-    HIPCHK(hipMemcpyAsync(c->bidx.p, hb, nb * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(launch_gather_u64(two ? c->pbase.as<uint64_t>() : c->oqoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb,
-                             c->bval.as<uint64_t>(), s));
-    HIPCHK(hipMemcpyAsync(hb, c->bval.p, nb * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    obounds.assign(hb, hb + nb);
+    if (two) {  // tile offsets (read back above)
+      const uint64_t* tb = c->h_pbase.as<uint64_t>();
+      for (uint64_t i = 0; i < nb; ++i) obounds.push_back(tb[(qb[i] + qg - 1) / qg]);
+    } else {
+      HIPCHK(c->bidx.reserve(nb * 8 + 8, 0, s));
+      HIPCHK(c->bval.reserve(nb * 8 + 8, 0, s));
+      HIPCHK(c->h_bounds.reserve(nb * 8 + 8));
+      uint64_t* hb = c->h_bounds.as<uint64_t>();
+      memcpy(hb, qb.data(), nb * 8);
+      HIPCHK(hipMemcpyAsync(c->bidx.p, hb, nb * 8, hipMemcpyHostToDevice, s));
+      HIPCHK(launch_gather_u64(c->oqoff.as<uint64_t>(), c->bidx.as<uint64_t>(), nb, c->bval.as<uint64_t>(), s));
+      HIPCHK(hipMemcpyAsync(hb, c->bval.p, nb * 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      obounds.assign(hb, hb + nb);
+    }
     // a half holds the chunk's slots from the wave of its first one (k_score_sym2's chunks
     // start inside a wave), plus 64 B the count pass's 16-B reads may touch past the end:
     // slot s of chunk ci at half + s - (obounds[ci] & ~63), 16-B aligned like s

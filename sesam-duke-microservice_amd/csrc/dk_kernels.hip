@@ -1645,43 +1645,48 @@ struct EmitSeg {
   uint32_t lo, qa, pq, pad;
 };
 
-// The count pass: one thread per query counts the non-zero decision bytes of its owner
-// slots [oqoff[qi], oqoff[qi + 1]) (padding slots hold 0) and of its mirror slots
-// [mqoff[qi], mqoff[qi + 1]) -- both contiguous runs, read 16 bytes at a time, four loads in
-// flight -- instead of walking the candidate order (a wave per query was latency bound).
+// The count pass: kCountLanes threads per query count the non-zero decision bytes of its
+// owner slots [oqoff[qi], + ocnt[qi]) (padding slots hold 0) and of its mirror slots
+// [mqoff[qi], mqoff[qi + 1]) -- both contiguous runs, read 16 bytes per thread and step --
+// instead of walking the candidate order (a wave per query was latency bound; a thread per
+// query left a chunk's launch a few waves per CU).
+constexpr int kCountLanes = 8;
+
 __device__ __forceinline__ uint32_t nz_bytes(uint32_t x) {  // decision bytes are 0, 1 or 2
   return (uint32_t)__popc((x | (x >> 1)) & 0x01010101u);
 }
 
-__device__ __forceinline__ uint32_t nz_run(const uint8_t* base, uint64_t a, uint64_t e) {
+// this thread's share (16-B blocks k, k + kCountLanes, ...) of the run [a, e) of base
+__device__ __forceinline__ uint32_t nz_run(const uint8_t* base, uint64_t a, uint64_t e, uint32_t k) {
   uint32_t n = 0;
-  for (uint64_t p = a & ~(uint64_t)15; p < e; p += 64) {
-    uint4 v[4];
+  for (uint64_t p = (a & ~(uint64_t)15) + 16u * k; p < e; p += 16u * kCountLanes) {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      v[i] = p + 16 * i < e ? *reinterpret_cast<const uint4*>(base + p + 16 * i) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint64_t b0 = p + 16 * i + 4 * j;  // bytes [b0, b0 + 4) of the run's buffer
-        uint32_t x = w[j];
-        if (b0 < a) x = a - b0 >= 4 ? 0u : x & (~0u << (8 * (a - b0)));
-        if (b0 + 4 > e) x = b0 >= e ? 0u : x & (~0u >> (8 * (b0 + 4 - e)));
-        n += nz_bytes(x);
-      }
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t b0 = p + 4 * j;  // bytes [b0, b0 + 4) of the run's buffer
+      uint32_t x = w[j];
+      if (b0 < a) x = a - b0 >= 4 ? 0u : x & (~0u << (8 * (a - b0)));
+      if (b0 + 4 > e) x = b0 >= e ? 0u : x & (~0u >> (8 * (b0 + 4 - e)));
+      n += nz_bytes(x);
     }
   }
   return n;
 }
 
 __global__ __launch_bounds__(256) void k_sym_count(const EmitSource S, uint64_t q0, uint64_t nqc) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nqc) return;
-  const uint64_t qi = q0 + i;
-  const uint64_t oa = S.oqoff[qi], oe = S.ocnt ? oa + S.ocnt[qi] : S.oqoff[qi + 1];
-  S.ecount[qi] = nz_run(S.okind, oa, oe) + nz_run(S.mkind, S.mqoff[qi], S.mqoff[qi + 1]);
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = t / kCountLanes;
+  const uint32_t k = (uint32_t)(t % kCountLanes);
+  uint32_t n = 0;
+  const uint64_t qi = q0 + min(i, nqc - 1);
+  if (i < nqc) {
+    const uint64_t oa = S.oqoff[qi], oe = S.ocnt ? oa + S.ocnt[qi] : S.oqoff[qi + 1];
+    n = nz_run(S.okind, oa, oe, k) + nz_run(S.mkind, S.mqoff[qi], S.mqoff[qi + 1], k);
+  }
+#pragma unroll
+  for (int o = kCountLanes / 2; o > 0; o >>= 1) n += __shfl_xor(n, o, kCountLanes);
+  if (i < nqc && k == 0) S.ecount[qi] = n;
 }
 
 template <bool WRITE>
@@ -2756,7 +2761,7 @@ hipError_t launch_sym_emit(const EmitSource& src, uint64_t q0, uint64_t nqc, boo
   DK_LAUNCH_GUARD(nqc);
   const unsigned grid = grid1d(nqc, kScoreBlock / 64);
   if (write) k_sym_emit<true><<<grid, kScoreBlock, 0, s>>>(src, q0, nqc, base, out, first);
-  else k_sym_count<<<grid1d(nqc), 256, 0, s>>>(src, q0, nqc);
+  else k_sym_count<<<grid1d(nqc * kCountLanes), 256, 0, s>>>(src, q0, nqc);
   return hipGetLastError();
 }
 
