@@ -77,6 +77,9 @@ def parse():
                          "(rank 0 reads the node list in place: SURVEY §8d's result gather); "
                          "rccl = device lists gathered to GPU 0 over xGMI; none = each rank's "
                          "list stays in its HBM, only the per-rank counts are all-gathered")
+    ap.add_argument("--phase-steps", type=int, default=3,
+                    help="untimed steps after the timed region that give phases_ms_per_step "
+                         "(0: take the phases from the timed region, with every phase's events in it)")
     ap.add_argument("--pcie-steps", type=int, default=3,
                     help="N=1: extra steps with the match list copied to pinned host memory "
                          "(the PCIe-inclusive rate, reported beside `value`; 0 = skip)")
@@ -497,7 +500,10 @@ def main():
         else:
             step()
     eng.reset_profile()
-    eng.set_profiling(True)
+    # the timed region records HIP events around the scoring kernels only (the roofline's
+    # launch times); the phase split comes from its own untimed pass (--phase-steps), since
+    # each phase's two events cost the stream a few microseconds between dependent kernels
+    eng.set_profiling(2 if args.phase_steps > 0 else True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -513,6 +519,16 @@ def main():
     el = time.perf_counter() - t
     eng.set_profiling(False)
     prof = eng.profile()
+    prof_ph, nph = prof, args.steps
+    if args.phase_steps > 0:
+        nph = args.phase_steps
+        eng.reset_profile()
+        eng.set_profiling(True)
+        for _ in range(nph):
+            last, _ = step()
+        torch.cuda.synchronize()
+        eng.set_profiling(False)
+        prof_ph = eng.profile()
     if dist is not None:
         tt = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -648,7 +664,7 @@ def main():
             "entries_per_query": ((sum(c[0] for c in shared.counts) if shared is not None
                                    else sum(c[0] for c in holder["counts"]) if "counts" in holder
                                    else int(last.n) if last is not None else 0) / max(1, len(allq))),
-            "list_ms_per_step": prof["ms_gather"] / args.steps,
+            "list_ms_per_step": prof_ph["ms_gather"] / nph,
             # k_score_gq: the scored pairs its single-precision screen sent to the exact pass
             "exact_pass_fraction": (prof["pairs_exact"] / prof["pairs_scored"]
                                     if prof.get("pairs_exact") and prof["pairs_scored"] else None),
@@ -685,9 +701,11 @@ def main():
             # per-rank pairs scored of the last step (tile balance; N>1)
             "rank_pairs": ([c[1] for c in holder["counts"]] if "counts" in holder else
                            [c[1] for c in shared.counts] if shared is not None and shared.counts else None),
-            "phases_ms_per_step": {k: prof[k] / args.steps for k in
+            # device time per phase, from the untimed phase pass (phase_steps steps)
+            "phases_ms_per_step": {k: prof_ph[k] / nph for k in
                                    ("ms_index", "ms_generate", "ms_score", "ms_emit", "ms_gather", "ms_copy",
                                     "ms_total")},
+            "phase_steps": nph,
         }
         if world == 1 and args.cpu_seconds > 0:
             if last is None or last.on_device:

@@ -301,6 +301,8 @@ uint64_t dk_num_rows(const dk_ctx* ctx);
 /* IncrementalLuceneDatabase.findRecordById: the row of the live version of a record ID
  * (dk_batch.ident numbering); DK_E_INVALID when none is indexed */
 int dk_row_of_ident(const dk_ctx* ctx, uint64_t ident, uint32_t* row);
+/* on: 0 off, 1 every phase's device time (dk_profile.ms_*), 2 the scoring kernels only
+ * (ms_score: no events between the other phases' dependent kernels) */
 int dk_set_profiling(dk_ctx* ctx, int on);
 int dk_get_profile(const dk_ctx* ctx, dk_profile* out);
 int dk_reset_profile(dk_ctx* ctx);

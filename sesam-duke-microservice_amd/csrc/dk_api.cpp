@@ -589,7 +589,7 @@ struct dk_ctx {
     uint8_t* kind = nullptr;
   } region;
   // profiling (Processor.setPerformanceProfiling)
-  bool profiling = false;
+  int profiling = 0;  // 0 off, 1 every phase, 2 the scoring kernels only
   dk_profile prof{};
   // Lucene-compatible candidate source (dk_schema.lucene): per lookup field a term
   // dictionary; per row its query clauses (host offsets + device copy) and length norms;
@@ -829,8 +829,9 @@ int dk_row_of_ident(const dk_ctx* c, uint64_t ident, uint32_t* row) {
 
 int dk_set_profiling(dk_ctx* c, int on) {
   if (!c) return fail(DK_E_INVALID, "ctx is NULL");
-  c->profiling = on != 0;
-  for (dk_ctx* m : c->members) m->profiling = on != 0;
+  const int lv = on == 2 ? 2 : (on != 0 ? 1 : 0);  // 2: the scoring kernels' spans only
+  c->profiling = lv;
+  for (dk_ctx* m : c->members) m->profiling = lv;
   return DK_OK;
 }
 
@@ -1710,7 +1711,9 @@ static hipEvent_t pooled_event(dk_ctx* c) {
 }
 
 Timer::Timer(dk_ctx* ctx, double* target, hipStream_t st) : c(ctx), acc(target), s(st) {
-  if (!c->profiling) return;
+  // level 2: only the scoring kernels' launches (each span's two events cost the stream a
+  // few microseconds between dependent kernels)
+  if (!c->profiling || (c->profiling == 2 && target != &c->prof.ms_score)) return;
   a = pooled_event(c);
   if (a) (void)hipEventRecord(a, s);
 }

@@ -255,7 +255,8 @@ class GpuEngine:
         return out.value
 
     def set_profiling(self, on):
-        A.check(self.lib.dk_set_profiling(self.ctx, 1 if on else 0))
+        """on: False / True (every phase), or 2 (the scoring kernels only)."""
+        A.check(self.lib.dk_set_profiling(self.ctx, 2 if on == 2 and on is not True else (1 if on else 0)))
 
     def profile(self):
         p = A.dk_profile()
