@@ -559,7 +559,7 @@ struct dk_ctx {
   DevBuf ocounts, oqoff, owq, obase, okind, ores, mcounts, mqoff, mbase, mkind, mres, ecount, eincl, bidx, bval;
   DevBuf ploc, ptot, pbase;  // k_opack: first slot within the tile, tile slots, their scan
   // k_count_sym's bucket lookup for large batches (SymIndex), built once per table build
-  DevBuf sx_posof, sx_hflag, sx_bstart, sx_bend, sx_tmp;
+  DevBuf sx_posof, sx_hflag, sx_bstart, sx_bend, sx_bse, sx_tmp;
   uint64_t sx_gen = 0;
   DevBuf raised;           // k_score_geo: a compared GeopositionComparator value without ','
   PinnedBuf h_raised;
@@ -2567,11 +2567,14 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       HIPCHK(c->sx_bend.reserve(P.rstride * 4 + 4, 0, s));
       HIPCHK(c->sx_tmp.reserve(tb + 16, 0, s));
       HIPCHK(hipMemsetAsync(c->sx_posof.p, 0xFF, (uint64_t)T.nseg * c->nrows * 4, s));
+      HIPCHK(c->sx_bse.reserve(P.rstride * 8 + 8, 0, s));
       HIPCHK(launch_symidx(T, c->nrows, c->sx_posof.as<uint32_t>(), c->sx_hflag.as<uint32_t>(),
-                           c->sx_bstart.as<uint32_t>(), c->sx_bend.as<uint32_t>(), c->sx_tmp.p, tb, s));
+                           c->sx_bstart.as<uint32_t>(), c->sx_bend.as<uint32_t>(), c->sx_bse.as<uint2>(), c->sx_tmp.p,
+                           tb, s));
       c->sx_gen = c->tables_gen;
     }
-    sx = SymIndex{c->sx_posof.as<uint32_t>(), c->sx_bstart.as<uint32_t>(), c->sx_bend.as<uint32_t>(), c->nrows};
+    sx = SymIndex{c->sx_posof.as<uint32_t>(), c->sx_bstart.as<uint32_t>(), c->sx_bend.as<uint32_t>(), c->nrows,
+                  c->sx_bse.as<uint2>()};
   }
   if (sym) {
     HIPCHK(c->ranges.reserve((uint64_t)T.nseg * nq * 16 + 16, 0, s));
@@ -2595,7 +2598,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
       return exclusive_scan_u64(t, b, c->counts.as<uint64_t>(), c->qoff.as<uint64_t>(), nq + 1, s);
     }));
     if (two) {
-      // waves of at most two queries, per tile of 256 queries (in the order of their length
+      // waves of at most two queries, per tile of kPackTile queries (in the order of their length
       // on the longest Levenshtein property; DK_SYM_ORDER=0: query order)
       const uint64_t nt = opack_tiles(nq);
       HIPCHK(c->ploc.reserve(nq * 4 + 4, 0, s));
@@ -2641,7 +2644,7 @@ static int run_match(dk_ctx* c, const uint32_t* query_rows, uint64_t nq, int fla
   uint64_t ochunk = 1;
   if (sym) {
     // k_score_sym2's chunks are whole tiles of k_opack (its queries are ordered per tile)
-    const uint64_t qg = two ? 256 : 1;
+    const uint64_t qg = two ? (uint64_t)kPackTile : 1;
     auto qcut = [&](uint64_t x) { return std::min(nq, (x + qg / 2) / qg * qg); };
     qb.push_back(0);
     const uint64_t nch = std::max<uint64_t>(1, (total + chunk_len(total) - 1) / chunk_len(total));

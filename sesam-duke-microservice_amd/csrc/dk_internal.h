@@ -475,11 +475,12 @@ hipError_t launch_count_exact(const uint32_t* queries, uint64_t nq, const BlockT
                               uint2* ranges, uint64_t* counts, hipStream_t s);
 // wq[w] = qi for every group w of 2^shift slots of query qi (qoff in multiples of 2^shift)
 hipError_t launch_wavemap(const uint64_t* qoff, uint64_t nq, uint32_t* wq, hipStream_t s, int shift = 6);
-// k_score_sym2's owner slots, per tile of 256 queries (k_opack): own[i] (owned candidates)
+// k_score_sym2's owner slots, per tile of kPackTile queries (k_opack): own[i] (owned candidates)
 // -> the query's slots with the padding that keeps every wave to two queries, loc[i] its
 // first slot within the tile (queries ordered by klen[queries[i]] when klen is given),
 // ttot[t] the tile's slots; oqoff[i] = tbase[tile] + loc[i] with tbase the exclusive scan
 // of ttot (k_opack_fin); wq2[w] = {query of wave w's first slot, query of its last slot}
+constexpr int kPackTile = 64;  // queries per k_opack tile (one wave walks it)
 uint64_t opack_tiles(uint64_t nq);
 hipError_t launch_opack(uint64_t* own, uint64_t nq, const uint32_t* queries, const uint16_t* klen,
                         uint32_t* loc, uint64_t* ttot, hipStream_t s);
@@ -515,6 +516,7 @@ struct SymIndex {
   const uint32_t* bstart;  // [replica position]: its bucket's first position (segment-relative)
   const uint32_t* bend;    // [replica position of a bucket's first entry]: the bucket's end
   uint64_t nrows;
+  const uint2* bse;        // [replica position]: {its bucket's first position, end} in one load
 };
 hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTables& T, uint32_t r0,
                             uint4* sranges, uint64_t* counts, uint64_t* ocounts, uint64_t* mcounts,
@@ -522,7 +524,7 @@ hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTab
 // builds SymIndex over every segment of T (hflag: scratch of one u32 per replica position;
 // tmp: symidx_scan_bytes of the longest segment)
 hipError_t launch_symidx(const BlockTables& T, uint64_t nrows, uint32_t* posof, uint32_t* hflag,
-                         uint32_t* bstart, uint32_t* bend, void* tmp, size_t tmp_bytes, hipStream_t s);
+                         uint32_t* bstart, uint32_t* bend, uint2* bse, void* tmp, size_t tmp_bytes, hipStream_t s);
 hipError_t symidx_scan_bytes(uint64_t n, size_t* bytes);
 hipError_t launch_obase(const uint4* sranges, const uint64_t* oqoff, const uint64_t* mqoff,
                         uint64_t nq, int nseg, uint64_t* obase, uint64_t* mbase, hipStream_t s);

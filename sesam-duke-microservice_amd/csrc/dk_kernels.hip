@@ -2135,6 +2135,16 @@ __global__ void k_symidx_end(const BlockTables T, int k, const uint32_t* __restr
   if (i + 1 == n || T.skeys[k][i + 1] != T.skeys[k][i]) bend[off + bstart[off + i]] = (uint32_t)(i + 1);
 }
 
+// per position {bucket start, bucket end}: k_count_sym's bucket in one load
+__global__ void k_symidx_pair(const BlockTables T, int k, const uint32_t* __restrict__ bstart,
+                              const uint32_t* __restrict__ bend, uint2* __restrict__ bse) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T.seg_len[k]) return;
+  const uint64_t off = T.seg_off[k];
+  const uint32_t b = bstart[off + i];
+  bse[off + i] = make_uint2(b, bend[off + b]);
+}
+
 __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, const BlockTables T,
                             uint32_t r0, uint4* __restrict__ sranges, uint64_t* __restrict__ counts,
                             uint64_t* __restrict__ ocounts, uint64_t* __restrict__ mcounts,
@@ -2147,11 +2157,15 @@ __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, c
       const uint32_t* rows = T.rowof + T.seg_off[k];
       const uint32_t px = X.posof ? X.posof[(uint64_t)k * X.nrows + q] : kNoPos;
       uint64_t lo, hi, qa, p;
+      bool self = false;  // rows[p] == q is known (posof)
       if (px != kNoPos) {  // the query's own entry: its bucket from the index
-        lo = X.bstart[T.seg_off[k] + px];
-        hi = X.bend[T.seg_off[k] + lo];
-        qa = rows[lo] >= r0 ? lo : lower_bound_u32(rows, lo, hi, r0);
+        const uint2 be = X.bse[T.seg_off[k] + px];
+        lo = be.x;
+        hi = be.y;
+        // (r0 == 0: every row of the bucket is a batch row -- no load)
+        qa = r0 == 0 || rows[lo] >= r0 ? lo : lower_bound_u32(rows, lo, hi, r0);
         p = px;
+        self = true;
       } else {
         const uint64_t key = T.keys[k >> T.seg_shift][q];
         lo = lower_bound_u64(T.skeys[k], T.seg_len[k], key);
@@ -2161,7 +2175,7 @@ __global__ void k_count_sym(const uint32_t* __restrict__ queries, uint64_t nq, c
       }
       // a superseded base entry is no candidate, so its query is not "in" the segment
       // either: it owns its whole bucket and expects no mirrored results
-      const bool in_t = p < hi && rows[p] == q && T.rident[T.seg_off[k] + p] != kDeadIdent;
+      const bool in_t = p < hi && (self || rows[p] == q) && T.rident[T.seg_off[k] + p] != kDeadIdent;
       const uint32_t qa_eff = in_t ? (uint32_t)qa : (uint32_t)hi;
       sranges[(uint64_t)k * nq + i] =
           make_uint4((uint32_t)lo, (uint32_t)hi, qa_eff, in_t ? (uint32_t)p : kNoPos);
@@ -2228,7 +2242,6 @@ __global__ void k_wavemap(const uint64_t* __restrict__ qoff, uint64_t nq, uint32
 // becomes its slots with trailing padding, loc[i] its first slot within the tile, ttot[t]
 // the tile's slots.  Padding is ~2 % of the slots, against ~7 % with every query padded to
 // a half-wave.
-constexpr int kPackTile = 256;
 
 __global__ __launch_bounds__(kPackTile) void k_opack(uint64_t* __restrict__ own, uint64_t nq,
                                                      const uint32_t* __restrict__ queries,
@@ -2730,7 +2743,7 @@ hipError_t launch_count_sym(const uint32_t* queries, uint64_t nq, const BlockTab
 }
 
 hipError_t launch_symidx(const BlockTables& T, uint64_t nrows, uint32_t* posof, uint32_t* hflag,
-                         uint32_t* bstart, uint32_t* bend, void* tmp, size_t tmp_bytes, hipStream_t s) {
+                         uint32_t* bstart, uint32_t* bend, uint2* bse, void* tmp, size_t tmp_bytes, hipStream_t s) {
   for (int k = 0; k < T.nseg; ++k) {
     const uint64_t n = T.seg_len[k];
     if (!n) continue;
@@ -2740,6 +2753,7 @@ hipError_t launch_symidx(const BlockTables& T, uint64_t nrows, uint32_t* posof, 
                                            rocprim::maximum<uint32_t>(), s);
     if (e != hipSuccess) return e;
     k_symidx_end<<<grid1d(n), 256, 0, s>>>(T, k, bstart, bend);
+    k_symidx_pair<<<grid1d(n), 256, 0, s>>>(T, k, bstart, bend, bse);
   }
   return hipGetLastError();
 }
