@@ -24,7 +24,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 KERNELS = {  # bench.py roofline pmc_key -> (the kernel its launches use, loop region priced)
     # "inner": the innermost loop bodies (the DP kernels' cell loops); "outer": the largest
     # loop body (k_score_gq's per-group loop, whose inner loops are rare tails)
-    "dedup": ("_ZN2dk7k_scoreILi40ELb1ELb0E", "inner"),  # GR = false: no gram-set code
+    "dedup": ("_ZN2dk12k_score_sym2ILi40E", "inner"),  # two queries per wave (k_score_sym2)
     "dedup_utf16": ("_ZN2dk7k_scoreILi40ELb1ELb0E", "inner"),
     "linkage": ("_ZN2dk10k_score_gqILi2ELi2ELi0E", "outer"),   # role 0 deferred (the build's default)
     "allpairs_lev": ("_ZN2dk7k_scoreILi16ELb0ELb0E", "inner"),
