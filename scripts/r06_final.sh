@@ -24,7 +24,7 @@ for what in "$@"; do
     dedup) run dedup --workload dedup --steps 20 --warmup 5 ;;
     dedup_utf16) run dedup_utf16 --workload dedup --utf16-frac 0.01 --steps 10 ;;
     linkage) run linkage --workload linkage --steps 20 --warmup 5 ;;
-    linkage_10m) run linkage_10m --workload linkage --records 20000000 --steps 3 --warmup 1 --pcie-steps 0 ;;
+    linkage_10m) run linkage_10m --workload linkage --records 10000000 --steps 3 --warmup 1 --pcie-steps 0 ;;
     allpairs_lev) run allpairs_lev --workload allpairs --comparator lev --steps 3 ;;
     allpairs_jw) run allpairs_jw --workload allpairs --comparator jw --steps 3 ;;
     longtext) run longtext --workload longtext --steps 5 ;;

@@ -20,6 +20,8 @@ for spec in "$@"; do
     --no-json-batch > $OUT/$name/trace_bench.json 2> $OUT/$name/trace_bench.err
   KREGEX="k_score" bash scripts/pmc_profile.sh $OUT/$name/pmc $args --steps 1 --warmup 0 --cpu-seconds 0 --cpu-single-seconds 0 \
     --no-warm-batch --pcie-steps 0 --no-json-batch --phase-steps 0
+  rm -f $OUT/$name/trace/*kernel_trace.csv  # the stats and counters are what is kept (gpurun_out <= 64 MiB)
+  du -sh $OUT/$name
   echo "$name done"
 done
 echo done
