@@ -1971,10 +1971,13 @@ __global__ __launch_bounds__(256) void k_gram_seed(const uint64_t* __restrict__ 
     for (int k = 0; k < m; ++k) zero = zero || gram_key(g[k]) == 0u;
     // the smallest table first: a probe's LDS bank conflicts grow with the table's words per
     // bank (none at 64 16-bit slots, scripts/micro/lds_probe.hip); m <= kGramPerfectMax = 64
+    // (the smaller sizes get a few tries each: a failed try stops at its first collision, but
+    // an upsert seeds every row)
     const int lt_hi = m <= 32 ? 8 : 9;
     for (int lt = lt_hi - 2; lt <= lt_hi && out == kGramSeedNone && !zero; ++lt) {
       const int words = 1 << (lt - 5);
-      for (int t = 0; t < kGramSeedTries; ++t) {
+      const int tries = lt == lt_hi ? kGramSeedTries : (lt == lt_hi - 1 ? 32 : 16);
+      for (int t = 0; t < tries; ++t) {
         const uint32_t mult = gram_mult((uint32_t)t);
         // k_score_gq's slot-0 sentinel is a key in 1..64 whose slot is not 0
         if (((64u * mult) >> (32 - lt)) == 0u) continue;
