@@ -19,6 +19,9 @@
 #include "dk_internal.h"
 #include "dk_device.h"
 
+#ifndef DK_WAVES_COUNT
+#define DK_WAVES_COUNT 1  // k_sym_count occupancy floor (A/B)
+#endif
 #define DK_JW_NARROW 32  // JaroWinkler on 32-bit position masks up to this query length (kPeqNarrow)
 #ifndef DK_WAVES_SHORT
 #define DK_WAVES_SHORT 5  // k_score waves per SIMD up to 40 Levenshtein rows
@@ -1637,7 +1640,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_LO
 // ecount[qi] on, with their candidate rows and probabilities, and first[qi] (the chunk's
 // last query first[qi + 1] too).  No staging, no compaction and no per-entry query index:
 // the list is written where it ends up.
-constexpr int kEmitBatch = 8;
+#ifndef DK_EMIT_BATCH
+#define DK_EMIT_BATCH 8
+#endif
+constexpr int kEmitBatch = DK_EMIT_BATCH;
 
 struct EmitSeg {
   uint64_t start;       // first index of the segment in the query's candidate order
@@ -1674,7 +1680,7 @@ __device__ __forceinline__ uint32_t nz_run(const uint8_t* base, uint64_t a, uint
   return n;
 }
 
-__global__ __launch_bounds__(256) void k_sym_count(const EmitSource S, uint64_t q0, uint64_t nqc) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_COUNT, 8))) void k_sym_count(const EmitSource S, uint64_t q0, uint64_t nqc) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i = t / kCountLanes;
   const uint32_t k = (uint32_t)(t % kCountLanes);
@@ -1689,8 +1695,13 @@ __global__ __launch_bounds__(256) void k_sym_count(const EmitSource S, uint64_t 
   if (i < nqc && k == 0) S.ecount[qi] = n;
 }
 
+// the write pass is latency bound: 8 waves per SIMD (<= 64 VGPRs) rather than the 6 its
+// registers would give (configs[1] write pass 2.19 -> 1.68 ms per step)
+#ifndef DK_WAVES_EMIT
+#define DK_WAVES_EMIT 8
+#endif
 template <bool WRITE>
-__global__ __launch_bounds__(256) void k_sym_emit(const EmitSource S, uint64_t q0, uint64_t nqc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DK_WAVES_EMIT, 8))) void k_sym_emit(const EmitSource S, uint64_t q0, uint64_t nqc,
                                                   uint64_t base, MatchList out,
                                                   uint64_t* __restrict__ first) {
   __shared__ EmitSeg seg[kScoreBlock / 64][kMaxSegs];
