@@ -23,6 +23,9 @@
 #define DK_WAVES_COUNT 1  // k_sym_count occupancy floor (A/B)
 #endif
 #define DK_JW_NARROW 32  // JaroWinkler on 32-bit position masks up to this query length (kPeqNarrow)
+#ifndef DK_WAVES_SYM2
+#define DK_WAVES_SYM2 7  // k_score_sym2 up to 40 rows (5 / 6 / 7 waves: configs[1] ms_score 23.9 / 23.2 / 22.3)
+#endif
 #ifndef DK_WAVES_SHORT
 #define DK_WAVES_SHORT 5  // k_score waves per SIMD up to 40 Levenshtein rows
 #endif
@@ -1397,7 +1400,7 @@ void k_score(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t n
 // slice (256 entries each), the row bucket covers the longer query value, and the query side
 // of every comparator is per lane (its query); the rest is score_body's SYM path.
 template <int RMAX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? DK_WAVES_SHORT : 4, 8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RMAX <= 40 ? DK_WAVES_SYM2 : 4, 8)))
 void k_score_sym2(const ScoreParams P, const PairSource S, uint64_t slot0, uint64_t nslots, StageOut out) {
   uint64_t* tab = g_wave_tables[threadIdx.x >> 6];
   for (int e = (int)lane_id(); e < kPeqEntries; e += 64) tab[e] = 0;
