@@ -1381,7 +1381,7 @@ __device__ __forceinline__ void score_body(const ScoreParams& P, const PairSourc
 }
 
 // The fused scoring kernel.  Short-value variants pin the occupancy (the DP is
-// latency-bound: 5 waves/SIMD up to 40 rows, 4 above); the long-value variants (LR > 0)
+// latency-bound: 7 waves/SIMD up to 40 rows -- spills and all, measured faster than 5 or 6 -- 4 above); the long-value variants (LR > 0)
 // carry the systolic DP's f64 rows and take what the register allocator needs.
 // GR = false: no QGram / token property (the dedup headline's Levenshtein + JaroWinkler):
 // the gram-set code and its registers are compiled out.
