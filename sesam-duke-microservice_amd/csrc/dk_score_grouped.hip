@@ -475,7 +475,7 @@ hipError_t launch_score_grouped(const ScoreParams& P, const PairSource& src, uin
 //  * The waves of a SIMD (DK_WAVES_GQ) cover that one round trip.
 // =======================================================================================
 #ifndef DK_WAVES_GQ
-#define DK_WAVES_GQ 7  // k_score_gq waves per SIMD (<= 72 VGPRs; 15 KB LDS per 4 waves)
+#define DK_WAVES_GQ 8  // k_score_gq waves per SIMD (<= 64 VGPRs; 15 KB LDS per 4 waves; 7 -> 8: configs[2] 1M ms_score 8.50 -> 8.20)
 #endif
 #ifndef DK_GQ_ABL
 #define DK_GQ_ABL 0  // timing ablations only (wrong results): 1 probes, 2 f64 math, 4 row traffic
